@@ -1,0 +1,262 @@
+// ray_hip.cpp -- C++ host driver over librt_hip.so; the drop-in CLI.
+//
+// Invoked as `ray_serial` / `ray_openmp` (symlinks) it keeps the reference's
+// argv grammar, output file names and stdout lines (src/main.cpp:93-209):
+//   ray_serial [scene]            -> output_serial.ppm, "Serial time: X seconds"
+//   ray_openmp [--openmp] [scene] -> without --openmp: serial pass then OpenMP
+//                                    pass (output_serial.ppm + output_openmp.ppm),
+//                                    with --openmp: only output_openmp.ppm
+// Both passes run on the GPU through the C-ABI: the names keep scripts such as
+// the reference's makefile:48-96 and scripts/test.sh working unchanged.
+// Invoked as `ray_hip` it behaves like the reference's ray_cuda driver
+// (src/main_gpu.cu:357-540): output_gpu.ppm and "GPU rendering time: X seconds".
+//
+// Extra options (defaults equal the reference's hard-coded values,
+// main.cpp:95-97): --width W --height H --depth D, --gpus G (rows sharded over
+// G devices in cyclic 8-row bands, gathered to device 0 with ncclGather over
+// xGMI), --device N, --out FILE, --p6 (binary PPM), --repeat N, --json.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_hip.h"
+
+namespace {
+
+struct Opts {
+  std::string mode = "hip";  // hip | serial | openmp
+  std::string scene = "scenes/simple.txt";
+  bool openmp_only = false;
+  int width = 1280, height = 720, depth = 10;
+  int gpus = 1, device = 0, repeat = 1;
+  std::string out;
+  bool p6 = false, json = false;
+};
+
+int usage(const char *argv0) {
+  std::fprintf(stderr,
+               "usage: %s [--openmp] [--width W] [--height H] [--depth D] [--gpus G] [--device N]\n"
+               "          [--out FILE] [--p6] [--repeat N] [--json] [scene.txt]\n",
+               argv0);
+  return 2;
+}
+
+#define CK(call)                                                                          \
+  do {                                                                                    \
+    int rc_ = (call);                                                                     \
+    if (rc_ != RT_OK) {                                                                   \
+      std::fprintf(stderr, "%s failed: %s\n", #call, rt_error_string(rc_));                \
+      return 1;                                                                           \
+    }                                                                                     \
+  } while (0)
+#define HK(call)                                                                          \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      std::fprintf(stderr, "%s failed: %s\n", #call, hipGetErrorString(e_));               \
+      return 1;                                                                           \
+    }                                                                                     \
+  } while (0)
+#define NK(call)                                                                          \
+  do {                                                                                    \
+    ncclResult_t r_ = (call);                                                             \
+    if (r_ != ncclSuccess) {                                                              \
+      std::fprintf(stderr, "%s failed: %s\n", #call, ncclGetErrorString(r_));              \
+      return 1;                                                                           \
+    }                                                                                     \
+  } while (0)
+
+struct Result {
+  double wall_s = 0;       // host wall time of the last frame (render + gather)
+  double kernel_ms = 0;    // max over devices of the render kernel time
+  uint64_t primary = 0, shadow = 0, reflect = 0, negative = 0;
+};
+
+// Single device: render the full frame.
+int render_single(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::vector<uint8_t> &img, Result &res) {
+  rt_ctx *ctx = nullptr;
+  CK(rt_create(o.device, &ctx));
+  CK(rt_upload_scene(ctx, &sc));
+  rt_stats st{};
+  for (int it = 0; it < o.repeat; it++) {
+    auto t0 = std::chrono::high_resolution_clock::now();
+    CK(rt_render(ctx, &cam, o.width, o.height, o.depth, nullptr, img.data(), 0, &st));
+    auto t1 = std::chrono::high_resolution_clock::now();
+    res.wall_s = std::chrono::duration<double>(t1 - t0).count();
+  }
+  res.kernel_ms = st.kernel_ms;
+  res.primary = st.rays_primary;
+  res.shadow = st.rays_shadow;
+  res.reflect = st.rays_reflect;
+  res.negative = st.negative_clamped;
+  rt_destroy(ctx);
+  return 0;
+}
+
+// G devices in one process: cyclic 8-row bands, ncclGather to device 0, unpermute.
+int render_multi(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::vector<uint8_t> &img, Result &res) {
+  const int G = o.gpus, W = o.width, H = o.height, band = 8;
+  const int nb = (H + band - 1) / band, R = ((nb + G - 1) / G) * band;
+  const size_t shard_bytes = (size_t)R * W * 3;
+  std::vector<rt_ctx *> ctx(G, nullptr);
+  std::vector<hipStream_t> streams(G);
+  std::vector<uint8_t *> shard(G, nullptr);
+  std::vector<int> devs(G);
+  uint8_t *gathered = nullptr, *image = nullptr;
+  for (int g = 0; g < G; g++) {
+    devs[g] = g;
+    CK(rt_create(g, &ctx[g]));
+    CK(rt_upload_scene(ctx[g], &sc));
+    HK(hipSetDevice(g));
+    HK(hipStreamCreateWithFlags(&streams[g], hipStreamNonBlocking));
+    CK(rt_set_stream(ctx[g], streams[g]));
+    HK(hipMalloc(&shard[g], shard_bytes));
+  }
+  HK(hipSetDevice(0));
+  HK(hipMalloc(&gathered, shard_bytes * G));
+  HK(hipMalloc(&image, (size_t)H * W * 3));
+  std::vector<ncclComm_t> comms(G);
+  NK(ncclCommInitAll(comms.data(), G, devs.data()));
+  for (int it = 0; it < o.repeat; it++) {
+    for (int g = 0; g < G; g++) {
+      HK(hipSetDevice(g));
+      HK(hipDeviceSynchronize());
+    }
+    auto t0 = std::chrono::high_resolution_clock::now();
+    for (int g = 0; g < G; g++) {
+      rt_rows rows{band, g, G, R};
+      CK(rt_render_async(ctx[g], &cam, W, H, o.depth, &rows, shard[g]));
+    }
+    NK(ncclGroupStart());
+    for (int g = 0; g < G; g++) {
+      HK(hipSetDevice(g));
+      NK(ncclGather(shard[g], g == 0 ? gathered : nullptr, shard_bytes, ncclUint8, 0, comms[g], streams[g]));
+    }
+    NK(ncclGroupEnd());
+    CK(rt_unpermute_rows(ctx[0], gathered, image, W, H, band, G, R));
+    HK(hipSetDevice(0));
+    HK(hipStreamSynchronize(streams[0]));
+    auto t1 = std::chrono::high_resolution_clock::now();
+    res.wall_s = std::chrono::duration<double>(t1 - t0).count();
+  }
+  HK(hipSetDevice(0));
+  HK(hipMemcpy(img.data(), image, (size_t)H * W * 3, hipMemcpyDeviceToHost));
+  res.kernel_ms = 0;
+  for (int g = 0; g < G; g++) {
+    rt_stats st{};
+    CK(rt_render_stats(ctx[g], &st));
+    res.kernel_ms = std::max(res.kernel_ms, st.kernel_ms);
+    res.primary += st.rays_primary;
+    res.shadow += st.rays_shadow;
+    res.reflect += st.rays_reflect;
+    res.negative += st.negative_clamped;
+  }
+  for (int g = 0; g < G; g++) {
+    ncclCommDestroy(comms[g]);
+    HK(hipSetDevice(g));
+    HK(hipFree(shard[g]));
+    rt_destroy(ctx[g]);
+    HK(hipStreamDestroy(streams[g]));
+  }
+  HK(hipSetDevice(0));
+  HK(hipFree(gathered));
+  HK(hipFree(image));
+  return 0;
+}
+
+int render_pass(const Opts &o, const rt_scene &sc, const rt_camera &cam, const char *label, const char *file) {
+  std::vector<uint8_t> img((size_t)o.width * o.height * 3);
+  Result res;
+  int rc = o.gpus > 1 ? render_multi(o, sc, cam, img, res) : render_single(o, sc, cam, img, res);
+  if (rc) return rc;
+  if (o.mode == "hip")
+    std::printf("GPU rendering time: %g seconds\n", res.wall_s);  // main_gpu.cu:519
+  else
+    std::printf("%s time: %g seconds\n", label, res.wall_s);      // main.cpp:161 / :203
+  if (res.negative)
+    std::fprintf(stderr, "warning: %llu channels quantised below 0 were stored as 0\n",
+                 (unsigned long long)res.negative);
+  if (o.json) {
+    uint64_t rays = res.primary + res.shadow + res.reflect;
+    std::printf(
+        "{\"scene\": \"%s\", \"width\": %d, \"height\": %d, \"depth\": %d, \"gpus\": %d, \"rays\": %llu, "
+        "\"primary\": %llu, \"shadow\": %llu, \"reflect\": %llu, \"kernel_ms\": %.4f, \"wall_ms\": %.4f, "
+        "\"mrays_per_s\": %.2f}\n",
+        o.scene.c_str(), o.width, o.height, o.depth, o.gpus, (unsigned long long)rays,
+        (unsigned long long)res.primary, (unsigned long long)res.shadow, (unsigned long long)res.reflect,
+        res.kernel_ms, res.wall_s * 1e3, rays / (res.kernel_ms * 1e-3) / 1e6);
+  }
+  std::fflush(stdout);
+  int wrc = rt_write_ppm(file, img.data(), o.width, o.height, o.p6 ? 1 : 0);
+  if (wrc != RT_OK) {
+    std::fprintf(stderr, "could not write %s: %s\n", file, rt_error_string(wrc));
+    return 1;
+  }
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  Opts o;
+  std::string base = argv[0];
+  size_t slash = base.find_last_of('/');
+  if (slash != std::string::npos) base = base.substr(slash + 1);
+  if (base == "ray_serial") o.mode = "serial";
+  else if (base == "ray_openmp") o.mode = "openmp";
+  for (int i = 1; i < argc; i++) {
+    std::string a = argv[i];
+    auto next = [&](int &dst) {
+      if (i + 1 >= argc) return false;
+      dst = std::atoi(argv[++i]);
+      return true;
+    };
+    if (a == "--openmp") o.openmp_only = true;
+    else if (a == "--width") { if (!next(o.width)) return usage(argv[0]); }
+    else if (a == "--height") { if (!next(o.height)) return usage(argv[0]); }
+    else if (a == "--depth") { if (!next(o.depth)) return usage(argv[0]); }
+    else if (a == "--gpus") { if (!next(o.gpus)) return usage(argv[0]); }
+    else if (a == "--device") { if (!next(o.device)) return usage(argv[0]); }
+    else if (a == "--repeat") { if (!next(o.repeat)) return usage(argv[0]); }
+    else if (a == "--out") { if (i + 1 >= argc) return usage(argv[0]); o.out = argv[++i]; }
+    else if (a == "--p6") o.p6 = true;
+    else if (a == "--json") o.json = true;
+    else if (a == "-h" || a == "--help") return usage(argv[0]);
+    else o.scene = a;  // any other argument is the scene path, as main.cpp:103-110
+  }
+  if (o.width <= 0 || o.height <= 0 || o.gpus < 1 || o.repeat < 1) return usage(argv[0]);
+
+  std::printf("Testing scene loader with: %s\n\n", o.scene.c_str());  // main.cpp:116
+  rt_scene sc;
+  int rc = rt_scene_load(o.scene.c_str(), &sc, 1);
+  if (rc != RT_OK) {
+    std::fprintf(stderr, "terminate called after throwing an instance of 'std::runtime_error'\n"
+                         "  what():  Could not open scene file: %s\n", o.scene.c_str());
+    return 134 - 128;  // the reference aborts on the uncaught exception
+  }
+  rt_camera cam;
+  rt_camera_from_scene(&sc, &cam);
+
+  int status = 0;
+  if (o.mode == "hip") {
+    status = render_pass(o, sc, cam, "GPU", o.out.empty() ? "output_gpu.ppm" : o.out.c_str());
+  } else {
+    if (!o.openmp_only) {  // main.cpp:142-164
+      std::printf("Rendering (Serial)...\n");
+      status = render_pass(o, sc, cam, "Serial", o.out.empty() ? "output_serial.ppm" : o.out.c_str());
+    }
+    if (!status && o.mode == "openmp") {  // main.cpp:168-206
+      std::printf("\nRendering (OpenMP)...\n");
+      status = render_pass(o, sc, cam, "OpenMP", "output_openmp.ppm");
+    }
+  }
+  rt_scene_free(&sc);
+  return status;
+}

@@ -1,0 +1,541 @@
+// rt_kernel.hip -- gfx950 (MI355X / CDNA4) render loop + device half of the C-ABI.
+//
+// One lane per pixel, wave64 over an 8x8 pixel tile, 256-thread workgroups
+// (2x2 waves = 16x16 pixels).  Sphere geometry (cx,cy,cz,r*r as fp64, 32 B) and
+// the light list are staged into LDS per workgroup and read as wave-uniform
+// broadcasts; materials (48 B) are read from global memory only on a hit.
+// Shadow rays exit early once no lane of the wave is still unoccluded
+// (__ballot).  Reflections are walked iteratively; each level's
+// (shade*(1-refl), refl) is pushed on a per-lane stack and unwound at the end,
+// which reproduces the reference recursion's rounding exactly.
+//
+// Numerics follow the serial fp64 path operation by operation:
+// vec3.h:13-33, ray.h:12, camera.h:17-25, sphere.h:26-64, scene.h:41-121,
+// main.cpp:16-58 and the quantiser main.cpp:85-87.  Build with
+// -ffp-contract=off (also forced below): no FMA contraction, IEEE division and
+// sqrt, so the output bytes equal ray_serial's.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "rt_hip.h"
+
+#pragma clang fp contract(off)
+
+namespace rtk {
+
+constexpr double kEps = 0.001;  // ray_math_constants.h:22
+constexpr double kInf = 1e20;   // ray_math_constants.h:23
+constexpr double kSpec = 0.5;   // scene.h:38
+constexpr int kBlock = 256;
+constexpr int kTile = 16;       // workgroup tile edge (pixels)
+constexpr size_t kLdsBudget = 64 * 1024;
+
+struct __attribute__((aligned(32))) SphGeo {
+  double cx, cy, cz, rr;  // rr = radius*radius, rounded once on the host as sphere.h:33 does
+};
+struct SphMat {
+  double cr, cg, cb, refl, shin, pad;
+};
+struct LightD {
+  double px, py, pz, cr, cg, cb;
+};
+
+struct D3 {
+  double x, y, z;
+};
+__device__ __forceinline__ D3 mk(double x, double y, double z) { return D3{x, y, z}; }
+__device__ __forceinline__ D3 add(D3 a, D3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ D3 sub(D3 a, D3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ D3 mul(D3 a, D3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ D3 scale(D3 a, double t) { return mk(a.x * t, a.y * t, a.z * t); }
+__device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ double length(D3 a) { return __builtin_sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ D3 normalized(D3 a) {
+  double len = length(a);
+  return mk(a.x / len, a.y / len, a.z / len);
+}
+__device__ __forceinline__ double max0(double x) { return (0.0 < x) ? x : 0.0; }  // std::max(0.0, x)
+__device__ __forceinline__ double min1(double x) { return (x < 1.0) ? x : 1.0; }  // std::min(1.0, x)
+
+// Sphere::intersect (sphere.h:26-59) for a ray whose a = dot(d,d) is hoisted:
+// a4 = 4*a, a2 = 2*a (both exact scalings).  Returns true and t on a hit.
+__device__ __forceinline__ bool intersect(const SphGeo &s, D3 o, D3 d, double a4, double a2, double &t) {
+  double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
+  double b = 2.0 * ((ocx * d.x + ocy * d.y) + ocz * d.z);
+  double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.rr;
+  double disc = b * b - a4 * c;
+  if (!(disc >= 0.0)) return false;  // disc < 0 -> miss; a NaN disc can never be recorded either
+  if (disc == 0.0) {
+    t = -b / a2;  // tangent root, kept even when negative (sphere.h:43-47)
+    return true;
+  }
+  double sq = __builtin_sqrt(disc);
+  double t1 = (-b - sq) / a2;
+  double t2 = (-b + sq) / a2;
+  double tmx = (t1 < t2) ? t2 : t1;
+  if (tmx < 0.0) return false;
+  double tmn = (t2 < t1) ? t2 : t1;
+  t = (tmn < 0.0) ? tmx : tmn;
+  return true;
+}
+
+// Scene::find_intersection (scene.h:41-61): all spheres in order, strict '<'.
+__device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, int n, D3 o, D3 d, double &best_t) {
+  const double a = dot(d, d);
+  const double a4 = 4.0 * a, a2 = 2.0 * a;
+  double bt = kInf;
+  int bi = -1;
+  for (int i = 0; i < n; ++i) {
+    double t;
+    if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
+      bt = t;
+      bi = i;
+    }
+  }
+  best_t = bt;
+  return bi;
+}
+
+// Scene::in_shadow (scene.h:65-86) as an any-hit: some sphere with t < 1e20 and
+// t < dist.  Lanes stop testing once occluded; the wave leaves the sweep as
+// soon as the ballot of still-searching lanes is empty.
+__device__ __forceinline__ bool occluded(const SphGeo *__restrict__ g, int n, D3 o, D3 d, double dist) {
+  const double a = dot(d, d);
+  const double a4 = 4.0 * a, a2 = 2.0 * a;
+  bool occ = false;
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {
+    if (!occ) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        double t;
+        if (intersect(g[i + u], o, d, a4, a2, t) && t < kInf && t < dist) occ = true;
+      }
+    }
+    if (__ballot(!occ) == 0) return occ;
+  }
+  for (; i < n; ++i) {
+    double t;
+    if (!occ && intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist) occ = true;
+  }
+  return occ;
+}
+
+struct Cam {
+  double px, py, pz, fx, fy, fz, rx, ry, rz, ux, uy, uz, scale;
+};
+struct Rows {
+  int band, first, stride, count;
+};
+
+template <int MAXS>
+__device__ __forceinline__ D3 trace_pixel(const SphGeo *__restrict__ g, int n, const SphMat *__restrict__ mat,
+                                          const LightD *__restrict__ lights, int nl, D3 amb, D3 o, D3 d, int depth,
+                                          unsigned &c_shadow, unsigned &c_reflect) {
+  double stA[3][MAXS];
+  double stR[MAXS];
+  int lev = 0;
+  D3 res = mk(0.0, 0.0, 0.0);
+  int dleft = depth;
+  // depth <= 0 -> black (main.cpp:17-18)
+  while (dleft >= 1) {
+    double t;
+    int hi = closest_hit(g, n, o, d, t);
+    if (hi < 0) {  // sky, main.cpp:26-30
+      double st = 0.5 * (d.y + 1.0);
+      res = add(scale(mk(1.0, 1.0, 1.0), 1.0 - st), scale(mk(0.5, 0.7, 1.0), st));
+      break;
+    }
+    const SphGeo sg = g[hi];
+    const SphMat m = mat[hi];
+    D3 hit = add(o, scale(d, t));                             // main.cpp:32
+    D3 nrm = normalized(sub(hit, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
+    D3 view = normalized(sub(o, hit));                       // main.cpp:38
+    D3 mc = mk(m.cr, m.cg, m.cb);
+    D3 col = mul(amb, mc);                                   // scene.h:91
+    for (int l = 0; l < nl; ++l) {                           // scene.h:94-120
+      const LightD L = lights[l];
+      D3 lp = mk(L.px, L.py, L.pz);
+      D3 to_light = sub(lp, hit);
+      double dist = length(to_light);
+      D3 ldir = normalized(to_light);
+      ++c_shadow;
+      if (occluded(g, n, add(hit, scale(ldir, kEps)), normalized(ldir), dist)) continue;
+      double ndl = max0(dot(nrm, ldir));
+      D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
+      D3 nl2 = scale(ldir, -1.0);
+      D3 rdir = sub(nl2, scale(scale(nrm, 2.0), dot(nl2, nrm)));  // reflect(), vec3.h:31-33
+      double rdv = max0(dot(rdir, view));
+      double spec = pow(rdv, m.shin);
+      D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
+      col = add(add(specular, diffuse), col);                 // scene.h:117
+    }
+    if (m.refl > 0.0) {                                       // main.cpp:43-55
+      const double w = 1.0 - m.refl;
+      const D3 A = mk(col.x * w, col.y * w, col.z * w);
+      if (dleft - 1 >= 1) {  // host picks MAXS >= depth-1, so lev < MAXS here
+        stA[0][lev] = A.x;
+        stA[1][lev] = A.y;
+        stA[2][lev] = A.z;
+        stR[lev] = m.refl;
+        ++lev;
+        D3 rd = sub(d, scale(scale(nrm, 2.0), dot(d, nrm)));
+        o = add(hit, scale(nrm, kEps));
+        d = normalized(rd);
+        --dleft;
+        ++c_reflect;
+        continue;
+      }
+      // trace_ray(depth 0) is black (main.cpp:17-18): A + (0,0,0)*refl == A.
+      res = A;
+      break;
+    }
+    res = col;
+    break;
+  }
+  while (lev > 0) {  // unwind: shade*(1-refl) + reflected*refl, innermost first
+    --lev;
+    double r = stR[lev];
+    res = mk(stA[0][lev] + res.x * r, stA[1][lev] + res.y * r, stA[2][lev] + res.z * r);
+  }
+  return res;
+}
+
+__device__ __forceinline__ int quantize(double c) {
+  double m = 255.99 * min1(c);  // main.cpp:85
+  return (int)m;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
+  unsigned long long s = v;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  return s;
+}
+
+template <int MAXS, bool kLdsGeo>
+__global__ __launch_bounds__(kBlock) void render_kernel(const SphGeo *__restrict__ geo, const SphMat *__restrict__ mat,
+                                                        const LightD *__restrict__ lights, int n, int nl, D3 amb,
+                                                        Cam cam, int W, int H, int depth, Rows rows,
+                                                        uint8_t *__restrict__ out,
+                                                        unsigned long long *__restrict__ counters) {
+  extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
+  SphGeo *sgeo = reinterpret_cast<SphGeo *>(smem);
+  LightD *slight = reinterpret_cast<LightD *>(smem + (kLdsGeo ? (size_t)n * sizeof(SphGeo) : 0));
+  const int tid = threadIdx.x;
+  if (kLdsGeo)
+    for (int i = tid; i < n; i += kBlock) sgeo[i] = geo[i];
+  for (int i = tid; i < nl; i += kBlock) slight[i] = lights[i];
+  __syncthreads();
+  const SphGeo *gsrc = kLdsGeo ? sgeo : geo;
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int x = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
+  const int k = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
+  unsigned c_prim = 0, c_shadow = 0, c_reflect = 0, c_neg = 0;
+  if (x < W && k < rows.count) {
+    const long long y = (long long)(k / rows.band) * rows.band * rows.stride + (long long)rows.first * rows.band +
+                        (k % rows.band);
+    uint8_t *px = out + ((size_t)k * W + x) * 3;
+    if (y < H) {
+      const int j = H - 1 - (int)y;  // reference row (main.cpp:74)
+      const double u = (double)x / (W - 1), v = (double)j / (H - 1);  // main.cpp:151-152
+      // camera.h:17-25: ((u-0.5)*scale)*aspect with aspect = 1.0
+      const double su = ((u - 0.5) * cam.scale) * 1.0, sv = (v - 0.5) * cam.scale;
+      D3 dir = add(add(mk(cam.fx, cam.fy, cam.fz), scale(mk(cam.rx, cam.ry, cam.rz), su)),
+                   scale(mk(cam.ux, cam.uy, cam.uz), sv));
+      D3 d = normalized(normalized(dir));  // get_ray normalises, Ray() normalises again
+      D3 o = mk(cam.px, cam.py, cam.pz);
+      if (depth >= 1) c_prim = 1;
+      D3 c = trace_pixel<MAXS>(gsrc, n, mat, slight, nl, amb, o, d, depth, c_shadow, c_reflect);
+      int q0 = quantize(c.x), q1 = quantize(c.y), q2 = quantize(c.z);
+      c_neg = (q0 < 0) + (q1 < 0) + (q2 < 0);
+      px[0] = (uint8_t)(q0 < 0 ? 0 : q0);
+      px[1] = (uint8_t)(q1 < 0 ? 0 : q1);
+      px[2] = (uint8_t)(q2 < 0 ? 0 : q2);
+    } else {
+      px[0] = px[1] = px[2] = 0;
+    }
+  }
+  unsigned long long sp = wave_sum(c_prim), ss = wave_sum(c_shadow), sr = wave_sum(c_reflect),
+                     sn = wave_sum(c_neg);
+  if (lane == 0) {
+    if (sp) atomicAdd(&counters[0], sp);
+    if (ss) atomicAdd(&counters[1], ss);
+    if (sr) atomicAdd(&counters[2], sr);
+    if (sn) atomicAdd(&counters[3], sn);
+  }
+}
+
+// Reassemble rank-major shards into PPM row order (one workgroup per row).
+__global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                           int W, int H, int band, int G, int R) {
+  const int y = blockIdx.x;
+  if (y >= H) return;
+  const int b = y / band;
+  const int r = b % G;
+  const int k = (b / G) * band + (y % band);
+  const uint8_t *s = src + ((size_t)r * R + k) * (size_t)W * 3;
+  uint8_t *d = dst + (size_t)y * W * 3;
+  for (int i = threadIdx.x; i < W * 3; i += kBlock) d[i] = s[i];
+}
+
+}  // namespace rtk
+
+using namespace rtk;
+
+struct rt_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  SphGeo *d_geo = nullptr;
+  SphMat *d_mat = nullptr;
+  LightD *d_lights = nullptr;
+  int nsph = 0, nlight = 0;
+  double amb[3] = {0, 0, 0};
+  bool has_scene = false;
+  unsigned long long *d_counters = nullptr;
+  unsigned long long *h_counters = nullptr;  // pinned
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  uint8_t *d_tmp = nullptr;
+  size_t tmp_bytes = 0;
+  std::string err;
+};
+
+namespace {
+
+int fail(rt_ctx *c, hipError_t e, const char *what) {
+  if (c) c->err = std::string(what) + ": " + hipGetErrorString(e);
+  return e == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_HIP;
+}
+
+#define RT_TRY(ctx, call)                           \
+  do {                                              \
+    hipError_t e_ = (call);                         \
+    if (e_ != hipSuccess) return fail(ctx, e_, #call); \
+  } while (0)
+
+void free_scene(rt_ctx *c) {
+  if (c->d_geo) (void)hipFree(c->d_geo);
+  if (c->d_mat) (void)hipFree(c->d_mat);
+  if (c->d_lights) (void)hipFree(c->d_lights);
+  c->d_geo = nullptr;
+  c->d_mat = nullptr;
+  c->d_lights = nullptr;
+  c->has_scene = false;
+}
+
+template <int MAXS>
+void launch_render(rt_ctx *c, bool lds_geo, dim3 grid, size_t lds, const Cam &cam, int W, int H, int depth,
+                   const Rows &rows, uint8_t *out) {
+  D3 amb{c->amb[0], c->amb[1], c->amb[2]};
+  if (lds_geo)
+    hipLaunchKernelGGL((render_kernel<MAXS, true>), grid, dim3(kBlock), lds, c->stream, c->d_geo, c->d_mat,
+                       c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out, c->d_counters);
+  else
+    hipLaunchKernelGGL((render_kernel<MAXS, false>), grid, dim3(kBlock), lds, c->stream, c->d_geo, c->d_mat,
+                       c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out, c->d_counters);
+}
+
+int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_rows *rows, const void *out,
+             Rows &r) {
+  if (!c || !cam || !out || W <= 0 || H <= 0) return RT_ERR_INVALID_ARG;
+  if (!c->has_scene) return RT_ERR_NO_SCENE;
+  if (depth > RT_MAX_DEPTH) return RT_ERR_DEPTH;
+  r = rows ? Rows{rows->band, rows->first, rows->stride, rows->count} : Rows{1, 0, 1, H};
+  if (r.band < 1 || r.stride < 1 || r.first < 0 || r.count < 0) return RT_ERR_INVALID_ARG;
+  if ((long long)W * 3 * (long long)r.count > (1LL << 40)) return RT_ERR_INVALID_ARG;
+  return RT_OK;
+}
+
+int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows &r, uint8_t *dst) {
+  RT_TRY(c, hipSetDevice(c->device));
+  RT_TRY(c, hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+  RT_TRY(c, hipEventRecord(c->ev0, c->stream));
+  if (r.count > 0) {
+    Cam cam{cm->position[0], cm->position[1], cm->position[2], cm->forward[0], cm->forward[1], cm->forward[2],
+            cm->right[0],    cm->right[1],    cm->right[2],    cm->up[0],      cm->up[1],      cm->up[2],
+            cm->scale};
+    dim3 grid((W + kTile - 1) / kTile, (r.count + kTile - 1) / kTile);
+    size_t geo_bytes = (size_t)c->nsph * sizeof(SphGeo), light_bytes = (size_t)c->nlight * sizeof(LightD);
+    bool lds_geo = geo_bytes + light_bytes <= kLdsBudget;
+    size_t lds = (lds_geo ? geo_bytes : 0) + light_bytes;
+    if (lds > kLdsBudget) {
+      c->err = "light list does not fit in LDS";
+      return RT_ERR_INVALID_ARG;
+    }
+    int stack = depth - 1;
+    if (stack <= 4) launch_render<4>(c, lds_geo, grid, lds, cam, W, H, depth, r, dst);
+    else if (stack <= 16) launch_render<16>(c, lds_geo, grid, lds, cam, W, H, depth, r, dst);
+    else launch_render<RT_MAX_DEPTH>(c, lds_geo, grid, lds, cam, W, H, depth, r, dst);
+    RT_TRY(c, hipGetLastError());
+  }
+  RT_TRY(c, hipEventRecord(c->ev1, c->stream));
+  RT_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           c->stream));
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_device_count(int *count) {
+  if (!count) return RT_ERR_INVALID_ARG;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *count = e == hipSuccess ? n : 0;
+  return e == hipSuccess ? RT_OK : RT_ERR_NO_DEVICE;
+}
+
+int rt_create(int device, rt_ctx **out) {
+  if (!out) return RT_ERR_INVALID_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return RT_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return RT_ERR_INVALID_ARG;
+  rt_ctx *c = new rt_ctx();
+  c->device = device;
+  auto bail = [&](int rc) {
+    rt_destroy(c);
+    return rc;
+  };
+  if (hipSetDevice(device) != hipSuccess) return bail(RT_ERR_HIP);
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(RT_ERR_HIP);
+  c->stream = c->own_stream;
+  if (hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess) return bail(RT_ERR_OUT_OF_MEMORY);
+  if (hipHostMalloc(&c->h_counters, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+    return bail(RT_ERR_OUT_OF_MEMORY);
+  std::memset(c->h_counters, 0, 4 * sizeof(unsigned long long));
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) return bail(RT_ERR_HIP);
+  *out = c;
+  return RT_OK;
+}
+
+void rt_destroy(rt_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+  if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
+  free_scene(c);
+  if (c->d_counters) (void)hipFree(c->d_counters);
+  if (c->h_counters) (void)hipHostFree(c->h_counters);
+  if (c->d_tmp) (void)hipFree(c->d_tmp);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+const char *rt_last_error(const rt_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int rt_set_stream(rt_ctx *c, void *s) {
+  if (!c) return RT_ERR_INVALID_ARG;
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return RT_OK;
+}
+
+int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
+  if (!c || !s || s->num_spheres < 0 || s->num_lights < 0) return RT_ERR_INVALID_ARG;
+  if ((s->num_spheres > 0 && !s->spheres) || (s->num_lights > 0 && !s->lights)) return RT_ERR_INVALID_ARG;
+  RT_TRY(c, hipSetDevice(c->device));
+  RT_TRY(c, hipStreamSynchronize(c->stream));
+  free_scene(c);
+  const int n = s->num_spheres, nl = s->num_lights;
+  SphGeo *hg = new SphGeo[n + 1];
+  SphMat *hm = new SphMat[n + 1];
+  LightD *hl = new LightD[nl + 1];
+  for (int i = 0; i < n; i++) {
+    const rt_sphere &sp = s->spheres[i];
+    hg[i] = SphGeo{sp.center[0], sp.center[1], sp.center[2], sp.radius * sp.radius};
+    hm[i] = SphMat{sp.color[0], sp.color[1], sp.color[2], sp.reflectivity, sp.shininess, 0.0};
+  }
+  for (int i = 0; i < nl; i++) {
+    const rt_light &L = s->lights[i];
+    hl[i] = LightD{L.position[0], L.position[1], L.position[2], L.color[0], L.color[1], L.color[2]};
+  }
+  int rc = RT_OK;
+  hipError_t e = hipSuccess;
+  if ((e = hipMalloc(&c->d_geo, sizeof(SphGeo) * (n + 1))) != hipSuccess ||
+      (e = hipMalloc(&c->d_mat, sizeof(SphMat) * (n + 1))) != hipSuccess ||
+      (e = hipMalloc(&c->d_lights, sizeof(LightD) * (nl + 1))) != hipSuccess ||
+      (e = hipMemcpy(c->d_geo, hg, sizeof(SphGeo) * n, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(c->d_mat, hm, sizeof(SphMat) * n, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(c->d_lights, hl, sizeof(LightD) * nl, hipMemcpyHostToDevice)) != hipSuccess) {
+    rc = fail(c, e, "rt_upload_scene");
+    free_scene(c);
+  } else {
+    c->nsph = n;
+    c->nlight = nl;
+    for (int q = 0; q < 3; q++) c->amb[q] = s->ambient[q];
+    c->has_scene = true;
+  }
+  delete[] hg;
+  delete[] hm;
+  delete[] hl;
+  return rc;
+}
+
+int rt_render_async(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_rows *rows, uint8_t *out) {
+  Rows r;
+  int rc = validate(c, cam, W, H, depth, rows, out, r);
+  if (rc != RT_OK) return rc;
+  return enqueue(c, cam, W, H, depth, r, out);
+}
+
+int rt_render_stats(rt_ctx *c, rt_stats *st) {
+  if (!c || !st) return RT_ERR_INVALID_ARG;
+  RT_TRY(c, hipSetDevice(c->device));
+  RT_TRY(c, hipStreamSynchronize(c->stream));
+  float ms = 0.f;
+  RT_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  st->rays_primary = c->h_counters[0];
+  st->rays_shadow = c->h_counters[1];
+  st->rays_reflect = c->h_counters[2];
+  st->negative_clamped = c->h_counters[3];
+  st->kernel_ms = ms;
+  return RT_OK;
+}
+
+int rt_render(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_rows *rows, uint8_t *out,
+              int out_on_device, rt_stats *st) {
+  Rows r;
+  int rc = validate(c, cam, W, H, depth, rows, out, r);
+  if (rc != RT_OK) return rc;
+  RT_TRY(c, hipSetDevice(c->device));
+  size_t bytes = (size_t)r.count * W * 3;
+  uint8_t *dst = out;
+  if (!out_on_device) {
+    if (c->tmp_bytes < bytes) {
+      RT_TRY(c, hipStreamSynchronize(c->stream));
+      if (c->d_tmp) (void)hipFree(c->d_tmp);
+      c->d_tmp = nullptr;
+      c->tmp_bytes = 0;
+      RT_TRY(c, hipMalloc(&c->d_tmp, bytes ? bytes : 1));
+      c->tmp_bytes = bytes;
+    }
+    dst = c->d_tmp;
+  }
+  rc = enqueue(c, cam, W, H, depth, r, dst);
+  if (rc != RT_OK) return rc;
+  if (!out_on_device && bytes) RT_TRY(c, hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, c->stream));
+  rt_stats tmp;
+  rc = rt_render_stats(c, st ? st : &tmp);
+  return rc;
+}
+
+int rt_unpermute_rows(rt_ctx *c, const uint8_t *gathered, uint8_t *image, int W, int H, int band, int G, int R) {
+  if (!c || !gathered || !image || W <= 0 || H <= 0 || band < 1 || G < 1 || R < 0) return RT_ERR_INVALID_ARG;
+  const long long bands = (H + band - 1) / band;
+  if ((long long)((bands + G - 1) / G) * band > R) return RT_ERR_INVALID_ARG;
+  RT_TRY(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(unpermute_kernel, dim3(H), dim3(kBlock), 0, c->stream, gathered, image, W, H, band, G, R);
+  RT_TRY(c, hipGetLastError());
+  return RT_OK;
+}
+
+}  // extern "C"

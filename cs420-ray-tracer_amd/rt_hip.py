@@ -1,0 +1,273 @@
+"""ctypes binding of include/rt_hip.h (librt_hip.so) -- the Python host mirror.
+
+This is the binding a reference-side maintainer would add to drive the HIP
+render loop from Python; the C++ host (csrc/ray_hip.cpp) uses the same ABI.
+Nothing here falls back to a CPU path: if librt_hip.so is missing or no GPU is
+visible the calls raise.
+
+Reference interfaces mirrored (file:line in shininglegend/cs420-ray-tracer):
+  load_scene            include/scene_loader.h:27-135   -> Scene.load / Scene.parse
+  Camera(pos, look, fov) include/camera.h:10-15          -> Camera.from_scene
+  trace_ray pixel loop   src/main.cpp:146-157            -> Renderer.render
+  launch_gpu_kernel      src/kernel.cu:185-200           -> Renderer.render_async
+  write_ppm              src/main.cpp:69-91              -> write_ppm
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librt_hip.so")
+
+RT_MAX_DEPTH = 64
+
+
+class RtError(RuntimeError):
+    def __init__(self, status: int, what: str, detail: str = ""):
+        self.status = status
+        super().__init__(f"{what}: {status_string(status)}" + (f" ({detail})" if detail else ""))
+
+
+class rt_sphere(C.Structure):
+    _fields_ = [("center", C.c_double * 3), ("radius", C.c_double), ("color", C.c_double * 3),
+                ("reflectivity", C.c_double), ("shininess", C.c_double)]
+
+
+class rt_light(C.Structure):
+    _fields_ = [("position", C.c_double * 3), ("color", C.c_double * 3), ("intensity", C.c_double)]
+
+
+class rt_scene(C.Structure):
+    _fields_ = [("num_spheres", C.c_int32), ("num_lights", C.c_int32),
+                ("spheres", C.POINTER(rt_sphere)), ("lights", C.POINTER(rt_light)),
+                ("ambient", C.c_double * 3), ("cam_position", C.c_double * 3),
+                ("cam_look_at", C.c_double * 3), ("cam_fov", C.c_double),
+                ("has_camera", C.c_int32), ("warnings", C.c_int32)]
+
+
+class rt_camera(C.Structure):
+    _fields_ = [("position", C.c_double * 3), ("forward", C.c_double * 3), ("right", C.c_double * 3),
+                ("up", C.c_double * 3), ("scale", C.c_double)]
+
+
+class rt_rows(C.Structure):
+    _fields_ = [("band", C.c_int32), ("first", C.c_int32), ("stride", C.c_int32), ("count", C.c_int32)]
+
+
+class rt_stats(C.Structure):
+    _fields_ = [("rays_primary", C.c_uint64), ("rays_shadow", C.c_uint64), ("rays_reflect", C.c_uint64),
+                ("negative_clamped", C.c_uint64), ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {"primary": self.rays_primary, "shadow": self.rays_shadow, "reflect": self.rays_reflect,
+                "negative": self.negative_clamped, "kernel_ms": self.kernel_ms}
+
+    @property
+    def rays(self) -> int:
+        return self.rays_primary + self.rays_shadow + self.rays_reflect
+
+
+# Every symbol include/rt_hip.h declares, with its ctypes signature.
+_P = C.c_void_p
+SIGNATURES = {
+    "rt_scene_load": (C.c_int, [C.c_char_p, C.POINTER(rt_scene), C.c_int]),
+    "rt_scene_parse": (C.c_int, [C.c_char_p, C.POINTER(rt_scene), C.c_int]),
+    "rt_scene_free": (None, [C.POINTER(rt_scene)]),
+    "rt_camera_from_scene": (C.c_int, [C.POINTER(rt_scene), C.POINTER(rt_camera)]),
+    "rt_write_ppm": (C.c_int, [C.c_char_p, _P, C.c_int, C.c_int, C.c_int]),
+    "rt_error_string": (C.c_char_p, [C.c_int]),
+    "rt_abi_version": (C.c_int, []),
+    "rt_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "rt_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "rt_destroy": (None, [_P]),
+    "rt_last_error": (C.c_char_p, [_P]),
+    "rt_set_stream": (C.c_int, [_P, _P]),
+    "rt_upload_scene": (C.c_int, [_P, C.POINTER(rt_scene)]),
+    "rt_render": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.POINTER(rt_rows), _P,
+                            C.c_int, C.POINTER(rt_stats)]),
+    "rt_render_async": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.POINTER(rt_rows), _P]),
+    "rt_render_stats": (C.c_int, [_P, C.POINTER(rt_stats)]),
+    "rt_unpermute_rows": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+}
+
+_lib = None
+
+
+def lib(path: str = LIB_PATH):
+    """Load librt_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def status_string(status: int) -> str:
+    try:
+        return lib().rt_error_string(status).decode()
+    except Exception:  # pragma: no cover - only when the library itself is missing
+        return f"status {status}"
+
+
+def _check(rc: int, what: str, ctx=None):
+    if rc != 0:
+        detail = lib().rt_last_error(ctx).decode() if ctx else ""
+        raise RtError(rc, what, detail)
+
+
+class Scene:
+    """A parsed scene (owns the C arrays).  Mirrors load_scene(), scene_loader.h:27."""
+
+    def __init__(self):
+        self._s = rt_scene()
+        self._owned = False
+
+    @classmethod
+    def load(cls, path: str, verbose: bool = False) -> "Scene":
+        s = cls()
+        _check(lib().rt_scene_load(os.fsencode(path), C.byref(s._s), int(verbose)), f"rt_scene_load({path})")
+        s._owned = True
+        return s
+
+    @classmethod
+    def parse(cls, text: str, verbose: bool = False) -> "Scene":
+        s = cls()
+        _check(lib().rt_scene_parse(text.encode(), C.byref(s._s), int(verbose)), "rt_scene_parse")
+        s._owned = True
+        return s
+
+    @property
+    def raw(self) -> rt_scene:
+        return self._s
+
+    @property
+    def num_spheres(self) -> int:
+        return self._s.num_spheres
+
+    @property
+    def num_lights(self) -> int:
+        return self._s.num_lights
+
+    @property
+    def warnings(self) -> int:
+        return self._s.warnings
+
+    def sphere(self, i: int) -> dict:
+        sp = self._s.spheres[i]
+        return {"center": tuple(sp.center), "radius": sp.radius, "color": tuple(sp.color),
+                "reflectivity": sp.reflectivity, "shininess": sp.shininess}
+
+    def light(self, i: int) -> dict:
+        L = self._s.lights[i]
+        return {"position": tuple(L.position), "color": tuple(L.color), "intensity": L.intensity}
+
+    def camera(self) -> rt_camera:
+        cam = rt_camera()
+        _check(lib().rt_camera_from_scene(C.byref(self._s), C.byref(cam)), "rt_camera_from_scene")
+        return cam
+
+    def close(self):
+        if self._owned:
+            lib().rt_scene_free(C.byref(self._s))
+            self._owned = False
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def rows_for_shard(height: int, band: int, rank: int, world: int) -> rt_rows:
+    """Cyclic bands of `band` rows: rank r renders bands r, r+G, r+2G, ..."""
+    nb = -(-height // band)
+    per = -(-nb // world)
+    return rt_rows(band, rank, world, per * band)
+
+
+class Renderer:
+    """One device context (rt_ctx).  Mirrors GPUResources + launch_gpu_kernel."""
+
+    def __init__(self, device: int = 0):
+        self._ctx = C.c_void_p()
+        _check(lib().rt_create(device, C.byref(self._ctx)), f"rt_create({device})")
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def set_stream(self, stream_ptr: int | None):
+        _check(lib().rt_set_stream(self._ctx, C.c_void_p(stream_ptr or 0)), "rt_set_stream", self._ctx)
+
+    def upload(self, scene: Scene):
+        _check(lib().rt_upload_scene(self._ctx, C.byref(scene.raw)), "rt_upload_scene", self._ctx)
+
+    def render(self, cam: rt_camera, width: int, height: int, depth: int, rows: rt_rows | None = None,
+               out=None, out_on_device: bool = False) -> tuple[object, rt_stats]:
+        """Render into `out` (host bytearray/numpy if None) and return (buffer, stats)."""
+        count = rows.count if rows is not None else height
+        if out is None:
+            out = bytearray(count * width * 3)
+        ptr = _addr(out)
+        st = rt_stats()
+        _check(lib().rt_render(self._ctx, C.byref(cam), width, height, depth,
+                               C.byref(rows) if rows is not None else None, C.c_void_p(ptr), int(out_on_device),
+                               C.byref(st)), "rt_render", self._ctx)
+        return out, st
+
+    def render_async(self, cam: rt_camera, width: int, height: int, depth: int, rows: rt_rows | None,
+                     out_device_ptr: int):
+        _check(lib().rt_render_async(self._ctx, C.byref(cam), width, height, depth,
+                                     C.byref(rows) if rows is not None else None, C.c_void_p(out_device_ptr)),
+               "rt_render_async", self._ctx)
+
+    def stats(self) -> rt_stats:
+        st = rt_stats()
+        _check(lib().rt_render_stats(self._ctx, C.byref(st)), "rt_render_stats", self._ctx)
+        return st
+
+    def unpermute(self, gathered_ptr: int, image_ptr: int, width: int, height: int, band: int, shards: int,
+                  rows_per_shard: int):
+        _check(lib().rt_unpermute_rows(self._ctx, C.c_void_p(gathered_ptr), C.c_void_p(image_ptr), width, height,
+                                       band, shards, rows_per_shard), "rt_unpermute_rows", self._ctx)
+
+    def close(self):
+        if self._ctx:
+            lib().rt_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _addr(buf) -> int:
+    if isinstance(buf, bytes):
+        return C.cast(C.c_char_p(buf), C.c_void_p).value
+    if isinstance(buf, bytearray):
+        return C.addressof((C.c_char * len(buf)).from_buffer(buf))
+    if hasattr(buf, "ctypes"):  # numpy
+        return buf.ctypes.data
+    if hasattr(buf, "data_ptr"):  # torch
+        return buf.data_ptr()
+    raise TypeError(type(buf))
+
+
+def write_ppm(path: str, rgb, width: int, height: int, binary: bool = False):
+    _check(lib().rt_write_ppm(os.fsencode(path), C.c_void_p(_addr(rgb)), width, height, int(binary)), "rt_write_ppm")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    lib().rt_device_count(C.byref(n))
+    return n.value

@@ -1,0 +1,162 @@
+/*
+ * rt_hip.h -- C-ABI of the MI355X (gfx950) render-loop library, librt_hip.so.
+ *
+ * Drop-in boundary for the per-pixel render loop of shininglegend/cs420-ray-tracer.
+ * Plain C, POD structs, plain pointers and sizes; no HIP/torch types appear in
+ * any signature (streams are passed as `void *` = hipStream_t).
+ *
+ * What each entry point replaces in the reference (file:line):
+ *   rt_scene_load / rt_scene_parse  <- load_scene()           include/scene_loader.h:27-135
+ *   rt_scene_free                   <- Scene destructor       include/scene.h:28-33
+ *   rt_camera_from_scene            <- Camera::Camera()       include/camera.h:10-15 (+ scale of get_ray, :18-19)
+ *   rt_create / rt_destroy          <- GPUResources ctor/dtor src/main_hybrid.cpp:182-195, 300-316
+ *   rt_upload_scene                 <- GPUResources::upload_scene + upload_lights_and_ambience
+ *                                      src/main_hybrid.cpp:198-279, src/kernel.cu:202-207
+ *   rt_render                       <- the serial pixel loop  src/main.cpp:146-157 (trace_ray :16-58),
+ *                                      the OpenMP loop :185-199, and launch_gpu_kernel src/kernel.cu:185-200
+ *   rt_render_async                 <- launch_gpu_kernel(..., cudaStream_t) src/kernel.cu:185-200
+ *   rt_write_ppm                    <- write_ppm()            src/main.cpp:69-91
+ *   rt_unpermute_rows               <- (new) reassembly of the multi-GPU row shards
+ *
+ * Errors: every call returns an rt_status (0 = ok); the library never exits
+ * (the reference's CUDA_CHECK -> exit(1), src/main_gpu.cu:27-35, is not kept).
+ * Threading: one rt_ctx per device per host thread; distinct contexts are
+ * independent and may be used concurrently.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_HIP_ABI_VERSION 1
+/* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
+#define RT_MAX_DEPTH 64
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARG = 1,
+    RT_ERR_NO_DEVICE = 2,
+    RT_ERR_HIP = 3,          /* a HIP runtime call failed; see rt_last_error() */
+    RT_ERR_OUT_OF_MEMORY = 4,
+    RT_ERR_NO_SCENE = 5,     /* rt_render before rt_upload_scene */
+    RT_ERR_IO = 6,           /* scene file could not be opened / image not written */
+    RT_ERR_DEPTH = 7,        /* depth > RT_MAX_DEPTH */
+} rt_status;
+
+/* Sphere + Material, include/sphere.h:8-21.  reflectivity = the file's
+ * "metallic" column (scene_loader.h:288); roughness is dropped as upstream. */
+typedef struct rt_sphere {
+    double center[3];
+    double radius;
+    double color[3];
+    double reflectivity;
+    double shininess;
+} rt_sphere;
+
+/* Light, include/scene.h:10-14 (intensity is parsed but unused, scene.h:117). */
+typedef struct rt_light {
+    double position[3];
+    double color[3];
+    double intensity;
+} rt_light;
+
+/* Scene + CameraConfig, include/scene.h:17-38. */
+typedef struct rt_scene {
+    int32_t num_spheres;
+    int32_t num_lights;
+    rt_sphere *spheres;
+    rt_light *lights;
+    double ambient[3];        /* default (0,0,0) */
+    double cam_position[3];   /* default (0,0,0)   scene.h:22 */
+    double cam_look_at[3];    /* default (0,0,-1)  scene.h:22 */
+    double cam_fov;           /* default 60        scene.h:22 */
+    int32_t has_camera;
+    int32_t warnings;         /* records skipped by the parser */
+} rt_scene;
+
+/* Camera basis computed on the host (camera.h:10-15); scale = tan(fov*0.5*M_PI/180). */
+typedef struct rt_camera {
+    double position[3];
+    double forward[3];
+    double right[3];
+    double up[3];
+    double scale;
+} rt_camera;
+
+/* Which image rows a call renders.  Output row k (0 <= k < count) is image row
+ *   y = (k / band) * band * stride + first * band + (k % band)
+ * in PPM order (y = 0 is the TOP row, i.e. reference row j = H-1-y,
+ * src/main.cpp:74).  Rows with y >= H are padding: they are written as zeros.
+ * Full frame: {band=1, first=0, stride=1, count=H}.  Rank r of G GPUs with
+ * cyclic bands of B rows: {B, r, G, ceil(ceil(H/B)/G)*B}. */
+typedef struct rt_rows {
+    int32_t band;
+    int32_t first;
+    int32_t stride;
+    int32_t count;
+} rt_rows;
+
+/* Ray counts: primary = pixels traced; shadow = lights x shaded
+ * hits (counted even when the GPU exits early); reflect = reflection rays
+ * traced (reflective hit with depth-1 >= 1).  kernel_ms = HIP-event time of the
+ * render kernel(s) on the context's stream. */
+typedef struct rt_stats {
+    uint64_t rays_primary;
+    uint64_t rays_shadow;
+    uint64_t rays_reflect;
+    uint64_t negative_clamped; /* channels whose int(255.99*min(1,c)) < 0, stored as 0 */
+    double kernel_ms;
+} rt_stats;
+
+typedef struct rt_ctx rt_ctx;
+
+/* ---- host-side scene / camera / image I/O (no GPU needed) ---------------- */
+int rt_scene_load(const char *path, rt_scene *out, int verbose);
+int rt_scene_parse(const char *text, rt_scene *out, int verbose);
+void rt_scene_free(rt_scene *scene);
+int rt_camera_from_scene(const rt_scene *scene, rt_camera *out);
+/* binary=0: P3 text byte-identical to write_ppm (src/main.cpp:69-91); binary=1: P6. */
+int rt_write_ppm(const char *path, const uint8_t *rgb, int width, int height, int binary);
+const char *rt_error_string(int status);
+int rt_abi_version(void);
+
+/* ---- device ------------------------------------------------------------- */
+int rt_device_count(int *count);
+int rt_create(int device, rt_ctx **out);
+void rt_destroy(rt_ctx *ctx);
+const char *rt_last_error(const rt_ctx *ctx);
+/* Use an external stream (hipStream_t) for all work of this context; NULL
+ * restores the context's own stream. */
+int rt_set_stream(rt_ctx *ctx, void *hip_stream);
+/* Copies the scene into device memory owned by the context (replaces any
+ * previous scene).  The host arrays may be freed afterwards. */
+int rt_upload_scene(rt_ctx *ctx, const rt_scene *scene);
+
+/* Synchronous render.  rgb_out: rows->count * width * 3 bytes, PPM row order
+ * (see rt_rows).  out_on_device = 1 if rgb_out is device memory of this
+ * context's device, 0 for host memory.  rows = NULL means the full frame.
+ * stats may be NULL. */
+int rt_render(rt_ctx *ctx, const rt_camera *cam, int width, int height, int depth, const rt_rows *rows,
+              uint8_t *rgb_out, int out_on_device, rt_stats *stats);
+/* Asynchronous render into DEVICE memory on the context's stream; nothing is
+ * synchronised.  rt_render_stats() waits for the stream and returns the stats
+ * of the most recent rt_render_async. */
+int rt_render_async(rt_ctx *ctx, const rt_camera *cam, int width, int height, int depth, const rt_rows *rows,
+                    uint8_t *rgb_out_device);
+int rt_render_stats(rt_ctx *ctx, rt_stats *stats);
+
+/* Reassemble G shards gathered rank-major ([G][rows_per_rank][W][3], rank r
+ * rendered with rt_rows{band, r, G, rows_per_rank}) into a PPM-ordered
+ * [H][W][3] image.  Both pointers are device memory; runs on the ctx stream. */
+int rt_unpermute_rows(rt_ctx *ctx, const uint8_t *gathered_device, uint8_t *image_device, int width, int height,
+                      int band, int num_shards, int rows_per_shard);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HIP_H */

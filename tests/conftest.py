@@ -1,0 +1,56 @@
+import json
+import lzma
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "cs420-ray-tracer_amd")
+ORACLE = os.path.join(REPO, "oracle")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+SCENES = os.path.join(PKG, "scenes")
+for p in (PKG, ORACLE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs on the GPU box)")
+
+
+def scene_path(name: str) -> str:
+    return os.path.join(SCENES, name + ".txt")
+
+
+def manifest() -> dict:
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def golden_rgb(name: str) -> bytes:
+    """RGB8 bytes (PPM row order) of a committed golden fixture."""
+    with open(os.path.join(GOLDEN, name + ".ppm.xz"), "rb") as f:
+        data = lzma.decompress(f.read())
+    m = manifest()[name]
+    hdr = b"P6\n%d %d\n255\n" % (m["width"], m["height"])
+    assert data.startswith(hdr)
+    return data[len(hdr):]
+
+
+def diff_summary(a: bytes, b: bytes) -> str:
+    import numpy as np
+
+    x = np.frombuffer(a, np.uint8).astype(np.int16)
+    y = np.frombuffer(b, np.uint8).astype(np.int16)
+    d = np.abs(x - y)
+    return f"{int((d > 0).sum())} channels differ, {int((d > 1).sum())} by >1, max {int(d.max()) if d.size else 0}"
+
+
+@pytest.fixture(scope="session")
+def gpu_renderer():
+    import rt_hip
+
+    r = rt_hip.Renderer(0)
+    yield r
+    r.close()
