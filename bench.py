@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s of the HIP render loop (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+
+A step renders ONE frame of the workload: each rank traces its cyclic 8-row
+bands through librt_hip.so (rt_render_async on torch's current stream, output
+resident in HBM), then the shards are gathered to rank 0 with RCCL
+(torch.distributed "nccl" = RCCL over xGMI) and unpermuted into the final
+PPM-ordered framebuffer on device.  Total work per step is fixed as N grows
+("scaling": "strong").  value = rays of the frame x K / max-over-ranks wall
+time of the K timed steps.
+
+Also reported:
+  roofline      fp64 VALU roof of the render kernel: algorithmic FLOPs per
+                launch (25 per ray-sphere test x spheres x rays)
+                / mean in-stream HIP-event kernel time of the timed launches.
+  hbm_write     the north star's HBM-write roofline: W*H*3 bytes per frame.
+  cpu_baseline  the reference's own trace_ray (oracle/_ref/ref_render, built
+                from /root/reference/src/main.cpp) on 1 host core, same
+                workload, rank 0 at N=1 only; falls back to the C port
+                (oracle/liborc.so) when the reference build is absent.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "cs420-ray-tracer_amd")
+ORACLE = os.path.join(REPO, "oracle")
+sys.path.insert(0, PKG)
+
+METRIC = "Mrays/sec (primary+shadow+reflect) at 1920×1080, 200 spheres, depth 4"
+WORKLOADS = {
+    # name: (scene, W, H, depth)
+    "synth200_1920x1080_d4": ("synth200", 1920, 1080, 4),   # the metric (BASELINE cfg 3')
+    "complex_1920x1080_d4": ("complex", 1920, 1080, 4),     # north-star target
+    "medium_1920x1080_d2": ("medium", 1920, 1080, 2),       # cfg 2
+    "complex_3840x2160_d4": ("complex", 3840, 2160, 4),     # cfg 4
+    "synth10k_3840x2160_d6": ("synth10k", 3840, 2160, 6),   # cfg 5
+}
+FLOP_PER_TEST = 25          # A5 miss path: 3 sub + 5 (a) + 6 (b) + 7 (c) + 4 (disc), SURVEY 8(d)
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X vector FP64 (spec; 256 CU x 2.4 GHz x 128 FLOP/clk)
+HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+BAND = 8
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(scene_file: str, W: int, H: int, D: int, rays_per_frame: int) -> dict:
+    """Reference render loop on one host core over the full frame (the sample)."""
+    ref = os.path.join(ORACLE, "_ref", "ref_render")
+    if os.path.exists(ref):
+        out = subprocess.run([ref, scene_file, str(W), str(H), str(D)], capture_output=True, text=True,
+                             timeout=600, check=True).stdout
+        secs = float(out.split("Serial time:")[1].split()[0])
+        kind, rays = "reference", rays_per_frame
+        what = "oracle/_ref/ref_render: the reference's src/main.cpp trace_ray, g++ -O3, full frame"
+    else:
+        sys.path.insert(0, ORACLE)
+        import orc  # checker / CPU-baseline leg only
+
+        _, counts, secs = orc.OracleScene(scene_file).render(W, H, D, threads=1)
+        kind, rays = "port", counts["primary"] + counts["shadow"] + counts["reflect"]
+        what = "oracle/liborc.so C restatement, full frame"
+    return {"value": round(rays / secs / 1e6, 3), "unit": "Mrays/s", "cores": 1, "kind": kind,
+            "sample": f"{what}; {W}x{H} d{D}, {rays} rays in {secs:.3f} s on 1 thread of {cpu_model()}"}
+
+
+def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device):
+    scene_name, W, H, D = WORKLOADS[workload]
+    scene_file = os.path.join(PKG, "scenes", scene_name + ".txt")
+    scene = rt_hip.Scene.load(scene_file)
+    cam = scene.camera()
+    r = rt_hip.Renderer(device)
+    r.upload(scene)
+    stream = torch.cuda.current_stream()
+    r.set_stream(stream.cuda_stream)  # the kernel runs on torch's stream: events and RCCL order with it
+    rows = rt_hip.rows_for_shard(H, BAND, rank, world) if world > 1 else rt_hip.rt_rows(1, 0, 1, H)
+    R = rows.count
+    shard = torch.empty((R, W, 3), dtype=torch.uint8, device=f"cuda:{device}")
+    gathered = image = None
+    if world > 1 and rank == 0:
+        gathered = torch.empty((world, R, W, 3), dtype=torch.uint8, device=f"cuda:{device}")
+        image = torch.empty((H, W, 3), dtype=torch.uint8, device=f"cuda:{device}")
+
+    def step():
+        r.render_async(cam, W, H, D, rows, shard.data_ptr())
+        if world > 1:
+            dist.gather(shard, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                r.unpermute(gathered.data_ptr(), image.data_ptr(), W, H, BAND, world, R)
+
+    for _ in range(warmup):
+        step()
+    st = r.stats()  # syncs; ray counts of this rank's shard (identical every step)
+    r.kernel_times()  # drop warmup launches from the history
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ktimes = r.kernel_times(max(steps, 1))
+    kmean = sum(ktimes) / len(ktimes)
+    my_rays = st.rays
+    if world > 1:
+        t = torch.tensor([elapsed, kmean], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kmax = t.tolist()
+        n = torch.tensor([my_rays], dtype=torch.int64, device=f"cuda:{device}")
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        frame_rays = int(n.item())
+    else:
+        kmax = kmean
+        frame_rays = my_rays
+    r.close()
+    return {"scene": scene_name, "scene_file": scene_file, "W": W, "H": H, "D": D, "spheres": scene.num_spheres,
+            "lights": scene.num_lights, "frame_rays": frame_rays, "rank_rays": my_rays, "elapsed": elapsed,
+            "kernel_ms_mean": kmean, "kernel_ms_max_rank": kmax, "kernel_ms_min": min(ktimes),
+            "launches_timed": len(ktimes), "rows_per_rank": R}
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="synth200_1920x1080_d4", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-also", action="store_true", help="skip the complex.txt north-star line item")
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    import torch  # loads torch's HIP runtime first; librt_hip.so binds to it
+    import torch.distributed as dist
+    import rt_hip
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local)
+    also = {}
+    if not args.no_also and args.workload != "complex_1920x1080_d4":
+        a = measure(rt_hip, torch, dist, "complex_1920x1080_d4", max(args.steps // 2, 5), 2, world, rank, local)
+        also["complex_1920x1080_d4"] = {
+            "mrays_per_s": round(a["frame_rays"] * max(args.steps // 2, 5) / a["elapsed"] / 1e6, 2),
+            "ms_per_frame": round(a["elapsed"] / max(args.steps // 2, 5) * 1e3, 4),
+            "kernel_ms_mean": round(a["kernel_ms_mean"], 4), "rays_per_frame": a["frame_rays"],
+            "target_mrays_per_s": 1000}
+
+    if rank == 0:
+        value = m["frame_rays"] * args.steps / m["elapsed"] / 1e6
+        k_s = m["kernel_ms_mean"] * 1e-3
+        flops = FLOP_PER_TEST * m["spheres"] * m["rank_rays"]
+        achieved = flops / k_s / 1e12
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get(args.workload, {}).get("hbm_bytes_per_launch")
+        out_bytes = m["W"] * m["rows_per_rank"] * 3
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(m["elapsed"] / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: scenes/%s.txt (splitmix64 seed 420, SURVEY 8(d) generator) resident in HBM"
+                    % m["scene"] if m["scene"].startswith("synth") else "scenes/%s.txt" % m["scene"],
+            "config": {"workload": args.workload, "scene": m["scene"], "width": m["W"], "height": m["H"],
+                       "depth": m["D"], "spheres": m["spheres"], "lights": m["lights"],
+                       "rays_per_frame": m["frame_rays"],
+                       "parallelism": f"rows cyclic {BAND}-row bands x {world} GPU" +
+                                      (" + RCCL gather to rank 0" if world > 1 else "")},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 4),
+                         "traffic": traffic,
+                         "kernel": "rtk::render_kernel (fp64 VALU; no dense contraction, so no MFMA roof)",
+                         "per_launch": f"{FLOP_PER_TEST} FLOP x {m['spheres']} spheres x {m['rank_rays']} rays",
+                         "kernel_ms_mean": round(m["kernel_ms_mean"], 4),
+                         "kernel_ms_min": round(m["kernel_ms_min"], 4),
+                         "launches_timed": m["launches_timed"]},
+            "hbm_write": {"achieved": round(out_bytes / k_s / 1e9, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                          "frac": round(out_bytes / k_s / 1e9 / HBM_PEAK_GBPS, 6),
+                          "bytes_per_launch": out_bytes},
+            "also": also,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(m["scene_file"], m["W"], m["H"], m["D"], m["frame_rays"])
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

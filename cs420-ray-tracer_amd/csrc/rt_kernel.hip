@@ -300,7 +300,11 @@ struct rt_ctx {
   bool has_scene = false;
   unsigned long long *d_counters = nullptr;
   unsigned long long *h_counters = nullptr;  // pinned
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // In-stream HIP events around every render launch (a ring), so a caller can
+  // time a whole region of launches and read the per-launch durations after.
+  static constexpr int kRing = 256;
+  hipEvent_t ev0[kRing] = {}, ev1[kRing] = {};
+  long long launches = 0, hist_begin = 0;
   uint8_t *d_tmp = nullptr;
   size_t tmp_bytes = 0;
   std::string err;
@@ -355,7 +359,8 @@ int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_
 int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows &r, uint8_t *dst) {
   RT_TRY(c, hipSetDevice(c->device));
   RT_TRY(c, hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
-  RT_TRY(c, hipEventRecord(c->ev0, c->stream));
+  const int slot = (int)(c->launches % rt_ctx::kRing);
+  RT_TRY(c, hipEventRecord(c->ev0[slot], c->stream));
   if (r.count > 0) {
     Cam cam{cm->position[0], cm->position[1], cm->position[2], cm->forward[0], cm->forward[1], cm->forward[2],
             cm->right[0],    cm->right[1],    cm->right[2],    cm->up[0],      cm->up[1],      cm->up[2],
@@ -374,7 +379,8 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
     else launch_render<RT_MAX_DEPTH>(c, lds_geo, grid, lds, cam, W, H, depth, r, dst);
     RT_TRY(c, hipGetLastError());
   }
-  RT_TRY(c, hipEventRecord(c->ev1, c->stream));
+  RT_TRY(c, hipEventRecord(c->ev1[slot], c->stream));
+  c->launches++;
   RT_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                            c->stream));
   return RT_OK;
@@ -411,7 +417,8 @@ int rt_create(int device, rt_ctx **out) {
   if (hipHostMalloc(&c->h_counters, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
     return bail(RT_ERR_OUT_OF_MEMORY);
   std::memset(c->h_counters, 0, 4 * sizeof(unsigned long long));
-  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) return bail(RT_ERR_HIP);
+  for (int i = 0; i < rt_ctx::kRing; i++)
+    if (hipEventCreate(&c->ev0[i]) != hipSuccess || hipEventCreate(&c->ev1[i]) != hipSuccess) return bail(RT_ERR_HIP);
   *out = c;
   return RT_OK;
 }
@@ -425,8 +432,10 @@ void rt_destroy(rt_ctx *c) {
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->d_tmp) (void)hipFree(c->d_tmp);
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (int i = 0; i < rt_ctx::kRing; i++) {
+    if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
+    if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
+  }
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -492,7 +501,10 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
   RT_TRY(c, hipSetDevice(c->device));
   RT_TRY(c, hipStreamSynchronize(c->stream));
   float ms = 0.f;
-  RT_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  if (c->launches > 0) {
+    const int slot = (int)((c->launches - 1) % rt_ctx::kRing);
+    RT_TRY(c, hipEventElapsedTime(&ms, c->ev0[slot], c->ev1[slot]));
+  }
   st->rays_primary = c->h_counters[0];
   st->rays_shadow = c->h_counters[1];
   st->rays_reflect = c->h_counters[2];
@@ -526,6 +538,24 @@ int rt_render(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt
   rt_stats tmp;
   rc = rt_render_stats(c, st ? st : &tmp);
   return rc;
+}
+
+int rt_kernel_times(rt_ctx *c, double *ms_out, int max_n, int *n_out) {
+  if (!c || !n_out || max_n < 0 || (max_n > 0 && !ms_out)) return RT_ERR_INVALID_ARG;
+  RT_TRY(c, hipSetDevice(c->device));
+  RT_TRY(c, hipStreamSynchronize(c->stream));
+  long long avail = c->launches - c->hist_begin;
+  if (avail > rt_ctx::kRing) avail = rt_ctx::kRing;
+  if (avail > max_n) avail = max_n;
+  for (long long i = 0; i < avail; i++) {
+    const int slot = (int)((c->launches - avail + i) % rt_ctx::kRing);
+    float ms = 0.f;
+    RT_TRY(c, hipEventElapsedTime(&ms, c->ev0[slot], c->ev1[slot]));
+    ms_out[i] = ms;
+  }
+  *n_out = (int)avail;
+  c->hist_begin = c->launches;
+  return RT_OK;
 }
 
 int rt_unpermute_rows(rt_ctx *c, const uint8_t *gathered, uint8_t *image, int W, int H, int band, int G, int R) {

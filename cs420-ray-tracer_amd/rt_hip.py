@@ -88,6 +88,7 @@ SIGNATURES = {
                             C.c_int, C.POINTER(rt_stats)]),
     "rt_render_async": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.POINTER(rt_rows), _P]),
     "rt_render_stats": (C.c_int, [_P, C.POINTER(rt_stats)]),
+    "rt_kernel_times": (C.c_int, [_P, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int)]),
     "rt_unpermute_rows": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
 }
 
@@ -98,6 +99,14 @@ def lib(path: str = LIB_PATH):
     """Load librt_hip.so (raises if it has not been built)."""
     global _lib
     if _lib is None:
+        # torch bundles its own libamdhip64.so (SONAME libamdhip64.so.7).  If it
+        # is importable, load it first so the dynamic linker binds librt_hip.so
+        # to that same HIP runtime: two runtimes in one process cannot share
+        # the device (torch then reports "No HIP GPUs are available").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} missing: run __graft_entry__.build() (no CPU fallback exists)")
         L = C.CDLL(path)
@@ -233,6 +242,13 @@ class Renderer:
         st = rt_stats()
         _check(lib().rt_render_stats(self._ctx, C.byref(st)), "rt_render_stats", self._ctx)
         return st
+
+    def kernel_times(self, max_n: int = 256) -> list[float]:
+        """Per-launch kernel durations (ms) since the previous call (syncs the stream)."""
+        buf = (C.c_double * max_n)()
+        n = C.c_int(0)
+        _check(lib().rt_kernel_times(self._ctx, buf, max_n, C.byref(n)), "rt_kernel_times", self._ctx)
+        return list(buf[: n.value])
 
     def unpermute(self, gathered_ptr: int, image_ptr: int, width: int, height: int, band: int, shards: int,
                   rows_per_shard: int):

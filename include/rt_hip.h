@@ -16,6 +16,7 @@
  *                                      the OpenMP loop :185-199, and launch_gpu_kernel src/kernel.cu:185-200
  *   rt_render_async                 <- launch_gpu_kernel(..., cudaStream_t) src/kernel.cu:185-200
  *   rt_write_ppm                    <- write_ppm()            src/main.cpp:69-91
+ *   rt_kernel_times                 <- cudaEventElapsedTime around the kernel, src/main_gpu.cu:496-519
  *   rt_unpermute_rows               <- (new) reassembly of the multi-GPU row shards
  *
  * Errors: every call returns an rt_status (0 = ok); the library never exits
@@ -149,6 +150,11 @@ int rt_render(rt_ctx *ctx, const rt_camera *cam, int width, int height, int dept
 int rt_render_async(rt_ctx *ctx, const rt_camera *cam, int width, int height, int depth, const rt_rows *rows,
                     uint8_t *rgb_out_device);
 int rt_render_stats(rt_ctx *ctx, rt_stats *stats);
+
+/* Durations (ms, HIP events recorded in-stream around each render kernel) of
+ * the render launches issued since the previous call, oldest first, at most
+ * max_n (and at most the 256 most recent).  Waits for the context stream. */
+int rt_kernel_times(rt_ctx *ctx, double *ms_out, int max_n, int *n_out);
 
 /* Reassemble G shards gathered rank-major ([G][rows_per_rank][W][3], rank r
  * rendered with rt_rows{band, r, G, rows_per_rank}) into a PPM-ordered
