@@ -83,46 +83,166 @@ __device__ __forceinline__ bool intersect(const SphGeo &s, D3 o, D3 d, double a4
   return true;
 }
 
-// Scene::find_intersection (scene.h:41-61): all spheres in order, strict '<'.
-__device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, int n, D3 o, D3 d, double &best_t) {
+// ---------------------------------------------------------------------------
+// Wave-wide reductions.  Called only where all 64 lanes are active.
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ double wmax(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double o = __shfl_xor(v, off, 64);
+    v = (o > v) ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ double wmin(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double o = __shfl_xor(v, off, 64);
+    v = (o < v) ? o : v;
+  }
+  return v;
+}
+// Make a wave-uniform double live in SGPRs (the value is identical in every lane).
+__device__ __forceinline__ double uni(double v) {
+  unsigned long long b = __double_as_longlong(v);
+  unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+  unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// ---------------------------------------------------------------------------
+// Exact conservative culling of spheres per wave and per sweep.
+//
+// The active lanes' rays are treated as infinite LINES o_i + t d_i.  With a
+// reference point P (camera for primary rays, the light for shadow rays, an
+// active lane's origin for reflections), an axis a (normalised sum of the
+// d_i), theta = the widest line angle between any d_i and a, rho = the largest
+// distance from P to any line and `reach` = the largest |o_i - P|_1, every line
+// satisfies, for a sphere centre C with v = C - P:
+//     dist(C, line_i) >= |v x a| cos(theta) - |v . a| sin(theta) - rho.
+// A sphere is culled only when that lower bound exceeds r + m with the margin
+//     m = 1e-6 * (|v|_1 + r + reach).
+// The reference test (sphere.h:29-35) computes disc = 4|d|^2 (r^2 - dist'^2) + e
+// with |e| <= ~20 * 2^-53 * 4|d|^2 (2|oc|^2 + r^2) and dist' within 2^-53 |oc| of
+// dist, so dist >= r + m forces the computed disc < 0 with a margin of >100x:
+// every culled sphere is a miss for every active lane, in the reference's own
+// fp64 arithmetic -- including its disc == 0 (negative-root) quirk, which needs
+// disc == 0 exactly.  Candidates are still tested in file order with the exact
+// test, so closest-hit ties keep the lowest index.  NaN anywhere makes the
+// comparison false, i.e. keeps the sphere.  ("Culling".)
+struct Bound {
+  double px, py, pz, ax, ay, az, cos_t, sin_t, rho, reach;
+  bool cull;
+};
+
+__device__ __forceinline__ Bound make_bound(bool act, D3 o, D3 d, D3 P) {
+  Bound B;
+  double sx = wsum(act ? d.x : 0.0), sy = wsum(act ? d.y : 0.0), sz = wsum(act ? d.z : 0.0);
+  double len = __builtin_sqrt(sx * sx + sy * sy + sz * sz);
+  D3 a = (len > 0.0) ? mk(sx / len, sy / len, sz / len) : mk(1.0, 0.0, 0.0);
+  double ca = act ? __builtin_fabs(dot(d, a)) : 2.0;
+  D3 cr = mk(d.y * a.z - d.z * a.y, d.z * a.x - d.x * a.z, d.x * a.y - d.y * a.x);
+  double sa = act ? __builtin_sqrt(dot(cr, cr)) : 0.0;
+  D3 po = sub(P, o);
+  D3 pc = mk(po.y * d.z - po.z * d.y, po.z * d.x - po.x * d.z, po.x * d.y - po.y * d.x);
+  double rho = act ? __builtin_sqrt(dot(pc, pc)) : 0.0;
+  double reach = act ? __builtin_fabs(po.x) + __builtin_fabs(po.y) + __builtin_fabs(po.z) : 0.0;
+  B.px = uni(P.x);
+  B.py = uni(P.y);
+  B.pz = uni(P.z);
+  B.ax = uni(a.x);
+  B.ay = uni(a.y);
+  B.az = uni(a.z);
+  B.cos_t = uni(wmin(ca)) - 1e-9;
+  B.sin_t = uni(wmax(sa)) + 1e-9;
+  B.rho = uni(wmax(rho)) * (1.0 + 1e-9);
+  B.reach = uni(wmax(reach));
+  B.cull = B.cos_t > 0.0;
+  return B;
+}
+
+// True unless the sphere provably misses every active line (see above).
+__device__ __forceinline__ bool keep(const Bound &B, double cx, double cy, double cz, double r) {
+  double vx = cx - B.px, vy = cy - B.py, vz = cz - B.pz;
+  double va = __builtin_fabs(vx * B.ax + vy * B.ay + vz * B.az);
+  double wx = vy * B.az - vz * B.ay, wy = vz * B.ax - vx * B.az, wz = vx * B.ay - vy * B.ax;
+  double vp2 = wx * wx + wy * wy + wz * wz;
+  double m = 1e-6 * (__builtin_fabs(vx) + __builtin_fabs(vy) + __builtin_fabs(vz) + r + B.reach);
+  double rhs = r + B.rho + m + va * B.sin_t;
+  return !(B.cull && vp2 * (B.cos_t * B.cos_t) > rhs * rhs);
+}
+
+// Candidate mask of the 64 spheres [base, base+64) for this wave's bound.
+template <bool kCull>
+__device__ __forceinline__ unsigned long long candidates(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                                         int n, int base, const Bound &B) {
+  if (!kCull) {
+    const int cnt = n - base;
+    return cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull);
+  }
+  const int s = base + (int)(threadIdx.x & 63);
+  bool k = false;
+  if (s < n) {
+    const SphGeo q = g[s];
+    k = keep(B, q.cx, q.cy, q.cz, rad[s]);
+  }
+  return __ballot(k);
+}
+
+// Scene::find_intersection (scene.h:41-61): all candidate spheres in file
+// order, strict '<' (so ties keep the lowest index), t starts at 1e20.
+template <bool kCull>
+__device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
+                                             bool act, D3 o, D3 d, D3 P, double &best_t) {
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
   double bt = kInf;
   int bi = -1;
-  for (int i = 0; i < n; ++i) {
-    double t;
-    if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
-      bt = t;
-      bi = i;
+  Bound B;
+  if (kCull) B = make_bound(act, o, d, P);
+  for (int base = 0; base < n; base += 64) {
+    unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+    while (mask) {
+      const int i = base + __builtin_ctzll(mask);
+      mask &= mask - 1;
+      double t;
+      if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
+        bt = t;
+        bi = i;
+      }
     }
   }
   best_t = bt;
   return bi;
 }
 
-// Scene::in_shadow (scene.h:65-86) as an any-hit: some sphere with t < 1e20 and
-// t < dist.  Lanes stop testing once occluded; the wave leaves the sweep as
-// soon as the ballot of still-searching lanes is empty.
-__device__ __forceinline__ bool occluded(const SphGeo *__restrict__ g, int n, D3 o, D3 d, double dist) {
+// Scene::in_shadow (scene.h:65-86) as an any-hit over the candidates: some
+// sphere with t < 1e20 (the find_intersection start value) and t < dist.  The
+// wave leaves as soon as the ballot of still-unoccluded active lanes is empty.
+template <bool kCull>
+__device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
+                                             bool act, D3 o, D3 d, D3 P, double dist) {
+  if (__ballot(act) == 0) return false;
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
-  bool occ = false;
-  int i = 0;
-  for (; i + 4 <= n; i += 4) {
-    if (!occ) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        double t;
-        if (intersect(g[i + u], o, d, a4, a2, t) && t < kInf && t < dist) occ = true;
-      }
+  bool occ = !act;
+  Bound B;
+  if (kCull) B = make_bound(act, o, d, P);
+  for (int base = 0; base < n; base += 64) {
+    unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+    while (mask) {
+      const int i = base + __builtin_ctzll(mask);
+      mask &= mask - 1;
+      double t;
+      if (!occ && intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist) occ = true;
+      if (__ballot(!occ) == 0) return act;
     }
-    if (__ballot(!occ) == 0) return occ;
   }
-  for (; i < n; ++i) {
-    double t;
-    if (!occ && intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist) occ = true;
-  }
-  return occ;
+  return act && occ;
 }
 
 struct Cam {
@@ -131,79 +251,6 @@ struct Cam {
 struct Rows {
   int band, first, stride, count;
 };
-
-template <int MAXS>
-__device__ __forceinline__ D3 trace_pixel(const SphGeo *__restrict__ g, int n, const SphMat *__restrict__ mat,
-                                          const LightD *__restrict__ lights, int nl, D3 amb, D3 o, D3 d, int depth,
-                                          unsigned &c_shadow, unsigned &c_reflect) {
-  double stA[3][MAXS];
-  double stR[MAXS];
-  int lev = 0;
-  D3 res = mk(0.0, 0.0, 0.0);
-  int dleft = depth;
-  // depth <= 0 -> black (main.cpp:17-18)
-  while (dleft >= 1) {
-    double t;
-    int hi = closest_hit(g, n, o, d, t);
-    if (hi < 0) {  // sky, main.cpp:26-30
-      double st = 0.5 * (d.y + 1.0);
-      res = add(scale(mk(1.0, 1.0, 1.0), 1.0 - st), scale(mk(0.5, 0.7, 1.0), st));
-      break;
-    }
-    const SphGeo sg = g[hi];
-    const SphMat m = mat[hi];
-    D3 hit = add(o, scale(d, t));                             // main.cpp:32
-    D3 nrm = normalized(sub(hit, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
-    D3 view = normalized(sub(o, hit));                       // main.cpp:38
-    D3 mc = mk(m.cr, m.cg, m.cb);
-    D3 col = mul(amb, mc);                                   // scene.h:91
-    for (int l = 0; l < nl; ++l) {                           // scene.h:94-120
-      const LightD L = lights[l];
-      D3 lp = mk(L.px, L.py, L.pz);
-      D3 to_light = sub(lp, hit);
-      double dist = length(to_light);
-      D3 ldir = normalized(to_light);
-      ++c_shadow;
-      if (occluded(g, n, add(hit, scale(ldir, kEps)), normalized(ldir), dist)) continue;
-      double ndl = max0(dot(nrm, ldir));
-      D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
-      D3 nl2 = scale(ldir, -1.0);
-      D3 rdir = sub(nl2, scale(scale(nrm, 2.0), dot(nl2, nrm)));  // reflect(), vec3.h:31-33
-      double rdv = max0(dot(rdir, view));
-      double spec = pow(rdv, m.shin);
-      D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
-      col = add(add(specular, diffuse), col);                 // scene.h:117
-    }
-    if (m.refl > 0.0) {                                       // main.cpp:43-55
-      const double w = 1.0 - m.refl;
-      const D3 A = mk(col.x * w, col.y * w, col.z * w);
-      if (dleft - 1 >= 1) {  // host picks MAXS >= depth-1, so lev < MAXS here
-        stA[0][lev] = A.x;
-        stA[1][lev] = A.y;
-        stA[2][lev] = A.z;
-        stR[lev] = m.refl;
-        ++lev;
-        D3 rd = sub(d, scale(scale(nrm, 2.0), dot(d, nrm)));
-        o = add(hit, scale(nrm, kEps));
-        d = normalized(rd);
-        --dleft;
-        ++c_reflect;
-        continue;
-      }
-      // trace_ray(depth 0) is black (main.cpp:17-18): A + (0,0,0)*refl == A.
-      res = A;
-      break;
-    }
-    res = col;
-    break;
-  }
-  while (lev > 0) {  // unwind: shade*(1-refl) + reflected*refl, innermost first
-    --lev;
-    double r = stR[lev];
-    res = mk(stA[0][lev] + res.x * r, stA[1][lev] + res.y * r, stA[2][lev] + res.z * r);
-  }
-  return res;
-}
 
 __device__ __forceinline__ int quantize(double c) {
   double m = 255.99 * min1(c);  // main.cpp:85
@@ -217,42 +264,131 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
   return s;
 }
 
-template <int MAXS, bool kLdsGeo>
-__global__ __launch_bounds__(kBlock) void render_kernel(const SphGeo *__restrict__ geo, const SphMat *__restrict__ mat,
+// One lane per pixel; the whole wave walks the reflection levels together
+// (uniform control flow around every sweep, lanes masked by `alive`/`hit`).
+template <int MAXS, bool kLdsGeo, bool kCull>
+__global__ __launch_bounds__(kBlock) void render_kernel(const SphGeo *__restrict__ geo, const double *__restrict__ radius,
+                                                        const SphMat *__restrict__ mat,
                                                         const LightD *__restrict__ lights, int n, int nl, D3 amb,
                                                         Cam cam, int W, int H, int depth, Rows rows,
                                                         uint8_t *__restrict__ out,
                                                         unsigned long long *__restrict__ counters) {
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
   SphGeo *sgeo = reinterpret_cast<SphGeo *>(smem);
-  LightD *slight = reinterpret_cast<LightD *>(smem + (kLdsGeo ? (size_t)n * sizeof(SphGeo) : 0));
+  double *srad = reinterpret_cast<double *>(smem + (kLdsGeo ? (size_t)n * sizeof(SphGeo) : 0));
+  LightD *slight = reinterpret_cast<LightD *>(smem + (kLdsGeo ? (size_t)n * (sizeof(SphGeo) + sizeof(double)) : 0));
   const int tid = threadIdx.x;
   if (kLdsGeo)
-    for (int i = tid; i < n; i += kBlock) sgeo[i] = geo[i];
+    for (int i = tid; i < n; i += kBlock) {
+      sgeo[i] = geo[i];
+      srad[i] = radius[i];
+    }
   for (int i = tid; i < nl; i += kBlock) slight[i] = lights[i];
   __syncthreads();
-  const SphGeo *gsrc = kLdsGeo ? sgeo : geo;
+  const SphGeo *g = kLdsGeo ? sgeo : geo;
+  const double *rad = kLdsGeo ? srad : radius;
 
   const int wave = tid >> 6, lane = tid & 63;
   const int x = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
   const int k = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
-  unsigned c_prim = 0, c_shadow = 0, c_reflect = 0, c_neg = 0;
-  if (x < W && k < rows.count) {
-    const long long y = (long long)(k / rows.band) * rows.band * rows.stride + (long long)rows.first * rows.band +
-                        (k % rows.band);
+  const bool in_tile = x < W && k < rows.count;
+  const long long y = (long long)(k / rows.band) * rows.band * rows.stride + (long long)rows.first * rows.band +
+                      (k % rows.band);
+  const bool in_img = in_tile && y < H;
+
+  // Camera ray, camera.h:17-25 and main.cpp:151-154: ((u-0.5)*scale)*aspect, aspect = 1.0.
+  const int j = H - 1 - (int)(in_img ? y : 0);  // reference row (main.cpp:74)
+  const double u = (double)x / (W - 1), v = (double)j / (H - 1);
+  const double su = ((u - 0.5) * cam.scale) * 1.0, sv = (v - 0.5) * cam.scale;
+  D3 dir = add(add(mk(cam.fx, cam.fy, cam.fz), scale(mk(cam.rx, cam.ry, cam.rz), su)),
+               scale(mk(cam.ux, cam.uy, cam.uz), sv));
+  D3 d = normalized(normalized(dir));  // get_ray normalises, Ray() normalises again
+  D3 o = mk(cam.px, cam.py, cam.pz);
+  D3 P = o;
+
+  double stA[3][MAXS];
+  double stR[MAXS];
+  int lev = 0;
+  int dleft = depth;
+  D3 res = mk(0.0, 0.0, 0.0);     // depth <= 0 -> black (main.cpp:17-18)
+  bool alive = in_img && depth >= 1;
+  unsigned c_prim = alive ? 1u : 0u, c_shadow = 0, c_reflect = 0, c_neg = 0;
+
+  while (__ballot(alive)) {
+    double bt;
+    const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, P, bt);
+    const bool hit = alive && bi >= 0;
+    if (alive && !hit) {  // sky, main.cpp:26-30
+      const double st = 0.5 * (d.y + 1.0);
+      res = add(scale(mk(1.0, 1.0, 1.0), 1.0 - st), scale(mk(0.5, 0.7, 1.0), st));
+      alive = false;
+    }
+    const int hi = hit ? bi : 0;
+    const SphGeo sg = g[hi];
+    const SphMat m = mat[hi];
+    const D3 hp = add(o, scale(d, bt));                            // main.cpp:32
+    const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
+    const D3 view = normalized(sub(o, hp));                       // main.cpp:38
+    const D3 mc = mk(m.cr, m.cg, m.cb);
+    D3 col = mul(amb, mc);                                        // scene.h:91
+    for (int l = 0; l < nl; ++l) {                                // scene.h:94-120
+      const LightD L = slight[l];
+      const D3 lp = mk(L.px, L.py, L.pz);
+      const D3 to_light = sub(lp, hp);
+      const double dist = length(to_light);
+      const D3 ldir = normalized(to_light);
+      const bool occ = sweep_shadow<kCull>(g, rad, n, hit, add(hp, scale(ldir, kEps)), normalized(ldir), lp, dist);
+      if (hit && !occ) {
+        const double ndl = max0(dot(nrm, ldir));
+        const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
+        const D3 nl2 = scale(ldir, -1.0);
+        const D3 rdir = sub(nl2, scale(scale(nrm, 2.0), dot(nl2, nrm)));  // reflect(), vec3.h:31-33
+        const double rdv = max0(dot(rdir, view));
+        const double spec = pow(rdv, m.shin);
+        const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
+        col = add(add(specular, diffuse), col);                  // scene.h:117
+      }
+    }
+    if (hit) {
+      c_shadow += (unsigned)nl;
+      if (m.refl > 0.0) {                                         // main.cpp:43-55
+        const double w = 1.0 - m.refl;
+        const D3 A = mk(col.x * w, col.y * w, col.z * w);
+        if (dleft - 1 >= 1) {  // host picks MAXS >= depth-1, so lev < MAXS here
+          stA[0][lev] = A.x;
+          stA[1][lev] = A.y;
+          stA[2][lev] = A.z;
+          stR[lev] = m.refl;
+          ++lev;
+          const D3 rd = sub(d, scale(scale(nrm, 2.0), dot(d, nrm)));
+          o = add(hp, scale(nrm, kEps));
+          d = normalized(rd);
+          --dleft;
+          ++c_reflect;
+        } else {
+          res = A;  // trace_ray(depth 0) is black: A + (0,0,0)*refl == A
+          alive = false;
+        }
+      } else {
+        res = col;
+        alive = false;
+      }
+    }
+    const unsigned long long am = __ballot(alive);
+    if (am) {  // next reference point: the origin of the first still-alive lane
+      const int fl = __builtin_ctzll(am);
+      P = mk(__shfl(o.x, fl, 64), __shfl(o.y, fl, 64), __shfl(o.z, fl, 64));
+    }
+  }
+  while (lev > 0) {  // unwind: shade*(1-refl) + reflected*refl, innermost first
+    --lev;
+    const double r = stR[lev];
+    res = mk(stA[0][lev] + res.x * r, stA[1][lev] + res.y * r, stA[2][lev] + res.z * r);
+  }
+  if (in_tile) {
     uint8_t *px = out + ((size_t)k * W + x) * 3;
-    if (y < H) {
-      const int j = H - 1 - (int)y;  // reference row (main.cpp:74)
-      const double u = (double)x / (W - 1), v = (double)j / (H - 1);  // main.cpp:151-152
-      // camera.h:17-25: ((u-0.5)*scale)*aspect with aspect = 1.0
-      const double su = ((u - 0.5) * cam.scale) * 1.0, sv = (v - 0.5) * cam.scale;
-      D3 dir = add(add(mk(cam.fx, cam.fy, cam.fz), scale(mk(cam.rx, cam.ry, cam.rz), su)),
-                   scale(mk(cam.ux, cam.uy, cam.uz), sv));
-      D3 d = normalized(normalized(dir));  // get_ray normalises, Ray() normalises again
-      D3 o = mk(cam.px, cam.py, cam.pz);
-      if (depth >= 1) c_prim = 1;
-      D3 c = trace_pixel<MAXS>(gsrc, n, mat, slight, nl, amb, o, d, depth, c_shadow, c_reflect);
-      int q0 = quantize(c.x), q1 = quantize(c.y), q2 = quantize(c.z);
+    if (in_img) {
+      const int q0 = quantize(res.x), q1 = quantize(res.y), q2 = quantize(res.z);
       c_neg = (q0 < 0) + (q1 < 0) + (q2 < 0);
       px[0] = (uint8_t)(q0 < 0 ? 0 : q0);
       px[1] = (uint8_t)(q1 < 0 ? 0 : q1);
@@ -261,8 +397,8 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const SphGeo *__restrict
       px[0] = px[1] = px[2] = 0;
     }
   }
-  unsigned long long sp = wave_sum(c_prim), ss = wave_sum(c_shadow), sr = wave_sum(c_reflect),
-                     sn = wave_sum(c_neg);
+  const unsigned long long sp = wave_sum(c_prim), ss = wave_sum(c_shadow), sr = wave_sum(c_reflect),
+                           sn = wave_sum(c_neg);
   if (lane == 0) {
     if (sp) atomicAdd(&counters[0], sp);
     if (ss) atomicAdd(&counters[1], ss);
@@ -293,7 +429,9 @@ struct rt_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   SphGeo *d_geo = nullptr;
+  double *d_rad = nullptr;  // |radius|, for the conservative cull only
   SphMat *d_mat = nullptr;
+  bool cull = true;
   LightD *d_lights = nullptr;
   int nsph = 0, nlight = 0;
   double amb[3] = {0, 0, 0};
@@ -325,24 +463,35 @@ int fail(rt_ctx *c, hipError_t e, const char *what) {
 
 void free_scene(rt_ctx *c) {
   if (c->d_geo) (void)hipFree(c->d_geo);
+  if (c->d_rad) (void)hipFree(c->d_rad);
   if (c->d_mat) (void)hipFree(c->d_mat);
   if (c->d_lights) (void)hipFree(c->d_lights);
   c->d_geo = nullptr;
+  c->d_rad = nullptr;
   c->d_mat = nullptr;
   c->d_lights = nullptr;
   c->has_scene = false;
 }
 
+template <int MAXS, bool kCull>
+void launch_render2(rt_ctx *c, bool lds_geo, dim3 grid, size_t lds, const Cam &cam, int W, int H, int depth,
+                    const Rows &rows, uint8_t *out) {
+  D3 amb{c->amb[0], c->amb[1], c->amb[2]};
+  if (lds_geo)
+    hipLaunchKernelGGL((render_kernel<MAXS, true, kCull>), grid, dim3(kBlock), lds, c->stream, c->d_geo, c->d_rad,
+                       c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out, c->d_counters);
+  else
+    hipLaunchKernelGGL((render_kernel<MAXS, false, kCull>), grid, dim3(kBlock), lds, c->stream, c->d_geo, c->d_rad,
+                       c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out, c->d_counters);
+}
+
 template <int MAXS>
 void launch_render(rt_ctx *c, bool lds_geo, dim3 grid, size_t lds, const Cam &cam, int W, int H, int depth,
                    const Rows &rows, uint8_t *out) {
-  D3 amb{c->amb[0], c->amb[1], c->amb[2]};
-  if (lds_geo)
-    hipLaunchKernelGGL((render_kernel<MAXS, true>), grid, dim3(kBlock), lds, c->stream, c->d_geo, c->d_mat,
-                       c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out, c->d_counters);
+  if (c->cull)
+    launch_render2<MAXS, true>(c, lds_geo, grid, lds, cam, W, H, depth, rows, out);
   else
-    hipLaunchKernelGGL((render_kernel<MAXS, false>), grid, dim3(kBlock), lds, c->stream, c->d_geo, c->d_mat,
-                       c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out, c->d_counters);
+    launch_render2<MAXS, false>(c, lds_geo, grid, lds, cam, W, H, depth, rows, out);
 }
 
 int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_rows *rows, const void *out,
@@ -366,7 +515,8 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
             cm->right[0],    cm->right[1],    cm->right[2],    cm->up[0],      cm->up[1],      cm->up[2],
             cm->scale};
     dim3 grid((W + kTile - 1) / kTile, (r.count + kTile - 1) / kTile);
-    size_t geo_bytes = (size_t)c->nsph * sizeof(SphGeo), light_bytes = (size_t)c->nlight * sizeof(LightD);
+    size_t geo_bytes = (size_t)c->nsph * (sizeof(SphGeo) + sizeof(double)),
+           light_bytes = (size_t)c->nlight * sizeof(LightD);
     bool lds_geo = geo_bytes + light_bytes <= kLdsBudget;
     size_t lds = (lds_geo ? geo_bytes : 0) + light_bytes;
     if (lds > kLdsBudget) {
@@ -448,6 +598,12 @@ int rt_set_stream(rt_ctx *c, void *s) {
   return RT_OK;
 }
 
+int rt_set_culling(rt_ctx *c, int enable) {
+  if (!c) return RT_ERR_INVALID_ARG;
+  c->cull = enable != 0;
+  return RT_OK;
+}
+
 int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
   if (!c || !s || s->num_spheres < 0 || s->num_lights < 0) return RT_ERR_INVALID_ARG;
   if ((s->num_spheres > 0 && !s->spheres) || (s->num_lights > 0 && !s->lights)) return RT_ERR_INVALID_ARG;
@@ -456,11 +612,13 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
   free_scene(c);
   const int n = s->num_spheres, nl = s->num_lights;
   SphGeo *hg = new SphGeo[n + 1];
+  double *hr = new double[n + 1];
   SphMat *hm = new SphMat[n + 1];
   LightD *hl = new LightD[nl + 1];
   for (int i = 0; i < n; i++) {
     const rt_sphere &sp = s->spheres[i];
     hg[i] = SphGeo{sp.center[0], sp.center[1], sp.center[2], sp.radius * sp.radius};
+    hr[i] = sp.radius < 0 ? -sp.radius : sp.radius;
     hm[i] = SphMat{sp.color[0], sp.color[1], sp.color[2], sp.reflectivity, sp.shininess, 0.0};
   }
   for (int i = 0; i < nl; i++) {
@@ -470,9 +628,11 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
   int rc = RT_OK;
   hipError_t e = hipSuccess;
   if ((e = hipMalloc(&c->d_geo, sizeof(SphGeo) * (n + 1))) != hipSuccess ||
+      (e = hipMalloc(&c->d_rad, sizeof(double) * (n + 1))) != hipSuccess ||
       (e = hipMalloc(&c->d_mat, sizeof(SphMat) * (n + 1))) != hipSuccess ||
       (e = hipMalloc(&c->d_lights, sizeof(LightD) * (nl + 1))) != hipSuccess ||
       (e = hipMemcpy(c->d_geo, hg, sizeof(SphGeo) * n, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(c->d_rad, hr, sizeof(double) * n, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMemcpy(c->d_mat, hm, sizeof(SphMat) * n, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMemcpy(c->d_lights, hl, sizeof(LightD) * nl, hipMemcpyHostToDevice)) != hipSuccess) {
     rc = fail(c, e, "rt_upload_scene");
@@ -484,6 +644,7 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     c->has_scene = true;
   }
   delete[] hg;
+  delete[] hr;
   delete[] hm;
   delete[] hl;
   return rc;

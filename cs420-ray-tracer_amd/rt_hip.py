@@ -84,6 +84,7 @@ SIGNATURES = {
     "rt_last_error": (C.c_char_p, [_P]),
     "rt_set_stream": (C.c_int, [_P, _P]),
     "rt_upload_scene": (C.c_int, [_P, C.POINTER(rt_scene)]),
+    "rt_set_culling": (C.c_int, [_P, C.c_int]),
     "rt_render": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.POINTER(rt_rows), _P,
                             C.c_int, C.POINTER(rt_stats)]),
     "rt_render_async": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.POINTER(rt_rows), _P]),
@@ -215,6 +216,9 @@ class Renderer:
 
     def set_stream(self, stream_ptr: int | None):
         _check(lib().rt_set_stream(self._ctx, C.c_void_p(stream_ptr or 0)), "rt_set_stream", self._ctx)
+
+    def set_culling(self, enable: bool):
+        _check(lib().rt_set_culling(self._ctx, int(enable)), "rt_set_culling", self._ctx)
 
     def upload(self, scene: Scene):
         _check(lib().rt_upload_scene(self._ctx, C.byref(scene.raw)), "rt_upload_scene", self._ctx)

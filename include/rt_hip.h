@@ -134,6 +134,10 @@ const char *rt_last_error(const rt_ctx *ctx);
 /* Use an external stream (hipStream_t) for all work of this context; NULL
  * restores the context's own stream. */
 int rt_set_stream(rt_ctx *ctx, void *hip_stream);
+/* Per-wave conservative sphere culling (default on).  Off = every ray tests
+ * every sphere (the reference's brute-force sweep, scene.h:47-58).  Output
+ * bytes are identical either way; only the work differs. */
+int rt_set_culling(rt_ctx *ctx, int enable);
 /* Copies the scene into device memory owned by the context (replaces any
  * previous scene).  The host arrays may be freed afterwards. */
 int rt_upload_scene(rt_ctx *ctx, const rt_scene *scene);

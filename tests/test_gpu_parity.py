@@ -23,8 +23,15 @@ def _render(r, name, rows=None):
     return bytes(rgb), st, m
 
 
+@pytest.fixture(params=[True, False], ids=["cull", "brute"])
+def culling(request, gpu_renderer):
+    gpu_renderer.set_culling(request.param)
+    yield request.param
+    gpu_renderer.set_culling(True)
+
+
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
-def test_golden_byte_identical(gpu_renderer, name):
+def test_golden_byte_identical(gpu_renderer, culling, name):
     rgb, st, m = _render(gpu_renderer, name)
     want = golden_rgb(name)
     d = np.abs(np.frombuffer(rgb, np.uint8).astype(int) - np.frombuffer(want, np.uint8).astype(int))
@@ -206,3 +213,60 @@ def test_4k_shards_match_sampled_oracle_rows(gpu_renderer):
     for y in range(0, H, 97):
         rgb, _, _ = ref.render(W, H, D, band=1, first=y, stride=1, count=1)
         assert full[y].tobytes() == rgb, f"row {y}"
+
+
+def _random_scene(seed: int, n: int) -> str:
+    """Dense random scenes: tiny and huge spheres, spheres behind and around the
+    camera, the camera inside a sphere for some seeds, many lights."""
+    import random
+
+    rng = random.Random(seed)
+    lines = []
+    for _ in range(n):
+        r = rng.choice([0.01, 0.05, 0.2, 0.5, 1.0, 3.0]) * rng.uniform(0.5, 1.5)
+        lines.append("sphere %.6f %.6f %.6f %.6f %.3f %.3f %.3f %.2f 0.5 %d" % (
+            rng.uniform(-12, 12), rng.uniform(-8, 8), rng.uniform(-40, 10), r, rng.random(), rng.random(),
+            rng.random(), rng.choice([0.0, 0.0, 0.3, 0.7, 1.0]), rng.choice([1, 5, 20, 100])))
+    for _ in range(rng.randint(1, 6)):
+        lines.append("light %.3f %.3f %.3f %.3f %.3f %.3f 1" % (rng.uniform(-15, 15), rng.uniform(-5, 15),
+                                                               rng.uniform(-30, 10), rng.random(), rng.random(),
+                                                               rng.random()))
+    lines.append("ambient 0.1 0.1 0.1")
+    cz = rng.choice([5.0, 0.0, -10.0])
+    lines.append("camera %.3f %.3f %.3f 0 0 -20 %d" % (rng.uniform(-2, 2), rng.uniform(-1, 3), cz,
+                                                      rng.choice([30, 65, 120])))
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_dense_scenes_vs_oracle(gpu_renderer, seed):
+    import orc
+    import rt_hip
+
+    text = _random_scene(seed, 60 + 40 * seed)
+    W, H, D = 96, 64, 5
+    sc = rt_hip.Scene.parse(text)
+    gpu_renderer.upload(sc)
+    ref, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=4)
+    for cull in (True, False):
+        gpu_renderer.set_culling(cull)
+        rgb, st = gpu_renderer.render(sc.camera(), W, H, D)
+        assert bytes(rgb) == ref, (cull, diff_summary(bytes(rgb), ref))
+        assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
+                                                                       counts["reflect"])
+    gpu_renderer.set_culling(True)
+
+
+def test_cull_equals_bruteforce_at_4k(gpu_renderer):
+    import rt_hip
+
+    sc = rt_hip.Scene.load(scene_path("synth200"))
+    gpu_renderer.upload(sc)
+    a, sa = gpu_renderer.render(sc.camera(), 3840, 2160, 6)
+    gpu_renderer.set_culling(False)
+    try:
+        b, sb = gpu_renderer.render(sc.camera(), 3840, 2160, 6)
+    finally:
+        gpu_renderer.set_culling(True)
+    assert bytes(a) == bytes(b)
+    assert sa.rays == sb.rays
