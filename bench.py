@@ -89,12 +89,13 @@ def cpu_baseline(scene_file: str, W: int, H: int, D: int, rays_per_frame: int) -
             "sample": f"{what}; {W}x{H} d{D}, {rays} rays in {secs:.3f} s on 1 thread of {cpu_model()}"}
 
 
-def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device):
+def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, cull=True):
     scene_name, W, H, D = WORKLOADS[workload]
     scene_file = os.path.join(PKG, "scenes", scene_name + ".txt")
     scene = rt_hip.Scene.load(scene_file)
     cam = scene.camera()
     r = rt_hip.Renderer(device)
+    r.set_culling(cull)
     r.upload(scene)
     stream = torch.cuda.current_stream()
     r.set_stream(stream.cuda_stream)  # the kernel runs on torch's stream: events and RCCL order with it
@@ -155,6 +156,8 @@ def main():
     ap.add_argument("--workload", default="synth200_1920x1080_d4", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-also", action="store_true", help="skip the complex.txt north-star line item")
+    ap.add_argument("--brute-force", action="store_true",
+                    help="disable the exact per-wave sphere culling: every ray tests every sphere")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
@@ -166,10 +169,12 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
-    m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local)
+    cull = not args.brute_force
+    m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local, cull)
     also = {}
     if not args.no_also and args.workload != "complex_1920x1080_d4":
-        a = measure(rt_hip, torch, dist, "complex_1920x1080_d4", max(args.steps // 2, 5), 2, world, rank, local)
+        a = measure(rt_hip, torch, dist, "complex_1920x1080_d4", max(args.steps // 2, 5), 2, world, rank, local,
+                    cull)
         also["complex_1920x1080_d4"] = {
             "mrays_per_s": round(a["frame_rays"] * max(args.steps // 2, 5) / a["elapsed"] / 1e6, 2),
             "ms_per_frame": round(a["elapsed"] / max(args.steps // 2, 5) * 1e3, 4),
