@@ -46,6 +46,7 @@ WORKLOADS = {
     "synth10k_3840x2160_d6": ("synth10k", 3840, 2160, 6),   # cfg 5
 }
 FLOP_PER_TEST = 25          # A5 miss path: 3 sub + 5 (a) + 6 (b) + 7 (c) + 4 (disc), SURVEY 8(d)
+FLOP_PER_CULL = 34          # rtk::keep(): 3 sub, |v.a| 5, v x a 9, |v x a|^2 5, margin 5, rhs 4, compare 3
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X vector FP64 (spec; 256 CU x 2.4 GHz x 128 FLOP/clk)
 HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 BAND = 8
@@ -131,6 +132,7 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     ktimes = r.kernel_times(max(steps, 1))
     kmean = sum(ktimes) / len(ktimes)
     my_rays = st.rays
+    tests_exact, tests_cull = st.tests_exact, st.tests_cull
     if world > 1:
         t = torch.tensor([elapsed, kmean], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -145,7 +147,8 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     return {"scene": scene_name, "scene_file": scene_file, "W": W, "H": H, "D": D, "spheres": scene.num_spheres,
             "lights": scene.num_lights, "frame_rays": frame_rays, "rank_rays": my_rays, "elapsed": elapsed,
             "kernel_ms_mean": kmean, "kernel_ms_max_rank": kmax, "kernel_ms_min": min(ktimes),
-            "launches_timed": len(ktimes), "rows_per_rank": R}
+            "launches_timed": len(ktimes), "rows_per_rank": R, "tests_exact": tests_exact,
+            "tests_cull": tests_cull, "cull": cull}
 
 
 def main():
@@ -184,8 +187,10 @@ def main():
     if rank == 0:
         value = m["frame_rays"] * args.steps / m["elapsed"] / 1e6
         k_s = m["kernel_ms_mean"] * 1e-3
-        flops = FLOP_PER_TEST * m["spheres"] * m["rank_rays"]
+        # executed work of one launch (device counters), not the brute-force count
+        flops = FLOP_PER_TEST * m["tests_exact"] + FLOP_PER_CULL * m["tests_cull"]
         achieved = flops / k_s / 1e12
+        brute = FLOP_PER_TEST * m["spheres"] * m["rank_rays"] / k_s / 1e12
         traffic = None
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
@@ -215,7 +220,11 @@ def main():
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 4),
                          "traffic": traffic,
                          "kernel": "rtk::render_kernel (fp64 VALU; no dense contraction, so no MFMA roof)",
-                         "per_launch": f"{FLOP_PER_TEST} FLOP x {m['spheres']} spheres x {m['rank_rays']} rays",
+                         "per_launch": f"{FLOP_PER_TEST} FLOP x {m['tests_exact']} exact ray-sphere tests + "
+                                       f"{FLOP_PER_CULL} FLOP x {m['tests_cull']} sphere-bound cull tests",
+                         "culling": m["cull"],
+                         "brute_force_equivalent_tflops": round(brute, 3),
+                         "brute_force_tests": m["spheres"] * m["rank_rays"],
                          "kernel_ms_mean": round(m["kernel_ms_mean"], 4),
                          "kernel_ms_min": round(m["kernel_ms_min"], 4),
                          "launches_timed": m["launches_timed"]},

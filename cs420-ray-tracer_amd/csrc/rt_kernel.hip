@@ -33,6 +33,7 @@ constexpr double kSpec = 0.5;   // scene.h:38
 constexpr int kBlock = 256;
 constexpr int kTile = 16;       // workgroup tile edge (pixels)
 constexpr size_t kLdsBudget = 64 * 1024;
+constexpr int kCounters = 6;  // primary, shadow, reflect, negative, exact tests, cull tests
 
 struct __attribute__((aligned(32))) SphGeo {
   double cx, cy, cz, rr;  // rr = radius*radius, rounded once on the host as sphere.h:33 does
@@ -195,17 +196,26 @@ __device__ __forceinline__ unsigned long long candidates(const SphGeo *__restric
 
 // Scene::find_intersection (scene.h:41-61): all candidate spheres in file
 // order, strict '<' (so ties keep the lowest index), t starts at 1e20.
+// Work counters (wave-uniform): n_exact = exact ray-sphere tests executed for
+// live lanes; n_cull = sphere-vs-bound tests (one per sphere per wave sweep).
+struct Work {
+  unsigned long long exact = 0, cull = 0;
+};
+
 template <bool kCull>
 __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
-                                             bool act, D3 o, D3 d, D3 P, double &best_t) {
+                                             bool act, D3 o, D3 d, D3 P, double &best_t, Work &work) {
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
   double bt = kInf;
   int bi = -1;
+  const unsigned live = (unsigned)__popcll(__ballot(act));
   Bound B;
   if (kCull) B = make_bound(act, o, d, P);
   for (int base = 0; base < n; base += 64) {
     unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+    if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
+    work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
     while (mask) {
       const int i = base + __builtin_ctzll(mask);
       mask &= mask - 1;
@@ -225,8 +235,9 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
 // wave leaves as soon as the ballot of still-unoccluded active lanes is empty.
 template <bool kCull>
 __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
-                                             bool act, D3 o, D3 d, D3 P, double dist) {
-  if (__ballot(act) == 0) return false;
+                                             bool act, D3 o, D3 d, D3 P, double dist, Work &work) {
+  unsigned long long live = __ballot(act);
+  if (live == 0) return false;
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
   bool occ = !act;
@@ -234,12 +245,15 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
   if (kCull) B = make_bound(act, o, d, P);
   for (int base = 0; base < n; base += 64) {
     unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+    if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
     while (mask) {
       const int i = base + __builtin_ctzll(mask);
       mask &= mask - 1;
       double t;
+      work.exact += (unsigned)__popcll(live);
       if (!occ && intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist) occ = true;
-      if (__ballot(!occ) == 0) return act;
+      live = __ballot(!occ);
+      if (live == 0) return act;
     }
   }
   return act && occ;
@@ -313,10 +327,11 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const SphGeo *__restrict
   D3 res = mk(0.0, 0.0, 0.0);     // depth <= 0 -> black (main.cpp:17-18)
   bool alive = in_img && depth >= 1;
   unsigned c_prim = alive ? 1u : 0u, c_shadow = 0, c_reflect = 0, c_neg = 0;
+  Work work;
 
   while (__ballot(alive)) {
     double bt;
-    const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, P, bt);
+    const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, P, bt, work);
     const bool hit = alive && bi >= 0;
     if (alive && !hit) {  // sky, main.cpp:26-30
       const double st = 0.5 * (d.y + 1.0);
@@ -337,7 +352,8 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const SphGeo *__restrict
       const D3 to_light = sub(lp, hp);
       const double dist = length(to_light);
       const D3 ldir = normalized(to_light);
-      const bool occ = sweep_shadow<kCull>(g, rad, n, hit, add(hp, scale(ldir, kEps)), normalized(ldir), lp, dist);
+      const bool occ =
+          sweep_shadow<kCull>(g, rad, n, hit, add(hp, scale(ldir, kEps)), normalized(ldir), lp, dist, work);
       if (hit && !occ) {
         const double ndl = max0(dot(nrm, ldir));
         const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
@@ -404,6 +420,8 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const SphGeo *__restrict
     if (ss) atomicAdd(&counters[1], ss);
     if (sr) atomicAdd(&counters[2], sr);
     if (sn) atomicAdd(&counters[3], sn);
+    if (work.exact) atomicAdd(&counters[4], work.exact);
+    if (work.cull) atomicAdd(&counters[5], work.cull);
   }
 }
 
@@ -507,7 +525,7 @@ int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_
 
 int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows &r, uint8_t *dst) {
   RT_TRY(c, hipSetDevice(c->device));
-  RT_TRY(c, hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+  RT_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounters * sizeof(unsigned long long), c->stream));
   const int slot = (int)(c->launches % rt_ctx::kRing);
   RT_TRY(c, hipEventRecord(c->ev0[slot], c->stream));
   if (r.count > 0) {
@@ -531,7 +549,7 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
   }
   RT_TRY(c, hipEventRecord(c->ev1[slot], c->stream));
   c->launches++;
-  RT_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+  RT_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounters * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                            c->stream));
   return RT_OK;
 }
@@ -563,10 +581,10 @@ int rt_create(int device, rt_ctx **out) {
   if (hipSetDevice(device) != hipSuccess) return bail(RT_ERR_HIP);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(RT_ERR_HIP);
   c->stream = c->own_stream;
-  if (hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess) return bail(RT_ERR_OUT_OF_MEMORY);
-  if (hipHostMalloc(&c->h_counters, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+  if (hipMalloc(&c->d_counters, kCounters * sizeof(unsigned long long)) != hipSuccess) return bail(RT_ERR_OUT_OF_MEMORY);
+  if (hipHostMalloc(&c->h_counters, kCounters * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
     return bail(RT_ERR_OUT_OF_MEMORY);
-  std::memset(c->h_counters, 0, 4 * sizeof(unsigned long long));
+  std::memset(c->h_counters, 0, kCounters * sizeof(unsigned long long));
   for (int i = 0; i < rt_ctx::kRing; i++)
     if (hipEventCreate(&c->ev0[i]) != hipSuccess || hipEventCreate(&c->ev1[i]) != hipSuccess) return bail(RT_ERR_HIP);
   *out = c;
@@ -670,6 +688,8 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
   st->rays_shadow = c->h_counters[1];
   st->rays_reflect = c->h_counters[2];
   st->negative_clamped = c->h_counters[3];
+  st->tests_exact = c->h_counters[4];
+  st->tests_cull = c->h_counters[5];
   st->kernel_ms = ms;
   return RT_OK;
 }

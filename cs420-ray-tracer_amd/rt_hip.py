@@ -57,11 +57,13 @@ class rt_rows(C.Structure):
 
 class rt_stats(C.Structure):
     _fields_ = [("rays_primary", C.c_uint64), ("rays_shadow", C.c_uint64), ("rays_reflect", C.c_uint64),
-                ("negative_clamped", C.c_uint64), ("kernel_ms", C.c_double)]
+                ("negative_clamped", C.c_uint64), ("kernel_ms", C.c_double), ("tests_exact", C.c_uint64),
+                ("tests_cull", C.c_uint64)]
 
     def as_dict(self):
         return {"primary": self.rays_primary, "shadow": self.rays_shadow, "reflect": self.rays_reflect,
-                "negative": self.negative_clamped, "kernel_ms": self.kernel_ms}
+                "negative": self.negative_clamped, "kernel_ms": self.kernel_ms, "tests_exact": self.tests_exact,
+                "tests_cull": self.tests_cull}
 
     @property
     def rays(self) -> int:

@@ -112,6 +112,8 @@ typedef struct rt_stats {
     uint64_t rays_reflect;
     uint64_t negative_clamped; /* channels whose int(255.99*min(1,c)) < 0, stored as 0 */
     double kernel_ms;
+    uint64_t tests_exact;      /* exact ray-sphere tests executed (sphere.h:26-59), live lanes only */
+    uint64_t tests_cull;       /* sphere-vs-wave-bound tests (one per sphere per wave sweep) */
 } rt_stats;
 
 typedef struct rt_ctx rt_ctx;
