@@ -18,6 +18,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -31,7 +32,6 @@ constexpr double kEps = 0.001;  // ray_math_constants.h:22
 constexpr double kInf = 1e20;   // ray_math_constants.h:23
 constexpr double kSpec = 0.5;   // scene.h:38
 constexpr int kBlock = 256;
-constexpr int kTile = 16;       // workgroup tile edge (pixels)
 constexpr size_t kLdsBudget = 64 * 1024;
 constexpr int kCounters = 6;  // primary, shadow, reflect, negative, exact tests, cull tests
 
@@ -120,49 +120,64 @@ __device__ __forceinline__ double uni(double v) {
 //
 // The active lanes' rays are treated as infinite LINES o_i + t d_i.  With a
 // reference point P (camera for primary rays, the light for shadow rays, an
-// active lane's origin for reflections), an axis a (normalised sum of the
-// d_i), theta = the widest line angle between any d_i and a, rho = the largest
-// distance from P to any line and `reach` = the largest |o_i - P|_1, every line
-// satisfies, for a sphere centre C with v = C - P:
-//     dist(C, line_i) >= |v x a| cos(theta) - |v . a| sin(theta) - rho.
-// A sphere is culled only when that lower bound exceeds r + m with the margin
-//     m = 1e-6 * (|v|_1 + r + reach).
+// active lane's origin for reflections) and a unit axis a (from the first and
+// last active lanes' directions), let theta be the widest line angle between
+// any d_i and a, rho_i the distance from P to line i and reach_i = |o_i - P|_1.
+// For a sphere centre C with v = C - P every line satisfies
+//     dist(C, line_i) >= |v x a| cos(theta) - |v . a| sin(theta) - rho_i.
+// A sphere is culled only when that bound exceeds r + m_i for every lane, with
+//     m_i = 1e-6 * (|v|_1 + r + reach_i)   (so |oc_i| <= |v|_1 + reach_i).
 // The reference test (sphere.h:29-35) computes disc = 4|d|^2 (r^2 - dist'^2) + e
 // with |e| <= ~20 * 2^-53 * 4|d|^2 (2|oc|^2 + r^2) and dist' within 2^-53 |oc| of
-// dist, so dist >= r + m forces the computed disc < 0 with a margin of >100x:
-// every culled sphere is a miss for every active lane, in the reference's own
-// fp64 arithmetic -- including its disc == 0 (negative-root) quirk, which needs
+// dist, so dist >= r + m forces the computed disc < 0 with >100x slack: every
+// culled sphere is a miss for every active lane in the reference's own fp64
+// arithmetic -- including its disc == 0 (negative-root) quirk, which needs
 // disc == 0 exactly.  Candidates are still tested in file order with the exact
 // test, so closest-hit ties keep the lowest index.  NaN anywhere makes the
-// comparison false, i.e. keeps the sphere.  ("Culling".)
+// comparison false, i.e. keeps the sphere.  Two wave reductions per sweep:
+// max sin^2(theta_i) and max slack_i = |po x d|_1 + 1e-6 reach_i
+// (|po x d|_1 >= rho_i |d|, |d| = 1 +- 2^-52).  ("Culling".)
 struct Bound {
-  double px, py, pz, ax, ay, az, cos_t, sin_t, rho, reach;
+  double px, py, pz, ax, ay, az, cos2, sin_t, slack;
   bool cull;
 };
 
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+  unsigned long long b = __double_as_longlong(v);
+  unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+  unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
 __device__ __forceinline__ Bound make_bound(bool act, D3 o, D3 d, D3 P) {
   Bound B;
-  double sx = wsum(act ? d.x : 0.0), sy = wsum(act ? d.y : 0.0), sz = wsum(act ? d.z : 0.0);
+  const unsigned long long am = __ballot(act);
+  const int l0 = __builtin_ctzll(am), l1 = 63 - __builtin_clzll(am);
+  double sx = lane_bcast(d.x, l0) + lane_bcast(d.x, l1);
+  double sy = lane_bcast(d.y, l0) + lane_bcast(d.y, l1);
+  double sz = lane_bcast(d.z, l0) + lane_bcast(d.z, l1);
   double len = __builtin_sqrt(sx * sx + sy * sy + sz * sz);
   D3 a = (len > 0.0) ? mk(sx / len, sy / len, sz / len) : mk(1.0, 0.0, 0.0);
-  double ca = act ? __builtin_fabs(dot(d, a)) : 2.0;
   D3 cr = mk(d.y * a.z - d.z * a.y, d.z * a.x - d.x * a.z, d.x * a.y - d.y * a.x);
-  double sa = act ? __builtin_sqrt(dot(cr, cr)) : 0.0;
+  double s2 = act ? dot(cr, cr) : 0.0;
   D3 po = sub(P, o);
   D3 pc = mk(po.y * d.z - po.z * d.y, po.z * d.x - po.x * d.z, po.x * d.y - po.y * d.x);
-  double rho = act ? __builtin_sqrt(dot(pc, pc)) : 0.0;
-  double reach = act ? __builtin_fabs(po.x) + __builtin_fabs(po.y) + __builtin_fabs(po.z) : 0.0;
+  double slack = act ? (__builtin_fabs(pc.x) + __builtin_fabs(pc.y) + __builtin_fabs(pc.z)) * (1.0 + 1e-9) +
+                           1e-6 * (__builtin_fabs(po.x) + __builtin_fabs(po.y) + __builtin_fabs(po.z))
+                     : 0.0;
+  const double s2max = uni(wmax(s2));
+  B.slack = uni(wmax(slack));
   B.px = uni(P.x);
   B.py = uni(P.y);
   B.pz = uni(P.z);
   B.ax = uni(a.x);
   B.ay = uni(a.y);
   B.az = uni(a.z);
-  B.cos_t = uni(wmin(ca)) - 1e-9;
-  B.sin_t = uni(wmax(sa)) + 1e-9;
-  B.rho = uni(wmax(rho)) * (1.0 + 1e-9);
-  B.reach = uni(wmax(reach));
-  B.cull = B.cos_t > 0.0;
+  // theta from the widest sine; 1e-9 covers the rounding of |a|, |d_i| and the products.
+  B.sin_t = __builtin_sqrt(s2max) + 1e-9;
+  const double c = __builtin_sqrt(1.0 - (s2max < 1.0 ? s2max : 1.0)) - 1e-9;
+  B.cos2 = c * c;
+  B.cull = c > 0.0 && B.sin_t < 1.0;
   return B;
 }
 
@@ -172,9 +187,9 @@ __device__ __forceinline__ bool keep(const Bound &B, double cx, double cy, doubl
   double va = __builtin_fabs(vx * B.ax + vy * B.ay + vz * B.az);
   double wx = vy * B.az - vz * B.ay, wy = vz * B.ax - vx * B.az, wz = vx * B.ay - vy * B.ax;
   double vp2 = wx * wx + wy * wy + wz * wz;
-  double m = 1e-6 * (__builtin_fabs(vx) + __builtin_fabs(vy) + __builtin_fabs(vz) + r + B.reach);
-  double rhs = r + B.rho + m + va * B.sin_t;
-  return !(B.cull && vp2 * (B.cos_t * B.cos_t) > rhs * rhs);
+  double m = 1e-6 * (__builtin_fabs(vx) + __builtin_fabs(vy) + __builtin_fabs(vz) + r);
+  double rhs = r + B.slack + m + va * B.sin_t;
+  return !(B.cull && vp2 * B.cos2 > rhs * rhs);
 }
 
 // Candidate mask of the 64 spheres [base, base+64) for this wave's bound.
@@ -280,8 +295,11 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
 
 // One lane per pixel; the whole wave walks the reflection levels together
 // (uniform control flow around every sweep, lanes masked by `alive`/`hit`).
-template <int MAXS, bool kLdsGeo, bool kCull>
-__global__ __launch_bounds__(kBlock) void render_kernel(const SphGeo *__restrict__ geo, const double *__restrict__ radius,
+#ifndef RT_MIN_WAVES_PER_EU
+#define RT_MIN_WAVES_PER_EU 1
+#endif
+template <int MAXS, bool kLdsGeo, bool kCull, int kWaves>
+__global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kernel(const SphGeo *__restrict__ geo, const double *__restrict__ radius,
                                                         const SphMat *__restrict__ mat,
                                                         const LightD *__restrict__ lights, int n, int nl, D3 amb,
                                                         Cam cam, int W, int H, int depth, Rows rows,
@@ -292,19 +310,22 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const SphGeo *__restrict
   double *srad = reinterpret_cast<double *>(smem + (kLdsGeo ? (size_t)n * sizeof(SphGeo) : 0));
   LightD *slight = reinterpret_cast<LightD *>(smem + (kLdsGeo ? (size_t)n * (sizeof(SphGeo) + sizeof(double)) : 0));
   const int tid = threadIdx.x;
+  constexpr int kThreads = 64 * kWaves;
   if (kLdsGeo)
-    for (int i = tid; i < n; i += kBlock) {
+    for (int i = tid; i < n; i += kThreads) {
       sgeo[i] = geo[i];
       srad[i] = radius[i];
     }
-  for (int i = tid; i < nl; i += kBlock) slight[i] = lights[i];
+  for (int i = tid; i < nl; i += kThreads) slight[i] = lights[i];
   __syncthreads();
   const SphGeo *g = kLdsGeo ? sgeo : geo;
   const double *rad = kLdsGeo ? srad : radius;
 
+  // Workgroup = kWaves waves, each an 8x8 pixel tile (2x2 waves for kWaves = 4).
+  constexpr int kWx = kWaves == 4 ? 2 : 1;
   const int wave = tid >> 6, lane = tid & 63;
-  const int x = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
-  const int k = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
+  const int x = blockIdx.x * (8 * kWx) + (wave % kWx) * 8 + (lane & 7);
+  const int k = blockIdx.y * (8 * (kWaves / kWx)) + (wave / kWx) * 8 + (lane >> 3);
   const bool in_tile = x < W && k < rows.count;
   const long long y = (long long)(k / rows.band) * rows.band * rows.stride + (long long)rows.first * rows.band +
                       (k % rows.band);
@@ -360,7 +381,8 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const SphGeo *__restrict
         const D3 nl2 = scale(ldir, -1.0);
         const D3 rdir = sub(nl2, scale(scale(nrm, 2.0), dot(nl2, nrm)));  // reflect(), vec3.h:31-33
         const double rdv = max0(dot(rdir, view));
-        const double spec = pow(rdv, m.shin);
+        // pow(+0, y > 0) is +0 exactly (C99 F.10.4.4), so most lanes skip ocml's pow.
+        const double spec = (rdv == 0.0 && m.shin > 0.0) ? 0.0 : pow(rdv, m.shin);
         const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
         col = add(add(specular, diffuse), col);                  // scene.h:117
       }
@@ -450,6 +472,7 @@ struct rt_ctx {
   double *d_rad = nullptr;  // |radius|, for the conservative cull only
   SphMat *d_mat = nullptr;
   bool cull = true;
+  int wg_waves = 1;  // waves per workgroup (tuning knob RT_HIP_WG_WAVES = 1 | 4)
   LightD *d_lights = nullptr;
   int nsph = 0, nlight = 0;
   double amb[3] = {0, 0, 0};
@@ -491,25 +514,32 @@ void free_scene(rt_ctx *c) {
   c->has_scene = false;
 }
 
-template <int MAXS, bool kCull>
-void launch_render2(rt_ctx *c, bool lds_geo, dim3 grid, size_t lds, const Cam &cam, int W, int H, int depth,
-                    const Rows &rows, uint8_t *out) {
+template <int MAXS, bool kCull, int kWaves>
+void launch_render3(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
+                    uint8_t *out) {
+  constexpr int kWx = kWaves == 4 ? 2 : 1, kWy = kWaves / kWx;
+  dim3 grid((W + 8 * kWx - 1) / (8 * kWx), (rows.count + 8 * kWy - 1) / (8 * kWy));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   if (lds_geo)
-    hipLaunchKernelGGL((render_kernel<MAXS, true, kCull>), grid, dim3(kBlock), lds, c->stream, c->d_geo, c->d_rad,
-                       c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out, c->d_counters);
+    hipLaunchKernelGGL((render_kernel<MAXS, true, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
+                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out,
+                       c->d_counters);
   else
-    hipLaunchKernelGGL((render_kernel<MAXS, false, kCull>), grid, dim3(kBlock), lds, c->stream, c->d_geo, c->d_rad,
-                       c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out, c->d_counters);
+    hipLaunchKernelGGL((render_kernel<MAXS, false, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
+                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out,
+                       c->d_counters);
 }
 
 template <int MAXS>
-void launch_render(rt_ctx *c, bool lds_geo, dim3 grid, size_t lds, const Cam &cam, int W, int H, int depth,
-                   const Rows &rows, uint8_t *out) {
-  if (c->cull)
-    launch_render2<MAXS, true>(c, lds_geo, grid, lds, cam, W, H, depth, rows, out);
-  else
-    launch_render2<MAXS, false>(c, lds_geo, grid, lds, cam, W, H, depth, rows, out);
+void launch_render(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
+                   uint8_t *out) {
+  if (c->cull) {
+    if (c->wg_waves == 4) launch_render3<MAXS, true, 4>(c, lds_geo, lds, cam, W, H, depth, rows, out);
+    else launch_render3<MAXS, true, 1>(c, lds_geo, lds, cam, W, H, depth, rows, out);
+  } else {
+    if (c->wg_waves == 4) launch_render3<MAXS, false, 4>(c, lds_geo, lds, cam, W, H, depth, rows, out);
+    else launch_render3<MAXS, false, 1>(c, lds_geo, lds, cam, W, H, depth, rows, out);
+  }
 }
 
 int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_rows *rows, const void *out,
@@ -532,7 +562,6 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
     Cam cam{cm->position[0], cm->position[1], cm->position[2], cm->forward[0], cm->forward[1], cm->forward[2],
             cm->right[0],    cm->right[1],    cm->right[2],    cm->up[0],      cm->up[1],      cm->up[2],
             cm->scale};
-    dim3 grid((W + kTile - 1) / kTile, (r.count + kTile - 1) / kTile);
     size_t geo_bytes = (size_t)c->nsph * (sizeof(SphGeo) + sizeof(double)),
            light_bytes = (size_t)c->nlight * sizeof(LightD);
     bool lds_geo = geo_bytes + light_bytes <= kLdsBudget;
@@ -542,9 +571,9 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
       return RT_ERR_INVALID_ARG;
     }
     int stack = depth - 1;
-    if (stack <= 4) launch_render<4>(c, lds_geo, grid, lds, cam, W, H, depth, r, dst);
-    else if (stack <= 16) launch_render<16>(c, lds_geo, grid, lds, cam, W, H, depth, r, dst);
-    else launch_render<RT_MAX_DEPTH>(c, lds_geo, grid, lds, cam, W, H, depth, r, dst);
+    if (stack <= 4) launch_render<4>(c, lds_geo, lds, cam, W, H, depth, r, dst);
+    else if (stack <= 16) launch_render<16>(c, lds_geo, lds, cam, W, H, depth, r, dst);
+    else launch_render<RT_MAX_DEPTH>(c, lds_geo, lds, cam, W, H, depth, r, dst);
     RT_TRY(c, hipGetLastError());
   }
   RT_TRY(c, hipEventRecord(c->ev1[slot], c->stream));
@@ -574,6 +603,7 @@ int rt_create(int device, rt_ctx **out) {
   if (device < 0 || device >= n) return RT_ERR_INVALID_ARG;
   rt_ctx *c = new rt_ctx();
   c->device = device;
+  if (const char *e = std::getenv("RT_HIP_WG_WAVES")) c->wg_waves = std::atoi(e) == 4 ? 4 : 1;
   auto bail = [&](int rc) {
     rt_destroy(c);
     return rc;

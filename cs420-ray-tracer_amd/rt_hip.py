@@ -18,7 +18,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librt_hip.so")
+# RT_HIP_LIB selects an alternative build of the same ABI (tuning experiments).
+LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(HERE, "librt_hip.so")
 
 RT_MAX_DEPTH = 64
 
