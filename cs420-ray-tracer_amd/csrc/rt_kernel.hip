@@ -20,278 +20,17 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <string>
 
 #include "rt_hip.h"
 
 #pragma clang fp contract(off)
 
+#include "rt_device.h"
+#include "rt_wavefront.h"
+
 namespace rtk {
-
-constexpr double kEps = 0.001;  // ray_math_constants.h:22
-constexpr double kInf = 1e20;   // ray_math_constants.h:23
-constexpr double kSpec = 0.5;   // scene.h:38
-constexpr int kBlock = 256;
-constexpr size_t kLdsBudget = 64 * 1024;
-constexpr int kCounters = 6;  // primary, shadow, reflect, negative, exact tests, cull tests
-
-struct __attribute__((aligned(32))) SphGeo {
-  double cx, cy, cz, rr;  // rr = radius*radius, rounded once on the host as sphere.h:33 does
-};
-struct SphMat {
-  double cr, cg, cb, refl, shin, pad;
-};
-struct LightD {
-  double px, py, pz, cr, cg, cb;
-};
-
-struct D3 {
-  double x, y, z;
-};
-__device__ __forceinline__ D3 mk(double x, double y, double z) { return D3{x, y, z}; }
-__device__ __forceinline__ D3 add(D3 a, D3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ D3 sub(D3 a, D3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ D3 mul(D3 a, D3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ D3 scale(D3 a, double t) { return mk(a.x * t, a.y * t, a.z * t); }
-__device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ double length(D3 a) { return __builtin_sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
-__device__ __forceinline__ D3 normalized(D3 a) {
-  double len = length(a);
-  return mk(a.x / len, a.y / len, a.z / len);
-}
-__device__ __forceinline__ double max0(double x) { return (0.0 < x) ? x : 0.0; }  // std::max(0.0, x)
-__device__ __forceinline__ double min1(double x) { return (x < 1.0) ? x : 1.0; }  // std::min(1.0, x)
-
-// Sphere::intersect (sphere.h:26-59) for a ray whose a = dot(d,d) is hoisted:
-// a4 = 4*a, a2 = 2*a (both exact scalings).  Returns true and t on a hit.
-__device__ __forceinline__ bool intersect(const SphGeo &s, D3 o, D3 d, double a4, double a2, double &t) {
-  double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
-  double b = 2.0 * ((ocx * d.x + ocy * d.y) + ocz * d.z);
-  double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.rr;
-  double disc = b * b - a4 * c;
-  if (!(disc >= 0.0)) return false;  // disc < 0 -> miss; a NaN disc can never be recorded either
-  if (disc == 0.0) {
-    t = -b / a2;  // tangent root, kept even when negative (sphere.h:43-47)
-    return true;
-  }
-  double sq = __builtin_sqrt(disc);
-  double t1 = (-b - sq) / a2;
-  double t2 = (-b + sq) / a2;
-  double tmx = (t1 < t2) ? t2 : t1;
-  if (tmx < 0.0) return false;
-  double tmn = (t2 < t1) ? t2 : t1;
-  t = (tmn < 0.0) ? tmx : tmn;
-  return true;
-}
-
-// ---------------------------------------------------------------------------
-// Wave-wide reductions.  Called only where all 64 lanes are active.
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-__device__ __forceinline__ double wmax(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    double o = __shfl_xor(v, off, 64);
-    v = (o > v) ? o : v;
-  }
-  return v;
-}
-__device__ __forceinline__ double wmin(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    double o = __shfl_xor(v, off, 64);
-    v = (o < v) ? o : v;
-  }
-  return v;
-}
-// Make a wave-uniform double live in SGPRs (the value is identical in every lane).
-__device__ __forceinline__ double uni(double v) {
-  unsigned long long b = __double_as_longlong(v);
-  unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
-  unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
-  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
-
-// ---------------------------------------------------------------------------
-// Exact conservative culling of spheres per wave and per sweep.
-//
-// The active lanes' rays are treated as infinite LINES o_i + t d_i.  With a
-// reference point P (camera for primary rays, the light for shadow rays, an
-// active lane's origin for reflections) and a unit axis a (from the first and
-// last active lanes' directions), let theta be the widest line angle between
-// any d_i and a, rho_i the distance from P to line i and reach_i = |o_i - P|_1.
-// For a sphere centre C with v = C - P every line satisfies
-//     dist(C, line_i) >= |v x a| cos(theta) - |v . a| sin(theta) - rho_i.
-// A sphere is culled only when that bound exceeds r + m_i for every lane, with
-//     m_i = 1e-6 * (|v|_1 + r + reach_i)   (so |oc_i| <= |v|_1 + reach_i).
-// The reference test (sphere.h:29-35) computes disc = 4|d|^2 (r^2 - dist'^2) + e
-// with |e| <= ~20 * 2^-53 * 4|d|^2 (2|oc|^2 + r^2) and dist' within 2^-53 |oc| of
-// dist, so dist >= r + m forces the computed disc < 0 with >100x slack: every
-// culled sphere is a miss for every active lane in the reference's own fp64
-// arithmetic -- including its disc == 0 (negative-root) quirk, which needs
-// disc == 0 exactly.  Candidates are still tested in file order with the exact
-// test, so closest-hit ties keep the lowest index.  NaN anywhere makes the
-// comparison false, i.e. keeps the sphere.  Two wave reductions per sweep:
-// max sin^2(theta_i) and max slack_i = |po x d|_1 + 1e-6 reach_i
-// (|po x d|_1 >= rho_i |d|, |d| = 1 +- 2^-52).  ("Culling".)
-struct Bound {
-  double px, py, pz, ax, ay, az, cos2, sin_t, slack;
-  bool cull;
-};
-
-__device__ __forceinline__ double lane_bcast(double v, int l) {
-  unsigned long long b = __double_as_longlong(v);
-  unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
-  unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
-  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
-
-__device__ __forceinline__ Bound make_bound(bool act, D3 o, D3 d, D3 P) {
-  Bound B;
-  const unsigned long long am = __ballot(act);
-  const int l0 = __builtin_ctzll(am), l1 = 63 - __builtin_clzll(am);
-  double sx = lane_bcast(d.x, l0) + lane_bcast(d.x, l1);
-  double sy = lane_bcast(d.y, l0) + lane_bcast(d.y, l1);
-  double sz = lane_bcast(d.z, l0) + lane_bcast(d.z, l1);
-  double len = __builtin_sqrt(sx * sx + sy * sy + sz * sz);
-  D3 a = (len > 0.0) ? mk(sx / len, sy / len, sz / len) : mk(1.0, 0.0, 0.0);
-  D3 cr = mk(d.y * a.z - d.z * a.y, d.z * a.x - d.x * a.z, d.x * a.y - d.y * a.x);
-  double s2 = act ? dot(cr, cr) : 0.0;
-  D3 po = sub(P, o);
-  D3 pc = mk(po.y * d.z - po.z * d.y, po.z * d.x - po.x * d.z, po.x * d.y - po.y * d.x);
-  double slack = act ? (__builtin_fabs(pc.x) + __builtin_fabs(pc.y) + __builtin_fabs(pc.z)) * (1.0 + 1e-9) +
-                           1e-6 * (__builtin_fabs(po.x) + __builtin_fabs(po.y) + __builtin_fabs(po.z))
-                     : 0.0;
-  const double s2max = uni(wmax(s2));
-  B.slack = uni(wmax(slack));
-  B.px = uni(P.x);
-  B.py = uni(P.y);
-  B.pz = uni(P.z);
-  B.ax = uni(a.x);
-  B.ay = uni(a.y);
-  B.az = uni(a.z);
-  // theta from the widest sine; 1e-9 covers the rounding of |a|, |d_i| and the products.
-  B.sin_t = __builtin_sqrt(s2max) + 1e-9;
-  const double c = __builtin_sqrt(1.0 - (s2max < 1.0 ? s2max : 1.0)) - 1e-9;
-  B.cos2 = c * c;
-  B.cull = c > 0.0 && B.sin_t < 1.0;
-  return B;
-}
-
-// True unless the sphere provably misses every active line (see above).
-__device__ __forceinline__ bool keep(const Bound &B, double cx, double cy, double cz, double r) {
-  double vx = cx - B.px, vy = cy - B.py, vz = cz - B.pz;
-  double va = __builtin_fabs(vx * B.ax + vy * B.ay + vz * B.az);
-  double wx = vy * B.az - vz * B.ay, wy = vz * B.ax - vx * B.az, wz = vx * B.ay - vy * B.ax;
-  double vp2 = wx * wx + wy * wy + wz * wz;
-  double m = 1e-6 * (__builtin_fabs(vx) + __builtin_fabs(vy) + __builtin_fabs(vz) + r);
-  double rhs = r + B.slack + m + va * B.sin_t;
-  return !(B.cull && vp2 * B.cos2 > rhs * rhs);
-}
-
-// Candidate mask of the 64 spheres [base, base+64) for this wave's bound.
-template <bool kCull>
-__device__ __forceinline__ unsigned long long candidates(const SphGeo *__restrict__ g, const double *__restrict__ rad,
-                                                         int n, int base, const Bound &B) {
-  if (!kCull) {
-    const int cnt = n - base;
-    return cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull);
-  }
-  const int s = base + (int)(threadIdx.x & 63);
-  bool k = false;
-  if (s < n) {
-    const SphGeo q = g[s];
-    k = keep(B, q.cx, q.cy, q.cz, rad[s]);
-  }
-  return __ballot(k);
-}
-
-// Scene::find_intersection (scene.h:41-61): all candidate spheres in file
-// order, strict '<' (so ties keep the lowest index), t starts at 1e20.
-// Work counters (wave-uniform): n_exact = exact ray-sphere tests executed for
-// live lanes; n_cull = sphere-vs-bound tests (one per sphere per wave sweep).
-struct Work {
-  unsigned long long exact = 0, cull = 0;
-};
-
-template <bool kCull>
-__device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
-                                             bool act, D3 o, D3 d, D3 P, double &best_t, Work &work) {
-  const double a = dot(d, d);
-  const double a4 = 4.0 * a, a2 = 2.0 * a;
-  double bt = kInf;
-  int bi = -1;
-  const unsigned live = (unsigned)__popcll(__ballot(act));
-  Bound B;
-  if (kCull) B = make_bound(act, o, d, P);
-  for (int base = 0; base < n; base += 64) {
-    unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
-    if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
-    work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
-    while (mask) {
-      const int i = base + __builtin_ctzll(mask);
-      mask &= mask - 1;
-      double t;
-      if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
-        bt = t;
-        bi = i;
-      }
-    }
-  }
-  best_t = bt;
-  return bi;
-}
-
-// Scene::in_shadow (scene.h:65-86) as an any-hit over the candidates: some
-// sphere with t < 1e20 (the find_intersection start value) and t < dist.  The
-// wave leaves as soon as the ballot of still-unoccluded active lanes is empty.
-template <bool kCull>
-__device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
-                                             bool act, D3 o, D3 d, D3 P, double dist, Work &work) {
-  unsigned long long live = __ballot(act);
-  if (live == 0) return false;
-  const double a = dot(d, d);
-  const double a4 = 4.0 * a, a2 = 2.0 * a;
-  bool occ = !act;
-  Bound B;
-  if (kCull) B = make_bound(act, o, d, P);
-  for (int base = 0; base < n; base += 64) {
-    unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
-    if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
-    while (mask) {
-      const int i = base + __builtin_ctzll(mask);
-      mask &= mask - 1;
-      double t;
-      work.exact += (unsigned)__popcll(live);
-      if (!occ && intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist) occ = true;
-      live = __ballot(!occ);
-      if (live == 0) return act;
-    }
-  }
-  return act && occ;
-}
-
-struct Cam {
-  double px, py, pz, fx, fy, fz, rx, ry, rz, ux, uy, uz, scale;
-};
-struct Rows {
-  int band, first, stride, count;
-};
-
-__device__ __forceinline__ int quantize(double c) {
-  double m = 255.99 * min1(c);  // main.cpp:85
-  return (int)m;
-}
-
-__device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
-  unsigned long long s = v;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  return s;
-}
 
 // One lane per pixel; the whole wave walks the reflection levels together
 // (uniform control flow around every sweep, lanes masked by `alive`/`hit`).
@@ -472,7 +211,12 @@ struct rt_ctx {
   double *d_rad = nullptr;  // |radius|, for the conservative cull only
   SphMat *d_mat = nullptr;
   bool cull = true;
-  int wg_waves = 1;  // waves per workgroup (tuning knob RT_HIP_WG_WAVES = 1 | 4)
+  int wg_waves = 1;  // megakernel waves per workgroup (tuning knob RT_HIP_WG_WAVES = 1 | 4)
+  int pipeline = 1;  // 1 = wavefront queues (default), 0 = megakernel (knob RT_HIP_PIPELINE)
+  int n_cu = 256;
+  // wavefront scratch: queues, per-pixel terminal colours / stack (grown on demand)
+  unsigned char *wf_buf = nullptr;
+  size_t wf_bytes = 0;
   LightD *d_lights = nullptr;
   int nsph = 0, nlight = 0;
   double amb[3] = {0, 0, 0};
@@ -542,6 +286,87 @@ void launch_render(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, i
   }
 }
 
+size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// Carve the wavefront scratch for npx pixels at this depth (grow-only).
+int ensure_wf(rt_ctx *c, size_t npx, int depth, WfArgs &a) {
+  const size_t levels = (size_t)(depth > 0 ? depth : 1);
+  const size_t b_hit = align_up(npx * sizeof(HitRec)), b_ray = align_up(npx * sizeof(RayRec)),
+               b_cnt = align_up(2 * (levels + 1) * sizeof(unsigned)), b_term = align_up(npx * sizeof(Term)),
+               b_nlev = align_up(npx), b_stack = align_up((levels - 1) * npx * sizeof(StackEnt));
+  const size_t need = b_hit + b_ray + b_cnt + b_term + b_nlev + b_stack;
+  if (c->wf_bytes < need) {
+    RT_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->wf_buf) (void)hipFree(c->wf_buf);
+    c->wf_buf = nullptr;
+    c->wf_bytes = 0;
+    RT_TRY(c, hipMalloc(&c->wf_buf, need));
+    c->wf_bytes = need;
+  }
+  unsigned char *p = c->wf_buf;
+  a.hitq = reinterpret_cast<HitRec *>(p);
+  p += b_hit;
+  a.rayq = reinterpret_cast<RayRec *>(p);
+  p += b_ray;
+  a.hit_cnt = reinterpret_cast<unsigned *>(p);
+  a.ray_cnt = a.hit_cnt + (levels + 1);
+  p += b_cnt;
+  a.term = reinterpret_cast<Term *>(p);
+  p += b_term;
+  a.nlev = p;
+  p += b_nlev;
+  a.stack = reinterpret_cast<StackEnt *>(p);
+  RT_TRY(c, hipMemsetAsync(a.hit_cnt, 0, 2 * (levels + 1) * sizeof(unsigned), c->stream));
+  return RT_OK;
+}
+
+template <bool kLds, bool kCull>
+int launch_wavefront2(rt_ctx *c, WfArgs &a, size_t lds) {
+  const int W = a.W;
+  const size_t npx = (size_t)a.npx;
+  static int blocks_per_cu = 0;  // resident 256-thread workgroups per CU for wf_shade
+  if (blocks_per_cu == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, wf_shade<kLds, kCull>, 256, lds) != hipSuccess || nb < 1)
+      nb = 2;
+    blocks_per_cu = nb;
+  }
+  size_t want = (npx + 255) / 256;
+  const unsigned persist = (unsigned)std::max<size_t>(1, std::min<size_t>(want, (size_t)c->n_cu * blocks_per_cu));
+  hipLaunchKernelGGL((wf_primary<kLds, kCull>), dim3((W + 15) / 16, (a.rows.count + 15) / 16), dim3(256), lds,
+                     c->stream, a);
+  for (int level = 0; level < a.depth; ++level) {
+    if (level > 0) hipLaunchKernelGGL((wf_reflect<kLds, kCull>), dim3(persist), dim3(256), lds, c->stream, a, level);
+    hipLaunchKernelGGL((wf_shade<kLds, kCull>), dim3(persist), dim3(256), lds, c->stream, a, level);
+  }
+  hipLaunchKernelGGL(wf_resolve, dim3((W + 63) / 64, (a.rows.count + 3) / 4), dim3(256), 0, c->stream, a);
+  return RT_OK;
+}
+
+int launch_wavefront(rt_ctx *c, const Cam &cam, int W, int H, int depth, const Rows &r, uint8_t *dst, bool lds_geo,
+                     size_t lds) {
+  WfArgs a;
+  a.geo = c->d_geo;
+  a.rad = c->d_rad;
+  a.mat = c->d_mat;
+  a.lights = c->d_lights;
+  a.n = c->nsph;
+  a.nl = c->nlight;
+  a.amb = D3{c->amb[0], c->amb[1], c->amb[2]};
+  a.cam = cam;
+  a.W = W;
+  a.H = H;
+  a.depth = depth;
+  a.rows = r;
+  a.npx = r.count * W;
+  a.out = dst;
+  a.counters = c->d_counters;
+  int rc = ensure_wf(c, (size_t)a.npx, depth, a);
+  if (rc != RT_OK) return rc;
+  if (lds_geo) return c->cull ? launch_wavefront2<true, true>(c, a, lds) : launch_wavefront2<true, false>(c, a, lds);
+  return c->cull ? launch_wavefront2<false, true>(c, a, lds) : launch_wavefront2<false, false>(c, a, lds);
+}
+
 int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_rows *rows, const void *out,
              Rows &r) {
   if (!c || !cam || !out || W <= 0 || H <= 0) return RT_ERR_INVALID_ARG;
@@ -570,10 +395,16 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
       c->err = "light list does not fit in LDS";
       return RT_ERR_INVALID_ARG;
     }
-    int stack = depth - 1;
-    if (stack <= 4) launch_render<4>(c, lds_geo, lds, cam, W, H, depth, r, dst);
-    else if (stack <= 16) launch_render<16>(c, lds_geo, lds, cam, W, H, depth, r, dst);
-    else launch_render<RT_MAX_DEPTH>(c, lds_geo, lds, cam, W, H, depth, r, dst);
+    if (c->pipeline == 1) {
+      if ((long long)r.count * W > (1LL << 31) - 1) return RT_ERR_INVALID_ARG;
+      int rc = launch_wavefront(c, cam, W, H, depth, r, dst, lds_geo, lds);
+      if (rc != RT_OK) return rc;
+    } else {
+      int stack = depth - 1;
+      if (stack <= 4) launch_render<4>(c, lds_geo, lds, cam, W, H, depth, r, dst);
+      else if (stack <= 16) launch_render<16>(c, lds_geo, lds, cam, W, H, depth, r, dst);
+      else launch_render<RT_MAX_DEPTH>(c, lds_geo, lds, cam, W, H, depth, r, dst);
+    }
     RT_TRY(c, hipGetLastError());
   }
   RT_TRY(c, hipEventRecord(c->ev1[slot], c->stream));
@@ -604,11 +435,17 @@ int rt_create(int device, rt_ctx **out) {
   rt_ctx *c = new rt_ctx();
   c->device = device;
   if (const char *e = std::getenv("RT_HIP_WG_WAVES")) c->wg_waves = std::atoi(e) == 4 ? 4 : 1;
+  if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::atoi(e) == 0 ? 0 : 1;
   auto bail = [&](int rc) {
     rt_destroy(c);
     return rc;
   };
   if (hipSetDevice(device) != hipSuccess) return bail(RT_ERR_HIP);
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+      c->n_cu = prop.multiProcessorCount;
+  }
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(RT_ERR_HIP);
   c->stream = c->own_stream;
   if (hipMalloc(&c->d_counters, kCounters * sizeof(unsigned long long)) != hipSuccess) return bail(RT_ERR_OUT_OF_MEMORY);
@@ -630,6 +467,7 @@ void rt_destroy(rt_ctx *c) {
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->d_tmp) (void)hipFree(c->d_tmp);
+  if (c->wf_buf) (void)hipFree(c->wf_buf);
   for (int i = 0; i < rt_ctx::kRing; i++) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
