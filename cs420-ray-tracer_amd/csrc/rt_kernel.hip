@@ -177,12 +177,13 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   const unsigned long long sp = wave_sum(c_prim), ss = wave_sum(c_shadow), sr = wave_sum(c_reflect),
                            sn = wave_sum(c_neg);
   if (lane == 0) {
-    if (sp) atomicAdd(&counters[0], sp);
-    if (ss) atomicAdd(&counters[1], ss);
-    if (sr) atomicAdd(&counters[2], sr);
-    if (sn) atomicAdd(&counters[3], sn);
-    if (work.exact) atomicAdd(&counters[4], work.exact);
-    if (work.cull) atomicAdd(&counters[5], work.cull);
+    unsigned long long *sc = counter_shard(counters);
+    if (sp) atomicAdd(&sc[0], sp);
+    if (ss) atomicAdd(&sc[1], ss);
+    if (sr) atomicAdd(&sc[2], sr);
+    if (sn) atomicAdd(&sc[3], sn);
+    if (work.exact) atomicAdd(&sc[4], work.exact);
+    if (work.cull) atomicAdd(&sc[5], work.cull);
   }
 }
 
@@ -289,11 +290,13 @@ void launch_render(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, i
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
 // Carve the wavefront scratch for npx pixels at this depth (grow-only).
-int ensure_wf(rt_ctx *c, size_t npx, int depth, WfArgs &a) {
+int ensure_wf(rt_ctx *c, size_t npx, int depth, size_t seg_cap, WfArgs &a) {
   const size_t levels = (size_t)(depth > 0 ? depth : 1);
-  const size_t b_hit = align_up(npx * sizeof(HitRec)), b_ray = align_up(npx * sizeof(RayRec)),
-               b_cnt = align_up(2 * (levels + 1) * sizeof(unsigned)), b_term = align_up(npx * sizeof(Term)),
-               b_nlev = align_up(npx), b_stack = align_up((levels - 1) * npx * sizeof(StackEnt));
+  const size_t qn = seg_cap * kShards;
+  const size_t b_hit = align_up(qn * sizeof(HitRec)), b_ray = align_up(qn * sizeof(RayRec)),
+               b_cnt = align_up(2 * (levels + 1) * kShards * sizeof(unsigned)),
+               b_term = align_up(npx * sizeof(Term)), b_nlev = align_up(npx),
+               b_stack = align_up((levels - 1) * npx * sizeof(StackEnt));
   const size_t need = b_hit + b_ray + b_cnt + b_term + b_nlev + b_stack;
   if (c->wf_bytes < need) {
     RT_TRY(c, hipStreamSynchronize(c->stream));
@@ -304,19 +307,20 @@ int ensure_wf(rt_ctx *c, size_t npx, int depth, WfArgs &a) {
     c->wf_bytes = need;
   }
   unsigned char *p = c->wf_buf;
+  a.seg_cap = (int)seg_cap;
   a.hitq = reinterpret_cast<HitRec *>(p);
   p += b_hit;
   a.rayq = reinterpret_cast<RayRec *>(p);
   p += b_ray;
   a.hit_cnt = reinterpret_cast<unsigned *>(p);
-  a.ray_cnt = a.hit_cnt + (levels + 1);
+  a.ray_cnt = a.hit_cnt + (levels + 1) * kShards;
   p += b_cnt;
   a.term = reinterpret_cast<Term *>(p);
   p += b_term;
   a.nlev = p;
   p += b_nlev;
   a.stack = reinterpret_cast<StackEnt *>(p);
-  RT_TRY(c, hipMemsetAsync(a.hit_cnt, 0, 2 * (levels + 1) * sizeof(unsigned), c->stream));
+  RT_TRY(c, hipMemsetAsync(a.hit_cnt, 0, 2 * (levels + 1) * kShards * sizeof(unsigned), c->stream));
   return RT_OK;
 }
 
@@ -331,8 +335,10 @@ int launch_wavefront2(rt_ctx *c, WfArgs &a, size_t lds) {
       nb = 2;
     blocks_per_cu = nb;
   }
-  size_t want = (npx + 255) / 256;
-  const unsigned persist = (unsigned)std::max<size_t>(1, std::min<size_t>(want, (size_t)c->n_cu * blocks_per_cu));
+  // persistent grid: a multiple of kShards, about one resident wave of workgroups
+  const size_t want = (npx + 255) / 256, resident = (size_t)c->n_cu * blocks_per_cu;
+  const size_t per_shard = std::max<size_t>(1, (std::min(want, resident) + kShards - 1) / kShards);
+  const unsigned persist = (unsigned)(per_shard * kShards);
   hipLaunchKernelGGL((wf_primary<kLds, kCull>), dim3((W + 15) / 16, (a.rows.count + 15) / 16), dim3(256), lds,
                      c->stream, a);
   for (int level = 0; level < a.depth; ++level) {
@@ -361,7 +367,9 @@ int launch_wavefront(rt_ctx *c, const Cam &cam, int W, int H, int depth, const R
   a.npx = r.count * W;
   a.out = dst;
   a.counters = c->d_counters;
-  int rc = ensure_wf(c, (size_t)a.npx, depth, a);
+  const size_t wgs = (size_t)((W + 15) / 16) * (size_t)((r.count + 15) / 16);
+  const size_t seg_cap = (wgs + kShards - 1) / kShards * 256;
+  int rc = ensure_wf(c, (size_t)a.npx, depth, seg_cap, a);
   if (rc != RT_OK) return rc;
   if (lds_geo) return c->cull ? launch_wavefront2<true, true>(c, a, lds) : launch_wavefront2<true, false>(c, a, lds);
   return c->cull ? launch_wavefront2<false, true>(c, a, lds) : launch_wavefront2<false, false>(c, a, lds);
@@ -380,7 +388,7 @@ int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_
 
 int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows &r, uint8_t *dst) {
   RT_TRY(c, hipSetDevice(c->device));
-  RT_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounters * sizeof(unsigned long long), c->stream));
+  RT_TRY(c, hipMemsetAsync(c->d_counters, 0, kShards * kShardStride * sizeof(unsigned long long), c->stream));
   const int slot = (int)(c->launches % rt_ctx::kRing);
   RT_TRY(c, hipEventRecord(c->ev0[slot], c->stream));
   if (r.count > 0) {
@@ -409,7 +417,7 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
   }
   RT_TRY(c, hipEventRecord(c->ev1[slot], c->stream));
   c->launches++;
-  RT_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounters * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+  RT_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, kShards * kShardStride * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                            c->stream));
   return RT_OK;
 }
@@ -448,10 +456,10 @@ int rt_create(int device, rt_ctx **out) {
   }
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(RT_ERR_HIP);
   c->stream = c->own_stream;
-  if (hipMalloc(&c->d_counters, kCounters * sizeof(unsigned long long)) != hipSuccess) return bail(RT_ERR_OUT_OF_MEMORY);
-  if (hipHostMalloc(&c->h_counters, kCounters * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+  if (hipMalloc(&c->d_counters, kShards * kShardStride * sizeof(unsigned long long)) != hipSuccess) return bail(RT_ERR_OUT_OF_MEMORY);
+  if (hipHostMalloc(&c->h_counters, kShards * kShardStride * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
     return bail(RT_ERR_OUT_OF_MEMORY);
-  std::memset(c->h_counters, 0, kCounters * sizeof(unsigned long long));
+  std::memset(c->h_counters, 0, kShards * kShardStride * sizeof(unsigned long long));
   for (int i = 0; i < rt_ctx::kRing; i++)
     if (hipEventCreate(&c->ev0[i]) != hipSuccess || hipEventCreate(&c->ev1[i]) != hipSuccess) return bail(RT_ERR_HIP);
   *out = c;
@@ -552,12 +560,15 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
     const int slot = (int)((c->launches - 1) % rt_ctx::kRing);
     RT_TRY(c, hipEventElapsedTime(&ms, c->ev0[slot], c->ev1[slot]));
   }
-  st->rays_primary = c->h_counters[0];
-  st->rays_shadow = c->h_counters[1];
-  st->rays_reflect = c->h_counters[2];
-  st->negative_clamped = c->h_counters[3];
-  st->tests_exact = c->h_counters[4];
-  st->tests_cull = c->h_counters[5];
+  unsigned long long sum[kCounters] = {};
+  for (int sh = 0; sh < kShards; sh++)
+    for (int q = 0; q < kCounters; q++) sum[q] += c->h_counters[sh * kShardStride + q];
+  st->rays_primary = sum[0];
+  st->rays_shadow = sum[1];
+  st->rays_reflect = sum[2];
+  st->negative_clamped = sum[3];
+  st->tests_exact = sum[4];
+  st->tests_cull = sum[5];
   st->kernel_ms = ms;
   return RT_OK;
 }

@@ -18,9 +18,16 @@
 //                   (shade*(1-refl) + reflected*refl, bit-identical to the
 //                   recursion) and quantises (main.cpp:85-87) into RGB8.
 //
-// Queue order follows the producing waves (runs of up to 64 hits from one
-// 8x8 tile), so the waves of wf_shade / wf_reflect stay spatially coherent
-// and the per-wave cull of rt_device.h stays tight.
+// Queues are split into kShards segments, each with its own append counter:
+// a producer workgroup appends to segment (workgroup id % kShards), and the
+// consumer workgroups of segment s are exactly those with id % kShards == s
+// (grid-stride inside the segment).  One contended word serialises device
+// atomics (~88/us); 64 words in separate lines do not.  Capacity: segment s of
+// the primary hit queue receives at most ceil(WGs/kShards) * 256 hits, and each
+// later pass maps segment s to segment s with at most one output per input, so
+// every queue segment needs the same `seg_cap` entries.  Segment order follows
+// the producing waves (runs of up to 64 hits from one 8x8 tile), so consumer
+// waves stay spatially coherent and the per-wave cull stays tight.
 #pragma once
 #include "rt_device.h"
 
@@ -64,10 +71,11 @@ struct WfArgs {
   int W, H, depth;
   Rows rows;
   int npx;            // rows.count * W
-  HitRec *hitq;
-  RayRec *rayq;
-  unsigned *hit_cnt;  // [depth]
-  unsigned *ray_cnt;  // [depth]
+  int seg_cap;        // entries per queue segment
+  HitRec *hitq;       // [kShards][seg_cap]
+  RayRec *rayq;       // [kShards][seg_cap]
+  unsigned *hit_cnt;  // [depth+1][kShards]
+  unsigned *ray_cnt;  // [depth+1][kShards]
   Term *term;
   uint8_t *nlev;
   StackEnt *stack;    // [(depth-1) * npx]
@@ -96,8 +104,9 @@ __device__ __forceinline__ void stage(const WfArgs &a, unsigned char *smem, cons
 
 __device__ __forceinline__ void flush_work(const Work &w, unsigned long long *counters) {
   if ((threadIdx.x & 63) == 0) {
-    if (w.exact) atomicAdd(&counters[4], w.exact);
-    if (w.cull) atomicAdd(&counters[5], w.cull);
+    unsigned long long *sc = counter_shard(counters);
+    if (w.exact) atomicAdd(&sc[4], w.exact);
+    if (w.cull) atomicAdd(&sc[5], w.cull);
   }
 }
 
@@ -139,7 +148,8 @@ __global__ __launch_bounds__(256) void wf_primary(WfArgs a) {
     a.term[pix] = Term{c.x, c.y, c.z};
     a.nlev[pix] = 0;
   }
-  const unsigned slot = wave_append(hit, &a.hit_cnt[0]);
+  const unsigned shard = (blockIdx.x + blockIdx.y * gridDim.x) % kShards;
+  const unsigned slot = wave_append(hit, &a.hit_cnt[shard]);
   if (hit) {
     HitRec h;
     h.ox = o.x; h.oy = o.y; h.oz = o.z;
@@ -150,18 +160,20 @@ __global__ __launch_bounds__(256) void wf_primary(WfArgs a) {
     h.dleft = a.depth;
     h.pad = 0;
     h.pad2 = 0;
-    a.hitq[slot] = h;
+    a.hitq[(size_t)shard * a.seg_cap + slot] = h;
   }
   const unsigned np = (unsigned)__popcll(__ballot(alive));
-  if (lane == 0 && np) atomicAdd(&a.counters[0], (unsigned long long)np);
+  if (lane == 0 && np) atomicAdd(&counter_shard(a.counters)[0], (unsigned long long)np);
   flush_work(work, a.counters);
 }
 
 // ---- pass 2 (per level): shading + shadow rays, spawns reflection rays -------
 template <bool kLdsGeo, bool kCull>
 __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
-  const unsigned cnt = a.hit_cnt[level];
-  if (blockIdx.x * 256u >= cnt) return;  // uniform: nothing for this workgroup
+  const unsigned shard = blockIdx.x % kShards, j = blockIdx.x / kShards, nj = gridDim.x / kShards;
+  const unsigned cnt = a.hit_cnt[level * kShards + shard];
+  if (j * 256u >= cnt) return;  // uniform: nothing for this workgroup
+  const HitRec *__restrict__ hq = a.hitq + (size_t)shard * a.seg_cap;
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
   const SphGeo *g;
   const double *rad;
@@ -170,11 +182,11 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   Work work;
   unsigned long long n_shadow = 0, n_reflect = 0;
-  const unsigned stride = gridDim.x * 256u;
-  for (unsigned base = blockIdx.x * 256u + wave * 64u; base < cnt; base += stride) {
+  const unsigned stride = nj * 256u;
+  for (unsigned base = j * 256u + wave * 64u; base < cnt; base += stride) {
     const unsigned idx = base + lane;
     const bool hit = idx < cnt;
-    const HitRec h = a.hitq[hit ? idx : base];
+    const HitRec h = hq[hit ? idx : base];
     const D3 o = mk(h.ox, h.oy, h.oz), d = mk(h.dx, h.dy, h.dz);
     const SphGeo sg = g[h.sph];
     const SphMat m = a.mat[h.sph];
@@ -224,13 +236,14 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
         a.nlev[h.pix] = (uint8_t)level;
       }
     }
-    const unsigned slot = wave_append(spawn, &a.ray_cnt[level + 1]);
-    if (spawn) a.rayq[slot] = RayRec{ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, h.pix, h.dleft - 1, 0.0};
+    const unsigned slot = wave_append(spawn, &a.ray_cnt[(level + 1) * kShards + shard]);
+    if (spawn)
+      a.rayq[(size_t)shard * a.seg_cap + slot] = RayRec{ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, h.pix, h.dleft - 1, 0.0};
     n_reflect += (unsigned long long)__popcll(__ballot(spawn));
   }
   if (lane == 0) {
-    if (n_shadow) atomicAdd(&a.counters[1], n_shadow);
-    if (n_reflect) atomicAdd(&a.counters[2], n_reflect);
+    if (n_shadow) atomicAdd(&counter_shard(a.counters)[1], n_shadow);
+    if (n_reflect) atomicAdd(&counter_shard(a.counters)[2], n_reflect);
   }
   flush_work(work, a.counters);
 }
@@ -238,8 +251,10 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
 // ---- pass 3 (per level >= 1): reflection rays -> hits ------------------------
 template <bool kLdsGeo, bool kCull>
 __global__ __launch_bounds__(256) void wf_reflect(WfArgs a, int level) {
-  const unsigned cnt = a.ray_cnt[level];
-  if (blockIdx.x * 256u >= cnt) return;
+  const unsigned shard = blockIdx.x % kShards, j = blockIdx.x / kShards, nj = gridDim.x / kShards;
+  const unsigned cnt = a.ray_cnt[level * kShards + shard];
+  if (j * 256u >= cnt) return;
+  const RayRec *__restrict__ rq = a.rayq + (size_t)shard * a.seg_cap;
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
   const SphGeo *g;
   const double *rad;
@@ -247,11 +262,11 @@ __global__ __launch_bounds__(256) void wf_reflect(WfArgs a, int level) {
   stage<kLdsGeo>(a, smem, g, rad, lights);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   Work work;
-  const unsigned stride = gridDim.x * 256u;
-  for (unsigned base = blockIdx.x * 256u + wave * 64u; base < cnt; base += stride) {
+  const unsigned stride = nj * 256u;
+  for (unsigned base = j * 256u + wave * 64u; base < cnt; base += stride) {
     const unsigned idx = base + lane;
     const bool alive = idx < cnt;
-    const RayRec r = a.rayq[alive ? idx : base];
+    const RayRec r = rq[alive ? idx : base];
     const D3 o = mk(r.ox, r.oy, r.oz), d = mk(r.dx, r.dy, r.dz);
     const D3 P = mk(lane_bcast(o.x, 0), lane_bcast(o.y, 0), lane_bcast(o.z, 0));  // lane 0 is always live
     double bt;
@@ -262,7 +277,7 @@ __global__ __launch_bounds__(256) void wf_reflect(WfArgs a, int level) {
       a.term[r.pix] = Term{c.x, c.y, c.z};
       a.nlev[r.pix] = (uint8_t)level;
     }
-    const unsigned slot = wave_append(hit, &a.hit_cnt[level]);
+    const unsigned slot = wave_append(hit, &a.hit_cnt[level * kShards + shard]);
     if (hit) {
       HitRec h;
       h.ox = o.x; h.oy = o.y; h.oz = o.z;
@@ -273,7 +288,7 @@ __global__ __launch_bounds__(256) void wf_reflect(WfArgs a, int level) {
       h.dleft = r.dleft;
       h.pad = 0;
       h.pad2 = 0;
-      a.hitq[slot] = h;
+      a.hitq[(size_t)shard * a.seg_cap + slot] = h;
     }
   }
   flush_work(work, a.counters);
@@ -306,7 +321,7 @@ __global__ __launch_bounds__(256) void wf_resolve(WfArgs a) {
     }
   }
   const unsigned long long sn = wave_sum(neg);
-  if ((threadIdx.x & 63) == 0 && sn) atomicAdd(&a.counters[3], sn);
+  if ((threadIdx.x & 63) == 0 && sn) atomicAdd(&counter_shard(a.counters)[3], sn);
 }
 
 }  // namespace rtk
