@@ -207,7 +207,19 @@ __device__ __forceinline__ unsigned long long candidates(const SphGeo *__restric
 // live lanes; n_cull = sphere-vs-bound tests (one per sphere per wave sweep).
 struct Work {
   unsigned long long exact = 0, cull = 0;
+#ifdef RT_STAMPS
+  // Diagnostic build only (-DRT_STAMPS): s_memtime cycles per phase, per wave.
+  unsigned long long st[8] = {};
+#endif
 };
+#ifdef RT_STAMPS
+#define RT_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define RT_ACC(w, slot, v) (w).st[slot] += __builtin_amdgcn_s_memtime() - (v)
+#else
+#define RT_T0(v)
+#define RT_ACC(w, slot, v)
+#endif
+// stamp slots: 0 bound, 1 cull, 2 candidate tests, 3 per-light setup, 4 shading, 5 whole wave
 
 template <bool kCull>
 __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
@@ -218,9 +230,14 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
   int bi = -1;
   const unsigned live = (unsigned)__popcll(__ballot(act));
   Bound B;
+  RT_T0(tb);
   if (kCull) B = make_bound(act, o, d, P);
+  RT_ACC(work, 0, tb);
   for (int base = 0; base < n; base += 64) {
+    RT_T0(tc);
     unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+    RT_ACC(work, 1, tc);
+    RT_T0(tt);
     if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
     work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
     while (mask) {
@@ -232,6 +249,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
         bi = i;
       }
     }
+    RT_ACC(work, 2, tt);
   }
   best_t = bt;
   return bi;
@@ -249,9 +267,14 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
   const double a4 = 4.0 * a, a2 = 2.0 * a;
   bool occ = !act;
   Bound B;
+  RT_T0(tb);
   if (kCull) B = make_bound(act, o, d, P);
+  RT_ACC(work, 0, tb);
   for (int base = 0; base < n; base += 64) {
+    RT_T0(tc);
     unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+    RT_ACC(work, 1, tc);
+    RT_T0(tt);
     if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
     while (mask) {
       const int i = base + __builtin_ctzll(mask);
@@ -260,8 +283,12 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
       work.exact += (unsigned)__popcll(live);
       if (!occ && intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist) occ = true;
       live = __ballot(!occ);
-      if (live == 0) return act;
+      if (live == 0) {
+        RT_ACC(work, 2, tt);
+        return act;
+      }
     }
+    RT_ACC(work, 2, tt);
   }
   return act && occ;
 }

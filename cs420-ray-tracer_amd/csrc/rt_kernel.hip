@@ -88,6 +88,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   bool alive = in_img && depth >= 1;
   unsigned c_prim = alive ? 1u : 0u, c_shadow = 0, c_reflect = 0, c_neg = 0;
   Work work;
+  RT_T0(t_wave);
 
   while (__ballot(alive)) {
     double bt;
@@ -107,13 +108,16 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
     const D3 mc = mk(m.cr, m.cg, m.cb);
     D3 col = mul(amb, mc);                                        // scene.h:91
     for (int l = 0; l < nl; ++l) {                                // scene.h:94-120
+      RT_T0(t_setup);
       const LightD L = slight[l];
       const D3 lp = mk(L.px, L.py, L.pz);
       const D3 to_light = sub(lp, hp);
       const double dist = length(to_light);
       const D3 ldir = normalized(to_light);
-      const bool occ =
-          sweep_shadow<kCull>(g, rad, n, hit, add(hp, scale(ldir, kEps)), normalized(ldir), lp, dist, work);
+      const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
+      RT_ACC(work, 3, t_setup);
+      const bool occ = sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, dist, work);
+      RT_T0(t_shade);
       if (hit && !occ) {
         const double ndl = max0(dot(nrm, ldir));
         const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
@@ -125,6 +129,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
         const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
         col = add(add(specular, diffuse), col);                  // scene.h:117
       }
+      RT_ACC(work, 4, t_shade);
     }
     if (hit) {
       c_shadow += (unsigned)nl;
@@ -176,8 +181,13 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   }
   const unsigned long long sp = wave_sum(c_prim), ss = wave_sum(c_shadow), sr = wave_sum(c_reflect),
                            sn = wave_sum(c_neg);
+  RT_ACC(work, 5, t_wave);
   if (lane == 0) {
     unsigned long long *sc = counter_shard(counters);
+#ifdef RT_STAMPS
+    for (int q = 0; q < 6; q++) atomicAdd(&sc[8 + q], work.st[q]);
+    atomicAdd(&sc[14], 1ull);
+#endif
     if (sp) atomicAdd(&sc[0], sp);
     if (ss) atomicAdd(&sc[1], ss);
     if (sr) atomicAdd(&sc[2], sr);
@@ -213,7 +223,7 @@ struct rt_ctx {
   SphMat *d_mat = nullptr;
   bool cull = true;
   int wg_waves = 1;  // megakernel waves per workgroup (tuning knob RT_HIP_WG_WAVES = 1 | 4)
-  int pipeline = 1;  // 1 = wavefront queues (default), 0 = megakernel (knob RT_HIP_PIPELINE)
+  int pipeline = 0;  // 0 = megakernel (default), 1 = wavefront queues (knob RT_HIP_PIPELINE)
   int n_cu = 256;
   // wavefront scratch: queues, per-pixel terminal colours / stack (grown on demand)
   unsigned char *wf_buf = nullptr;
@@ -443,7 +453,7 @@ int rt_create(int device, rt_ctx **out) {
   rt_ctx *c = new rt_ctx();
   c->device = device;
   if (const char *e = std::getenv("RT_HIP_WG_WAVES")) c->wg_waves = std::atoi(e) == 4 ? 4 : 1;
-  if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::atoi(e) == 0 ? 0 : 1;
+  if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::atoi(e) == 1 ? 1 : 0;
   auto bail = [&](int rc) {
     rt_destroy(c);
     return rc;
@@ -569,6 +579,15 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
   st->negative_clamped = sum[3];
   st->tests_exact = sum[4];
   st->tests_cull = sum[5];
+  if (std::getenv("RT_HIP_STAMPS")) {  // diagnostic builds (-DRT_STAMPS) fill slots 8..14
+    unsigned long long d[7] = {};
+    for (int sh = 0; sh < kShards; sh++)
+      for (int q = 0; q < 7; q++) d[q] += c->h_counters[sh * kShardStride + 8 + q];
+    std::fprintf(stderr, "RT_STAMPS waves=%llu cycles/wave: bound %.0f cull %.0f cand %.0f setup %.0f shade %.0f total %.0f\n",
+                 d[6], (double)d[0] / (d[6] ? d[6] : 1), (double)d[1] / (d[6] ? d[6] : 1),
+                 (double)d[2] / (d[6] ? d[6] : 1), (double)d[3] / (d[6] ? d[6] : 1),
+                 (double)d[4] / (d[6] ? d[6] : 1), (double)d[5] / (d[6] ? d[6] : 1));
+  }
   st->kernel_ms = ms;
   return RT_OK;
 }
