@@ -76,6 +76,34 @@ __device__ __forceinline__ bool intersect(const SphGeo &s, D3 o, D3 d, double a4
   return true;
 }
 
+// Division-free form of the same test.  With a2 = 2a > 0, t1 = fl(n1/a2) and
+// t2 = fl(n2/a2) where n1 = fl(-b - sq) <= n2 = fl(-b + sq) are exactly the
+// reference's numerators (sphere.h:49-50).  Division by a2 > 0 is monotone and
+// for |n| >= 2^-900, a2 in [2^-60, 2^60] it can neither underflow to a signed
+// zero nor change sign, so the root choice of sphere.h:51-57 (t2 < 0 -> miss;
+// t = t1 < 0 ? t2 : t1) is made on the numerators: t = fl(num / a2).
+// Returns 0 = miss, 1 = hit with numerator `num`, 2 = "decide with the exact
+// intersect()" (a numerator too close to zero, or a2 out of range).
+constexpr double kTinyNum = 0x1p-900;
+__device__ __forceinline__ int intersect_num(const SphGeo &s, D3 o, D3 d, double a4, double &num) {
+  double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
+  double b = 2.0 * ((ocx * d.x + ocy * d.y) + ocz * d.z);
+  double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.rr;
+  double disc = b * b - a4 * c;
+  if (!(disc >= 0.0)) return 0;
+  if (disc == 0.0) {
+    num = -b;  // t = -b / a2, negative roots included (sphere.h:43-47)
+    return 1;
+  }
+  double sq = __builtin_sqrt(disc);
+  double n1 = -b - sq, n2 = -b + sq;
+  if (__builtin_fabs(n1) < kTinyNum || __builtin_fabs(n2) < kTinyNum) return 2;
+  if (n2 < 0.0) return 0;
+  num = (n1 < 0.0) ? n2 : n1;
+  return 1;
+}
+__device__ __forceinline__ bool a2_ok(double a2) { return a2 >= 0x1p-60 && a2 <= 0x1p60; }
+
 // ---------------------------------------------------------------------------
 // Wave-wide reductions.  Called only where all 64 lanes are active.
 __device__ __forceinline__ double wsum(double v) {
@@ -226,8 +254,9 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
                                              bool act, D3 o, D3 d, D3 P, double &best_t, Work &work) {
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
-  double bt = kInf;
+  double bt = kInf, bn = __builtin_inf();
   int bi = -1;
+  const bool fast = a2_ok(a2);
   const unsigned live = (unsigned)__popcll(__ballot(act));
   Bound B;
   RT_T0(tb);
@@ -243,10 +272,26 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
     while (mask) {
       const int i = base + __builtin_ctzll(mask);
       mask &= mask - 1;
-      double t;
-      if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
-        bt = t;
-        bi = i;
+      // A candidate whose numerator is >= the best's cannot have a strictly
+      // smaller t = fl(num/a2); only would-be new bests pay the division.
+      double num;
+      const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+      if (r == 1) {
+        if (num < bn) {
+          const double t = num / a2;
+          if (t < bt) {
+            bt = t;
+            bn = num;
+            bi = i;
+          }
+        }
+      } else if (r == 2) {
+        double t;
+        if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
+          bt = t;
+          bn = __builtin_inf();  // no numerator for this best: every later candidate divides
+          bi = i;
+        }
       }
     }
     RT_ACC(work, 2, tt);
@@ -266,6 +311,13 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
   bool occ = !act;
+  // occluded <=> t < T, T = min(dist, 1e20).  With q = fl(a2*T), a numerator
+  // below q(1-2^-48) gives fl(num/a2) < T and one above q(1+2^-48) gives
+  // fl(num/a2) > T (both with >2^-50 relative room), so only the band between
+  // needs the exact division.
+  const double T = dist < kInf ? dist : kInf;
+  const bool fast = a2_ok(a2) && dist == dist && T >= 0x1p-900;
+  const double q = a2 * T, qlo = q * (1.0 - 0x1p-48), qhi = q * (1.0 + 0x1p-48);
   Bound B;
   RT_T0(tb);
   if (kCull) B = make_bound(act, o, d, P);
@@ -279,9 +331,21 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
     while (mask) {
       const int i = base + __builtin_ctzll(mask);
       mask &= mask - 1;
-      double t;
       work.exact += (unsigned)__popcll(live);
-      if (!occ && intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist) occ = true;
+      if (!occ) {
+        double num;
+        const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+        if (r == 1) {
+          if (num < qlo) occ = true;
+          else if (!(num > qhi)) {
+            const double t = num / a2;
+            occ = t < kInf && t < dist;
+          }
+        } else if (r == 2) {
+          double t;
+          occ = intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist;
+        }
+      }
       live = __ballot(!occ);
       if (live == 0) {
         RT_ACC(work, 2, tt);
