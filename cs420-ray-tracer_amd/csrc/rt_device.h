@@ -104,24 +104,6 @@ __device__ __forceinline__ int intersect_num(const SphGeo &s, D3 o, D3 d, double
 }
 __device__ __forceinline__ bool a2_ok(double a2) { return a2 >= 0x1p-60 && a2 <= 0x1p60; }
 
-// Straight-line (select-based) form of intersect_num, so the dependency
-// chains of two candidates interleave.  Same results: the sqrt of a negative
-// disc is computed on 0 and discarded; a non-finite disc goes to the exact path.
-__device__ __forceinline__ int intersect_num_bl(const SphGeo &s, D3 o, D3 d, double a4, double &num) {
-  const double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
-  const double b = 2.0 * ((ocx * d.x + ocy * d.y) + ocz * d.z);
-  const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.rr;
-  const double disc = b * b - a4 * c;
-  const double sq = __builtin_sqrt(disc > 0.0 ? disc : 0.0);
-  const double n1 = -b - sq, n2 = -b + sq;
-  const bool pos = disc > 0.0;
-  const bool exact = (pos && (__builtin_fabs(n1) < kTinyNum || __builtin_fabs(n2) < kTinyNum)) ||
-                     (disc >= 0.0 && !(__builtin_fabs(disc) <= 0x1.fffffffffffffp+1023));
-  const bool hit = disc == 0.0 || (pos && !(n2 < 0.0));
-  num = disc == 0.0 ? -b : ((n1 < 0.0) ? n2 : n1);
-  return exact ? 2 : (hit ? 1 : 0);
-}
-
 // ---------------------------------------------------------------------------
 // Wave-wide reductions.  Called only where all 64 lanes are active.
 __device__ __forceinline__ double wsum(double v) {
@@ -256,15 +238,12 @@ struct Work {
 #ifdef RT_STAMPS
   // Diagnostic build only (-DRT_STAMPS): s_memtime cycles per phase, per wave.
   unsigned long long st[8] = {};
-  unsigned long long iters = 0, sweeps = 0, hitpath = 0;
 #endif
 };
 #ifdef RT_STAMPS
 #define RT_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define RT_ACC(w, slot, v) (w).st[slot] += __builtin_amdgcn_s_memtime() - (v)
-#define RT_CNT(w, f, n) (w).f += (n)
 #else
-#define RT_CNT(w, f, n)
 #define RT_T0(v)
 #define RT_ACC(w, slot, v)
 #endif
@@ -283,7 +262,6 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
   RT_T0(tb);
   if (kCull) B = make_bound(act, o, d, P);
   RT_ACC(work, 0, tb);
-  RT_CNT(work, sweeps, 1);
   for (int base = 0; base < n; base += 64) {
     RT_T0(tc);
     unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
@@ -292,40 +270,27 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
     if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
     work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
     while (mask) {
-      // Two candidates per iteration (file order i0 < i1): independent
-      // straight-line tests, then the reference's updates in order.
-      const int i0 = base + __builtin_ctzll(mask);
+      const int i = base + __builtin_ctzll(mask);
       mask &= mask - 1;
-      const bool two = mask != 0;
-      const int i1 = two ? base + __builtin_ctzll(mask) : i0;
-      if (two) mask &= mask - 1;
-      RT_CNT(work, iters, 1);
-      double n0, n1;
-      const int r0 = fast ? intersect_num_bl(g[i0], o, d, a4, n0) : 2;
-      const int r1 = fast ? intersect_num_bl(g[i1], o, d, a4, n1) : 2;
       // A candidate whose numerator is >= the best's cannot have a strictly
       // smaller t = fl(num/a2); only would-be new bests pay the division.
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (u == 1 && !two) break;
-        const int r = u ? r1 : r0, i = u ? i1 : i0;
-        const double num = u ? n1 : n0;
-        if (r == 1) {
-          if (num < bn) {
-            const double t = num / a2;
-            if (t < bt) {
-              bt = t;
-              bn = num;
-              bi = i;
-            }
-          }
-        } else if (r == 2) {
-          double t;
-          if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
+      double num;
+      const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+      if (r == 1) {
+        if (num < bn) {
+          const double t = num / a2;
+          if (t < bt) {
             bt = t;
-            bn = __builtin_inf();  // no numerator for this best: every later candidate divides
+            bn = num;
             bi = i;
           }
+        }
+      } else if (r == 2) {
+        double t;
+        if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
+          bt = t;
+          bn = __builtin_inf();  // no numerator for this best: every later candidate divides
+          bi = i;
         }
       }
     }
@@ -357,7 +322,6 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
   RT_T0(tb);
   if (kCull) B = make_bound(act, o, d, P);
   RT_ACC(work, 0, tb);
-  RT_CNT(work, sweeps, 1);
   for (int base = 0; base < n; base += 64) {
     RT_T0(tc);
     unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
@@ -365,31 +329,21 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
     RT_T0(tt);
     if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
     while (mask) {
-      const int i0 = base + __builtin_ctzll(mask);
+      const int i = base + __builtin_ctzll(mask);
       mask &= mask - 1;
-      const bool two = mask != 0;
-      const int i1 = two ? base + __builtin_ctzll(mask) : i0;
-      if (two) mask &= mask - 1;
-      work.exact += (unsigned)__popcll(live) * (two ? 2u : 1u);
-      RT_CNT(work, iters, 1);
-      if (!occ) {  // any-hit: the order of the two tests does not matter
-        double n0, n1;
-        const int r0 = fast ? intersect_num_bl(g[i0], o, d, a4, n0) : 2;
-        const int r1 = fast ? intersect_num_bl(g[i1], o, d, a4, n1) : 2;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int r = u ? r1 : r0, i = u ? i1 : i0;
-          const double num = u ? n1 : n0;
-          if (r == 1) {
-            if (num < qlo) occ = true;
-            else if (!(num > qhi)) {
-              const double t = num / a2;
-              occ = occ || (t < kInf && t < dist);
-            }
-          } else if (r == 2) {
-            double t;
-            occ = occ || (intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist);
+      work.exact += (unsigned)__popcll(live);
+      if (!occ) {
+        double num;
+        const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+        if (r == 1) {
+          if (num < qlo) occ = true;
+          else if (!(num > qhi)) {
+            const double t = num / a2;
+            occ = t < kInf && t < dist;
           }
+        } else if (r == 2) {
+          double t;
+          occ = intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist;
         }
       }
       live = __ballot(!occ);

@@ -187,8 +187,6 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
 #ifdef RT_STAMPS
     for (int q = 0; q < 6; q++) atomicAdd(&sc[8 + q], work.st[q]);
     atomicAdd(&sc[14], 1ull);
-    atomicAdd(&sc[15], work.iters);
-    atomicAdd(&sc[16], work.sweeps);
 #endif
     if (sp) atomicAdd(&sc[0], sp);
     if (ss) atomicAdd(&sc[1], ss);
@@ -582,11 +580,9 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
   st->tests_exact = sum[4];
   st->tests_cull = sum[5];
   if (std::getenv("RT_HIP_STAMPS")) {  // diagnostic builds (-DRT_STAMPS) fill slots 8..14
-    unsigned long long d[9] = {};
+    unsigned long long d[7] = {};
     for (int sh = 0; sh < kShards; sh++)
-      for (int q = 0; q < 9; q++) d[q] += c->h_counters[sh * kShardStride + 8 + q];
-    std::fprintf(stderr, "RT_STAMPS candidate iterations/wave %.1f sweeps/wave %.2f\n",
-                 (double)d[7] / (d[6] ? d[6] : 1), (double)d[8] / (d[6] ? d[6] : 1));
+      for (int q = 0; q < 7; q++) d[q] += c->h_counters[sh * kShardStride + 8 + q];
     std::fprintf(stderr, "RT_STAMPS waves=%llu cycles/wave: bound %.0f cull %.0f cand %.0f setup %.0f shade %.0f total %.0f\n",
                  d[6], (double)d[0] / (d[6] ? d[6] : 1), (double)d[1] / (d[6] ? d[6] : 1),
                  (double)d[2] / (d[6] ? d[6] : 1), (double)d[3] / (d[6] ? d[6] : 1),
