@@ -258,6 +258,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
   int bi = -1;
   const bool fast = a2_ok(a2);
   const unsigned live = (unsigned)__popcll(__ballot(act));
+  RT_CNT(work, sw_closest, 1);
   Bound B;
   RT_T0(tb);
   if (kCull) B = make_bound(act, o, d, P);

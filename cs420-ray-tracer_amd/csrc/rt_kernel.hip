@@ -92,7 +92,13 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
 
   while (__ballot(alive)) {
     double bt;
+#ifdef RT_STAMPS
+    const unsigned long long it_before = work.it_closest;
+#endif
     const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, P, bt, work);
+#ifdef RT_STAMPS
+    if (dleft == depth) work.it_prim += work.it_closest - it_before;
+#endif
     const bool hit = alive && bi >= 0;
     if (alive && !hit) {  // sky, main.cpp:26-30
       const double st = 0.5 * (d.y + 1.0);
