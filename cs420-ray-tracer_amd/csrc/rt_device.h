@@ -238,12 +238,15 @@ struct Work {
 #ifdef RT_STAMPS
   // Diagnostic build only (-DRT_STAMPS): s_memtime cycles per phase, per wave.
   unsigned long long st[8] = {};
+  unsigned long long iters = 0, sweeps = 0, it_closest = 0, sw_closest = 0, it_prim = 0;
 #endif
 };
 #ifdef RT_STAMPS
 #define RT_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define RT_ACC(w, slot, v) (w).st[slot] += __builtin_amdgcn_s_memtime() - (v)
+#define RT_CNT(w, f, n) (w).f += (n)
 #else
+#define RT_CNT(w, f, n)
 #define RT_T0(v)
 #define RT_ACC(w, slot, v)
 #endif
@@ -263,6 +266,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
   RT_T0(tb);
   if (kCull) B = make_bound(act, o, d, P);
   RT_ACC(work, 0, tb);
+  RT_CNT(work, sweeps, 1);
   for (int base = 0; base < n; base += 64) {
     RT_T0(tc);
     unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
@@ -275,6 +279,8 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       mask &= mask - 1;
       // A candidate whose numerator is >= the best's cannot have a strictly
       // smaller t = fl(num/a2); only would-be new bests pay the division.
+      RT_CNT(work, iters, 1);
+      RT_CNT(work, it_closest, 1);
       double num;
       const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
       if (r == 1) {
@@ -323,6 +329,7 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
   RT_T0(tb);
   if (kCull) B = make_bound(act, o, d, P);
   RT_ACC(work, 0, tb);
+  RT_CNT(work, sweeps, 1);
   for (int base = 0; base < n; base += 64) {
     RT_T0(tc);
     unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
@@ -333,6 +340,7 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
       const int i = base + __builtin_ctzll(mask);
       mask &= mask - 1;
       work.exact += (unsigned)__popcll(live);
+      RT_CNT(work, iters, 1);
       if (!occ) {
         double num;
         const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
