@@ -51,6 +51,10 @@ __device__ __forceinline__ D3 normalized(D3 a) {
   double len = length(a);
   return mk(a.x / len, a.y / len, a.z / len);
 }
+// ocml's fp64 pow needs ~50 VGPRs when inlined into the render loop; called
+// out of line it only adds its own frame where little of the caller is live.
+__device__ __attribute__((noinline)) double pow_call(double x, double y) { return pow(x, y); }
+
 __device__ __forceinline__ double max0(double x) { return (0.0 < x) ? x : 0.0; }  // std::max(0.0, x)
 __device__ __forceinline__ double min1(double x) { return (x < 1.0) ? x : 1.0; }  // std::min(1.0, x)
 

@@ -37,7 +37,7 @@ namespace rtk {
 #ifndef RT_MIN_WAVES_PER_EU
 #define RT_MIN_WAVES_PER_EU 1
 #endif
-template <int MAXS, bool kLdsGeo, bool kCull, int kWaves>
+template <int MAXS, bool kLdsGeo, bool kCull, int kWaves, bool kLdsStack = (MAXS <= 4)>
 __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kernel(const SphGeo *__restrict__ geo, const double *__restrict__ radius,
                                                         const SphMat *__restrict__ mat,
                                                         const LightD *__restrict__ lights, int n, int nl, D3 amb,
@@ -48,6 +48,9 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   SphGeo *sgeo = reinterpret_cast<SphGeo *>(smem);
   double *srad = reinterpret_cast<double *>(smem + (kLdsGeo ? (size_t)n * sizeof(SphGeo) : 0));
   LightD *slight = reinterpret_cast<LightD *>(smem + (kLdsGeo ? (size_t)n * (sizeof(SphGeo) + sizeof(double)) : 0));
+  // per-wave reflection stack after the scene, 32-B aligned
+  const size_t stack_off = ((kLdsGeo ? (size_t)n * (sizeof(SphGeo) + sizeof(double)) : 0) +
+                            (size_t)nl * sizeof(LightD) + 31) & ~(size_t)31;
   const int tid = threadIdx.x;
   constexpr int kThreads = 64 * kWaves;
   if (kLdsGeo)
@@ -80,8 +83,11 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   D3 o = mk(cam.px, cam.py, cam.pz);
   D3 P = o;
 
-  double stA[3][MAXS];
-  double stR[MAXS];
+  // Reflection stack, one slot per level and lane, in LDS (kLdsStack: after
+  // the staged scene) or in per-lane private memory for the deepest variant.
+  double stA[3][kLdsStack ? 1 : MAXS];
+  double stR[kLdsStack ? 1 : MAXS];
+  StackEnt *lstack = reinterpret_cast<StackEnt *>(smem + stack_off) + (size_t)wave * MAXS * 64;
   int lev = 0;
   int dleft = depth;
   D3 res = mk(0.0, 0.0, 0.0);     // depth <= 0 -> black (main.cpp:17-18)
@@ -106,48 +112,72 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
       alive = false;
     }
     const int hi = hit ? bi : 0;
-    const SphGeo sg = g[hi];
-    const SphMat m = mat[hi];
     const D3 hp = add(o, scale(d, bt));                            // main.cpp:32
-    const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
-    const D3 view = normalized(sub(o, hp));                       // main.cpp:38
-    const D3 mc = mk(m.cr, m.cg, m.cb);
-    D3 col = mul(amb, mc);                                        // scene.h:91
-    for (int l = 0; l < nl; ++l) {                                // scene.h:94-120
-      RT_T0(t_setup);
-      const LightD L = slight[l];
-      const D3 lp = mk(L.px, L.py, L.pz);
-      const D3 to_light = sub(lp, hp);
-      const double dist = length(to_light);
-      const D3 ldir = normalized(to_light);
-      const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
-      RT_ACC(work, 3, t_setup);
-      const bool occ = sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, dist, work);
+    D3 col;
+    {
+      const SphMat m0 = mat[hi];
+      col = mul(amb, mk(m0.cr, m0.cg, m0.cb));                   // scene.h:91
+    }
+    // scene.h:94-120, split in two phases per block of 64 lights so that no
+    // shading state is live across the shadow sweeps: (A) occlusion bits for
+    // every light, (B) Phong terms in light order for the unoccluded ones.
+    // Phase B recomputes to_light / ldir with the same operations (same bits).
+    for (int l0 = 0; l0 < nl; l0 += 64) {
+      const int lend = nl - l0 < 64 ? nl : l0 + 64;
+      unsigned long long occm = 0;
+      for (int l = l0; l < lend; ++l) {
+        RT_T0(t_setup);
+        const LightD L = slight[l];
+        const D3 lp = mk(L.px, L.py, L.pz);
+        const D3 to_light = sub(lp, hp);
+        const double dist = length(to_light);
+        const D3 ldir = normalized(to_light);
+        const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
+        RT_ACC(work, 3, t_setup);
+        if (sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, dist, work)) occm |= 1ull << (l - l0);
+      }
       RT_T0(t_shade);
-      if (hit && !occ) {
-        const double ndl = max0(dot(nrm, ldir));
-        const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
-        const D3 nl2 = scale(ldir, -1.0);
-        const D3 rdir = sub(nl2, scale(scale(nrm, 2.0), dot(nl2, nrm)));  // reflect(), vec3.h:31-33
-        const double rdv = max0(dot(rdir, view));
-        // pow(+0, y > 0) is +0 exactly (C99 F.10.4.4), so most lanes skip ocml's pow.
-        const double spec = (rdv == 0.0 && m.shin > 0.0) ? 0.0 : pow(rdv, m.shin);
-        const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
-        col = add(add(specular, diffuse), col);                  // scene.h:117
+      if (hit && occm != ~0ull >> (64 - (lend - l0))) {
+        const SphGeo sg = g[hi];
+        const SphMat m = mat[hi];
+        const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
+        const D3 view = normalized(sub(o, hp));                       // main.cpp:38
+        const D3 mc = mk(m.cr, m.cg, m.cb);
+        for (int l = l0; l < lend; ++l) {
+          if (occm >> (l - l0) & 1ull) continue;
+          const LightD L = slight[l];
+          const D3 ldir = normalized(sub(mk(L.px, L.py, L.pz), hp));
+          const double ndl = max0(dot(nrm, ldir));
+          const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
+          const D3 nl2 = scale(ldir, -1.0);
+          const D3 rdir = sub(nl2, scale(scale(nrm, 2.0), dot(nl2, nrm)));  // reflect(), vec3.h:31-33
+          const double rdv = max0(dot(rdir, view));
+          // pow(+0, y > 0) is +0 exactly (C99 F.10.4.4), so most lanes skip ocml's pow.
+          const double spec = (rdv == 0.0 && m.shin > 0.0) ? 0.0 : pow_call(rdv, m.shin);
+          const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
+          col = add(add(specular, diffuse), col);                  // scene.h:117
+        }
       }
       RT_ACC(work, 4, t_shade);
     }
     if (hit) {
       c_shadow += (unsigned)nl;
+      const SphMat m = mat[hi];
       if (m.refl > 0.0) {                                         // main.cpp:43-55
         const double w = 1.0 - m.refl;
         const D3 A = mk(col.x * w, col.y * w, col.z * w);
         if (dleft - 1 >= 1) {  // host picks MAXS >= depth-1, so lev < MAXS here
-          stA[0][lev] = A.x;
-          stA[1][lev] = A.y;
-          stA[2][lev] = A.z;
-          stR[lev] = m.refl;
+          if (kLdsStack) {
+            lstack[lev * 64 + lane] = StackEnt{A.x, A.y, A.z, m.refl};
+          } else {
+            stA[0][lev] = A.x;
+            stA[1][lev] = A.y;
+            stA[2][lev] = A.z;
+            stR[lev] = m.refl;
+          }
           ++lev;
+          const SphGeo sg = g[hi];
+          const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));
           const D3 rd = sub(d, scale(scale(nrm, 2.0), dot(d, nrm)));
           o = add(hp, scale(nrm, kEps));
           d = normalized(rd);
@@ -170,8 +200,13 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   }
   while (lev > 0) {  // unwind: shade*(1-refl) + reflected*refl, innermost first
     --lev;
-    const double r = stR[lev];
-    res = mk(stA[0][lev] + res.x * r, stA[1][lev] + res.y * r, stA[2][lev] + res.z * r);
+    if (kLdsStack) {
+      const StackEnt e = lstack[lev * 64 + lane];
+      res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
+    } else {
+      const double r = stR[lev];
+      res = mk(stA[0][lev] + res.x * r, stA[1][lev] + res.y * r, stA[2][lev] + res.z * r);
+    }
   }
   if (in_tile) {
     uint8_t *px = out + ((size_t)k * W + x) * 3;
@@ -193,6 +228,11 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
 #ifdef RT_STAMPS
     for (int q = 0; q < 6; q++) atomicAdd(&sc[8 + q], work.st[q]);
     atomicAdd(&sc[14], 1ull);
+    atomicAdd(&sc[15], work.iters);
+    atomicAdd(&sc[16], work.sweeps);
+    atomicAdd(&sc[17], work.it_closest);
+    atomicAdd(&sc[18], work.sw_closest);
+    atomicAdd(&sc[19], work.it_prim);
 #endif
     if (sp) atomicAdd(&sc[0], sp);
     if (ss) atomicAdd(&sc[1], ss);
@@ -281,6 +321,7 @@ void launch_render3(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, 
   constexpr int kWx = kWaves == 4 ? 2 : 1, kWy = kWaves / kWx;
   dim3 grid((W + 8 * kWx - 1) / (8 * kWx), (rows.count + 8 * kWy - 1) / (8 * kWy));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
+  if (MAXS <= 4) lds = ((lds + 31) & ~(size_t)31) + (size_t)kWaves * 64 * MAXS * sizeof(StackEnt);
   if (lds_geo)
     hipLaunchKernelGGL((render_kernel<MAXS, true, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
                        c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out,
@@ -586,9 +627,14 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
   st->tests_exact = sum[4];
   st->tests_cull = sum[5];
   if (std::getenv("RT_HIP_STAMPS")) {  // diagnostic builds (-DRT_STAMPS) fill slots 8..14
-    unsigned long long d[7] = {};
+    unsigned long long d[12] = {};
     for (int sh = 0; sh < kShards; sh++)
-      for (int q = 0; q < 7; q++) d[q] += c->h_counters[sh * kShardStride + 8 + q];
+      for (int q = 0; q < 12; q++) d[q] += c->h_counters[sh * kShardStride + 8 + q];
+    const double nw = (double)(d[6] ? d[6] : 1);
+    std::fprintf(stderr,
+                 "RT_STAMPS per wave: candidate iterations %.1f (closest %.1f, of which primary %.1f), sweeps %.2f "
+                 "(closest %.2f)\n",
+                 d[7] / nw, d[9] / nw, d[11] / nw, d[8] / nw, d[10] / nw);
     std::fprintf(stderr, "RT_STAMPS waves=%llu cycles/wave: bound %.0f cull %.0f cand %.0f setup %.0f shade %.0f total %.0f\n",
                  d[6], (double)d[0] / (d[6] ? d[6] : 1), (double)d[1] / (d[6] ? d[6] : 1),
                  (double)d[2] / (d[6] ? d[6] : 1), (double)d[3] / (d[6] ? d[6] : 1),
