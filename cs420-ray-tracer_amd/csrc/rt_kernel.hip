@@ -32,6 +32,13 @@
 
 namespace rtk {
 
+#ifdef RT_STAMPS
+// Diagnostic timeline: per wave {start, end} (s_memrealtime, 100 MHz) and
+// {HW_ID, XCC_ID}; dumped by rt_render_stats when RT_HIP_STAMPS_FILE is set.
+constexpr int kTimelineWaves = 1 << 17;
+__device__ unsigned long long g_timeline[kTimelineWaves * 3];
+#endif
+
 // One lane per pixel; the whole wave walks the reflection levels together
 // (uniform control flow around every sweep, lanes masked by `alive`/`hit`).
 #ifndef RT_MIN_WAVES_PER_EU
@@ -95,6 +102,9 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   unsigned c_prim = alive ? 1u : 0u, c_shadow = 0, c_reflect = 0, c_neg = 0;
   Work work;
   RT_T0(t_wave);
+#ifdef RT_STAMPS
+  const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
   while (__ballot(alive)) {
     double bt;
@@ -223,6 +233,18 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   const unsigned long long sp = wave_sum(c_prim), ss = wave_sum(c_shadow), sr = wave_sum(c_reflect),
                            sn = wave_sum(c_neg);
   RT_ACC(work, 5, t_wave);
+#ifdef RT_STAMPS
+  if (lane == 0) {
+    const unsigned wid = (blockIdx.x + blockIdx.y * gridDim.x) * kWaves + wave;
+    if (wid < (unsigned)kTimelineWaves) {
+      g_timeline[3 * wid] = t_real0;
+      g_timeline[3 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+      const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+      const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+      g_timeline[3 * wid + 2] = ((unsigned long long)xcc << 32) | hw;
+    }
+  }
+#endif
   if (lane == 0) {
     unsigned long long *sc = counter_shard(counters);
 #ifdef RT_STAMPS
@@ -626,6 +648,17 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
   st->negative_clamped = sum[3];
   st->tests_exact = sum[4];
   st->tests_cull = sum[5];
+#ifdef RT_STAMPS
+  if (const char *tf = std::getenv("RT_HIP_STAMPS_FILE")) {
+    static unsigned long long host_tl[kTimelineWaves * 3];
+    if (hipMemcpyFromSymbol(host_tl, HIP_SYMBOL(g_timeline), sizeof(host_tl)) == hipSuccess) {
+      if (FILE *f = std::fopen(tf, "wb")) {
+        std::fwrite(host_tl, sizeof(host_tl), 1, f);
+        std::fclose(f);
+      }
+    }
+  }
+#endif
   if (std::getenv("RT_HIP_STAMPS")) {  // diagnostic builds (-DRT_STAMPS) fill slots 8..14
     unsigned long long d[12] = {};
     for (int sh = 0; sh < kShards; sh++)

@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Render a workload a few times with the diagnostic library (RT_HIP_LIB pointing
+at a -DRT_STAMPS build, RT_HIP_STAMPS_FILE set) so the last frame's per-wave
+timeline is dumped; then summarise it (run with --analyse FILE here)."""
+import os
+import sys
+
+if len(sys.argv) > 2 and sys.argv[1] == "--analyse":
+    import numpy as np
+    a = np.fromfile(sys.argv[2], dtype=np.uint64).reshape(-1, 3)
+    n = int(sys.argv[3]) if len(sys.argv) > 3 else (a[:, 1] > 0).sum()
+    a = a[:n]
+    t0 = a[:, 0].min()
+    s = (a[:, 0] - t0) / 100.0  # us (100 MHz)
+    e = (a[:, 1] - t0) / 100.0
+    d = e - s
+    print(f"waves {n}  span {e.max():.1f} us  dur mean {d.mean():.1f} med {np.median(d):.1f} p99 {np.percentile(d,99):.1f} max {d.max():.1f} us")
+    for q in (0.5, 0.9, 0.99, 1.0):
+        print(f"  {q*100:.0f}% of waves started by {np.percentile(s, q*100):.1f} us, ended by {np.percentile(e, q*100):.1f} us")
+    # concurrency over time
+    ts = np.linspace(0, e.max(), 41)
+    conc = [((s <= t) & (e > t)).sum() for t in ts]
+    print("  resident waves over time:", " ".join(str(c) for c in conc))
+    xcc = (a[:, 2] >> 32) & 0xF
+    print("  waves per XCC:", np.bincount(xcc.astype(np.int64), minlength=8).tolist())
+    # duration by tile row (image y)
+    W_tiles = int(sys.argv[4]) if len(sys.argv) > 4 else 240
+    rows = np.arange(n) // W_tiles
+    per_row = [d[rows == r].mean() for r in range(rows.max() + 1)]
+    print("  mean wave duration per tile row (us):", " ".join(f"{x:.0f}" for x in per_row))
+    sys.exit(0)
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "cs420-ray-tracer_amd"))
+import rt_hip  # noqa: E402
+
+scene = sys.argv[1] if len(sys.argv) > 1 else "synth200"
+W, H, D = 1920, 1080, 4
+sc = rt_hip.Scene.load(os.path.join(REPO, "cs420-ray-tracer_amd", "scenes", scene + ".txt"))
+r = rt_hip.Renderer(0)
+r.upload(sc)
+for _ in range(4):
+    _, st = r.render(sc.camera(), W, H, D)
+print("kernel ms", st.kernel_ms)
