@@ -256,72 +256,99 @@ struct Work {
 #endif
 // stamp slots: 0 bound, 1 cull, 2 candidate tests, 3 per-light setup, 4 shading, 5 whole wave
 
+// Lanes of a wave are swept in coherent groups: lanes whose rays leave the
+// same sphere (`key` = that sphere's index; -1 for camera rays) share one
+// bound, so a wave whose secondary rays leave several spheres does not pay the
+// candidate union of all of them.  Each lane takes part in exactly one group
+// pass and only its own pass updates it, so results (and closest-hit ties) are
+// unchanged.  `P` of a group is the origin of its first lane.
+__device__ __forceinline__ unsigned long long next_group(unsigned long long todo, int key) {
+  const int first = __builtin_ctzll(todo);
+  const int kf = __builtin_amdgcn_readlane(key, first);
+  return __ballot(key == kf) & todo;
+}
+
+// Scene::find_intersection (scene.h:41-61): all candidate spheres in file
+// order, strict '<' (so ties keep the lowest index), t starts at 1e20.
 template <bool kCull>
 __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
-                                             bool act, D3 o, D3 d, D3 P, double &best_t, Work &work) {
+                                             bool act, D3 o, D3 d, int key, double &best_t, Work &work) {
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
   double bt = kInf, bn = __builtin_inf();
   int bi = -1;
   const bool fast = a2_ok(a2);
-  const unsigned live = (unsigned)__popcll(__ballot(act));
+  const int lane = (int)(threadIdx.x & 63);
+  unsigned long long todo = __ballot(act);
   RT_CNT(work, sw_closest, 1);
-  Bound B;
-  RT_T0(tb);
-  if (kCull) B = make_bound(act, o, d, P);
-  RT_ACC(work, 0, tb);
-  RT_CNT(work, sweeps, 1);
-  for (int base = 0; base < n; base += 64) {
-    RT_T0(tc);
-    unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
-    RT_ACC(work, 1, tc);
-    RT_T0(tt);
-    if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
-    work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
-    while (mask) {
-      const int i = base + __builtin_ctzll(mask);
-      mask &= mask - 1;
-      // A candidate whose numerator is >= the best's cannot have a strictly
-      // smaller t = fl(num/a2); only would-be new bests pay the division.
-      RT_CNT(work, iters, 1);
-      RT_CNT(work, it_closest, 1);
-      double num;
-      const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
-      if (r == 1) {
-        if (num < bn) {
-          const double t = num / a2;
-          if (t < bt) {
-            bt = t;
-            bn = num;
-            bi = i;
+  while (todo) {
+    const unsigned long long grp = kCull ? next_group(todo, key) : todo;
+    todo &= ~grp;
+    const bool gact = (grp >> lane) & 1ull;
+    const unsigned live = (unsigned)__popcll(grp);
+    Bound B;
+    RT_T0(tb);
+    if (kCull) {
+      const int fl = __builtin_ctzll(grp);
+      B = make_bound(gact, o, d, mk(lane_bcast(o.x, fl), lane_bcast(o.y, fl), lane_bcast(o.z, fl)));
+    }
+    RT_ACC(work, 0, tb);
+    RT_CNT(work, sweeps, 1);
+    for (int base = 0; base < n; base += 64) {
+      RT_T0(tc);
+      unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+      RT_ACC(work, 1, tc);
+      RT_T0(tt);
+      if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
+      work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
+      if (gact) {
+        while (mask) {
+          const int i = base + __builtin_ctzll(mask);
+          mask &= mask - 1;
+          // A candidate whose numerator is >= the best's cannot have a strictly
+          // smaller t = fl(num/a2); only would-be new bests pay the division.
+          RT_CNT(work, iters, 1);
+          RT_CNT(work, it_closest, 1);
+          double num;
+          const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+          if (r == 1) {
+            if (num < bn) {
+              const double t = num / a2;
+              if (t < bt) {
+                bt = t;
+                bn = num;
+                bi = i;
+              }
+            }
+          } else if (r == 2) {
+            double t;
+            if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
+              bt = t;
+              bn = __builtin_inf();  // no numerator for this best: every later candidate divides
+              bi = i;
+            }
           }
         }
-      } else if (r == 2) {
-        double t;
-        if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
-          bt = t;
-          bn = __builtin_inf();  // no numerator for this best: every later candidate divides
-          bi = i;
-        }
       }
+      RT_ACC(work, 2, tt);
     }
-    RT_ACC(work, 2, tt);
   }
   best_t = bt;
   return bi;
 }
 
 // Scene::in_shadow (scene.h:65-86) as an any-hit over the candidates: some
-// sphere with t < 1e20 (the find_intersection start value) and t < dist.  The
-// wave leaves as soon as the ballot of still-unoccluded active lanes is empty.
+// sphere with t < 1e20 (the find_intersection start value) and t < dist.  A
+// group leaves as soon as the ballot of its still-unoccluded lanes is empty.
+// All shadow rays of a light pass (up to rounding) through the light, so P is
+// the light for every group; the key still splits lanes by surface sphere.
 template <bool kCull>
 __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
-                                             bool act, D3 o, D3 d, D3 P, double dist, Work &work) {
-  unsigned long long live = __ballot(act);
-  if (live == 0) return false;
+                                             bool act, D3 o, D3 d, D3 P, int key, double dist, Work &work) {
+  unsigned long long todo = __ballot(act);
+  if (todo == 0) return false;
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
-  bool occ = !act;
   // occluded <=> t < T, T = min(dist, 1e20).  With q = fl(a2*T), a numerator
   // below q(1-2^-48) gives fl(num/a2) < T and one above q(1+2^-48) gives
   // fl(num/a2) > T (both with >2^-50 relative room), so only the band between
@@ -329,43 +356,48 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
   const double T = dist < kInf ? dist : kInf;
   const bool fast = a2_ok(a2) && dist == dist && T >= 0x1p-900;
   const double q = a2 * T, qlo = q * (1.0 - 0x1p-48), qhi = q * (1.0 + 0x1p-48);
-  Bound B;
-  RT_T0(tb);
-  if (kCull) B = make_bound(act, o, d, P);
-  RT_ACC(work, 0, tb);
-  RT_CNT(work, sweeps, 1);
-  for (int base = 0; base < n; base += 64) {
-    RT_T0(tc);
-    unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
-    RT_ACC(work, 1, tc);
-    RT_T0(tt);
-    if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
-    while (mask) {
-      const int i = base + __builtin_ctzll(mask);
-      mask &= mask - 1;
-      work.exact += (unsigned)__popcll(live);
-      RT_CNT(work, iters, 1);
-      if (!occ) {
-        double num;
-        const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
-        if (r == 1) {
-          if (num < qlo) occ = true;
-          else if (!(num > qhi)) {
-            const double t = num / a2;
-            occ = t < kInf && t < dist;
+  const int lane = (int)(threadIdx.x & 63);
+  bool occ = false;
+  while (todo) {
+    const unsigned long long grp = kCull ? next_group(todo, key) : todo;
+    todo &= ~grp;
+    const bool gact = (grp >> lane) & 1ull;
+    unsigned long long live = grp;
+    Bound B;
+    RT_T0(tb);
+    if (kCull) B = make_bound(gact, o, d, P);
+    RT_ACC(work, 0, tb);
+    RT_CNT(work, sweeps, 1);
+    for (int base = 0; base < n && live; base += 64) {
+      RT_T0(tc);
+      unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+      RT_ACC(work, 1, tc);
+      RT_T0(tt);
+      if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
+      while (mask) {
+        const int i = base + __builtin_ctzll(mask);
+        mask &= mask - 1;
+        work.exact += (unsigned)__popcll(live);
+        RT_CNT(work, iters, 1);
+        if (gact && !occ) {
+          double num;
+          const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+          if (r == 1) {
+            if (num < qlo) occ = true;
+            else if (!(num > qhi)) {
+              const double t = num / a2;
+              occ = t < kInf && t < dist;
+            }
+          } else if (r == 2) {
+            double t;
+            occ = intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist;
           }
-        } else if (r == 2) {
-          double t;
-          occ = intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist;
         }
+        live = __ballot(gact && !occ);
+        if (live == 0) break;
       }
-      live = __ballot(!occ);
-      if (live == 0) {
-        RT_ACC(work, 2, tt);
-        return act;
-      }
+      RT_ACC(work, 2, tt);
     }
-    RT_ACC(work, 2, tt);
   }
   return act && occ;
 }

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
                scale(mk(cam.ux, cam.uy, cam.uz), sv));
   D3 d = normalized(normalized(dir));  // get_ray normalises, Ray() normalises again
   D3 o = mk(cam.px, cam.py, cam.pz);
-  D3 P = o;
+  int key = -1;  // sphere the current ray leaves (-1: camera), groups lanes in sweeps
 
   // Reflection stack, one slot per level and lane, in LDS (kLdsStack: after
   // the staged scene) or in per-lane private memory for the deepest variant.
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
 #ifdef RT_STAMPS
     const unsigned long long it_before = work.it_closest;
 #endif
-    const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, P, bt, work);
+    const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, key, bt, work);
 #ifdef RT_STAMPS
     if (dleft == depth) work.it_prim += work.it_closest - it_before;
 #endif
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
         const D3 ldir = normalized(to_light);
         const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
         RT_ACC(work, 3, t_setup);
-        if (sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, dist, work)) occm |= 1ull << (l - l0);
+        if (sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, hi, dist, work)) occm |= 1ull << (l - l0);
       }
       RT_T0(t_shade);
       if (hit && occm != ~0ull >> (64 - (lend - l0))) {
@@ -191,6 +191,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
           const D3 rd = sub(d, scale(scale(nrm, 2.0), dot(d, nrm)));
           o = add(hp, scale(nrm, kEps));
           d = normalized(rd);
+          key = hi;
           --dleft;
           ++c_reflect;
         } else {
@@ -201,11 +202,6 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
         res = col;
         alive = false;
       }
-    }
-    const unsigned long long am = __ballot(alive);
-    if (am) {  // next reference point: the origin of the first still-alive lane
-      const int fl = __builtin_ctzll(am);
-      P = mk(__shfl(o.x, fl, 64), __shfl(o.y, fl, 64), __shfl(o.z, fl, 64));
     }
   }
   while (lev > 0) {  // unwind: shade*(1-refl) + reflected*refl, innermost first

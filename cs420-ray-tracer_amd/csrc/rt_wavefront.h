@@ -36,7 +36,7 @@ namespace rtk {
 struct __attribute__((aligned(16))) RayRec {  // 64 B
   double ox, oy, oz, dx, dy, dz;
   int pix, dleft;
-  double pad;
+  int key, pad;  // key: sphere the ray leaves
 };
 struct __attribute__((aligned(16))) HitRec {  // 80 B
   double ox, oy, oz, dx, dy, dz, t;
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void wf_primary(WfArgs a) {
   const bool alive = in_img && a.depth >= 1;
   Work work;
   double bt;
-  const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, o, bt, work);
+  const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, -1, bt, work);
   const bool hit = alive && bi >= 0;
   if (in_img && !hit) {
     const D3 c = alive ? sky(d) : mk(0.0, 0.0, 0.0);  // depth <= 0 is black (main.cpp:17-18)
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
       const double dist = length(to_light);
       const D3 ldir = normalized(to_light);
       const bool occ =
-          sweep_shadow<kCull>(g, rad, a.n, hit, add(hp, scale(ldir, kEps)), normalized(ldir), lp, dist, work);
+          sweep_shadow<kCull>(g, rad, a.n, hit, add(hp, scale(ldir, kEps)), normalized(ldir), lp, h.sph, dist, work);
       if (hit && !occ) {
         const double ndl = max0(dot(nrm, ldir));
         const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
     }
     const unsigned slot = wave_append(spawn, &a.ray_cnt[(level + 1) * kShards + shard]);
     if (spawn)
-      a.rayq[(size_t)shard * a.seg_cap + slot] = RayRec{ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, h.pix, h.dleft - 1, 0.0};
+      a.rayq[(size_t)shard * a.seg_cap + slot] = RayRec{ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, h.pix, h.dleft - 1, h.sph, 0};
     n_reflect += (unsigned long long)__popcll(__ballot(spawn));
   }
   if (lane == 0) {
@@ -268,9 +268,8 @@ __global__ __launch_bounds__(256) void wf_reflect(WfArgs a, int level) {
     const bool alive = idx < cnt;
     const RayRec r = rq[alive ? idx : base];
     const D3 o = mk(r.ox, r.oy, r.oz), d = mk(r.dx, r.dy, r.dz);
-    const D3 P = mk(lane_bcast(o.x, 0), lane_bcast(o.y, 0), lane_bcast(o.z, 0));  // lane 0 is always live
     double bt;
-    const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, P, bt, work);
+    const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, r.key, bt, work);
     const bool hit = alive && bi >= 0;
     if (alive && !hit) {
       const D3 c = sky(d);
