@@ -36,7 +36,8 @@ namespace rtk {
 // Diagnostic timeline: per wave {start, end} (s_memrealtime, 100 MHz) and
 // {HW_ID, XCC_ID}; dumped by rt_render_stats when RT_HIP_STAMPS_FILE is set.
 constexpr int kTimelineWaves = 1 << 17;
-__device__ unsigned long long g_timeline[kTimelineWaves * 3];
+constexpr int kTl = 10;  // u64 per wave
+__device__ unsigned long long g_timeline[kTimelineWaves * kTl];
 #endif
 
 // One lane per pixel; the whole wave walks the reflection levels together
@@ -233,11 +234,19 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   if (lane == 0) {
     const unsigned wid = (blockIdx.x + blockIdx.y * gridDim.x) * kWaves + wave;
     if (wid < (unsigned)kTimelineWaves) {
-      g_timeline[3 * wid] = t_real0;
-      g_timeline[3 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+      unsigned long long *tl = g_timeline + (size_t)kTl * wid;
+      tl[0] = t_real0;
+      tl[1] = __builtin_amdgcn_s_memrealtime();
       const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
       const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
-      g_timeline[3 * wid + 2] = ((unsigned long long)xcc << 32) | hw;
+      tl[2] = ((unsigned long long)xcc << 32) | hw;
+      tl[3] = work.st[0];  // bound cycles
+      tl[4] = work.st[1];  // cull
+      tl[5] = work.st[2];  // candidates
+      tl[6] = work.st[4];  // shading
+      tl[7] = work.st[5];  // total
+      tl[8] = work.iters | (work.sweeps << 32);
+      tl[9] = (unsigned long long)__popcll(__ballot(in_img)) | ((unsigned long long)depth << 32);
     }
   }
 #endif
@@ -646,7 +655,7 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
   st->tests_cull = sum[5];
 #ifdef RT_STAMPS
   if (const char *tf = std::getenv("RT_HIP_STAMPS_FILE")) {
-    static unsigned long long host_tl[kTimelineWaves * 3];
+    static unsigned long long host_tl[kTimelineWaves * kTl];
     if (hipMemcpyFromSymbol(host_tl, HIP_SYMBOL(g_timeline), sizeof(host_tl)) == hipSuccess) {
       if (FILE *f = std::fopen(tf, "wb")) {
         std::fwrite(host_tl, sizeof(host_tl), 1, f);
