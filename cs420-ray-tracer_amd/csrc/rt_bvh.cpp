@@ -1,0 +1,156 @@
+// rt_bvh.cpp -- host-side binned-SAH BVH builder for the sphere list.
+#include "rt_bvh.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+namespace rtk {
+namespace {
+
+struct Box {
+  double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+  void grow(const double *l, const double *h) {
+    for (int k = 0; k < 3; k++) {
+      lo[k] = std::min(lo[k], l[k]);
+      hi[k] = std::max(hi[k], h[k]);
+    }
+  }
+  double area() const {
+    if (lo[0] > hi[0]) return 0.0;
+    double e[3];
+    for (int k = 0; k < 3; k++) e[k] = hi[k] - lo[k];
+    return 2.0 * (e[0] * e[1] + e[1] * e[2] + e[2] * e[0]);
+  }
+};
+
+struct Prim {
+  double lo[3], hi[3], c[3];
+  int32_t id;
+};
+
+float round_down(double v) {
+  float f = (float)v;
+  if ((double)f > v) f = std::nextafter(f, -FLT_MAX);
+  return f;
+}
+float round_up(double v) {
+  float f = (float)v;
+  if ((double)f < v) f = std::nextafter(f, FLT_MAX);
+  return f;
+}
+
+struct Builder {
+  std::vector<Prim> &p;
+  int max_leaf;
+  std::vector<BvhNode> &nodes;
+  std::vector<int32_t> &prims;
+
+  void emit_box(BvhNode &nd, const Box &b) {
+    for (int k = 0; k < 3; k++) {
+      nd.lo[k] = round_down(b.lo[k]);
+      nd.hi[k] = round_up(b.hi[k]);
+    }
+  }
+
+  // Builds [begin, end) in preorder; returns nothing, fills skip pointers.
+  void build(int begin, int end) {
+    Box b, cb;
+    for (int i = begin; i < end; i++) {
+      b.grow(p[i].lo, p[i].hi);
+      cb.grow(p[i].c, p[i].c);
+    }
+    const int me = (int)nodes.size();
+    nodes.push_back(BvhNode{});
+    emit_box(nodes[me], b);
+    const int count = end - begin;
+    int split = -1;
+    if (count > max_leaf || count > 15) {
+      // binned SAH over the centroid bounds
+      int axis = 0;
+      double ext = -1.0;
+      for (int k = 0; k < 3; k++)
+        if (cb.hi[k] - cb.lo[k] > ext) {
+          ext = cb.hi[k] - cb.lo[k];
+          axis = k;
+        }
+      if (ext > 0.0 && std::isfinite(ext)) {
+        constexpr int kBins = 16;
+        Box bins[kBins];
+        int cnt[kBins] = {};
+        auto bin_of = [&](const Prim &q) {
+          int bi = (int)((q.c[axis] - cb.lo[axis]) / ext * kBins);
+          return std::min(std::max(bi, 0), kBins - 1);
+        };
+        for (int i = begin; i < end; i++) {
+          int bi = bin_of(p[i]);
+          cnt[bi]++;
+          bins[bi].grow(p[i].lo, p[i].hi);
+        }
+        double best = DBL_MAX;
+        int best_bin = -1;
+        for (int s = 1; s < kBins; s++) {
+          Box l, r;
+          int nl = 0, nr = 0;
+          for (int i = 0; i < s; i++)
+            if (cnt[i]) l.grow(bins[i].lo, bins[i].hi), nl += cnt[i];
+          for (int i = s; i < kBins; i++)
+            if (cnt[i]) r.grow(bins[i].lo, bins[i].hi), nr += cnt[i];
+          if (!nl || !nr) continue;
+          double cost = l.area() * nl + r.area() * nr;
+          if (cost < best) {
+            best = cost;
+            best_bin = s;
+          }
+        }
+        if (best_bin > 0) {
+          auto mid = std::partition(p.begin() + begin, p.begin() + end,
+                                    [&](const Prim &q) { return bin_of(q) < best_bin; });
+          split = (int)(mid - p.begin());
+        }
+      }
+      if (split <= begin || split >= end) {  // degenerate centroids: median by index
+        split = begin + count / 2;
+      }
+    }
+    if (split < 0) {
+      nodes[me].leaf = ((int32_t)prims.size() << 4) | count;
+      for (int i = begin; i < end; i++) prims.push_back(p[i].id);
+    } else {
+      nodes[me].leaf = -1;
+      build(begin, split);
+      build(split, end);
+    }
+    nodes[me].skip = (int32_t)nodes.size();
+  }
+};
+
+}  // namespace
+
+void build_bvh(const double *cx, const double *cy, const double *cz, const double *r, int n, int max_leaf,
+               std::vector<BvhNode> &nodes, std::vector<int32_t> &prims) {
+  nodes.clear();
+  prims.clear();
+  if (n <= 0) return;
+  std::vector<Prim> p((size_t)n);
+  for (int i = 0; i < n; i++) {
+    const double c[3] = {cx[i], cy[i], cz[i]};
+    const double rr = std::fabs(r[i]);
+    for (int k = 0; k < 3; k++) {
+      p[i].c[k] = c[k];
+      p[i].lo[k] = c[k] - rr;
+      p[i].hi[k] = c[k] + rr;
+      if (!std::isfinite(p[i].lo[k]) || !std::isfinite(p[i].hi[k])) {  // NaN/inf: a box that always hits
+        p[i].lo[k] = -DBL_MAX;
+        p[i].hi[k] = DBL_MAX;
+        p[i].c[k] = 0.0;
+      }
+    }
+    p[i].id = i;
+  }
+  Builder b{p, std::max(1, std::min(max_leaf, 15)), nodes, prims};
+  nodes.reserve(2 * (size_t)n);
+  b.build(0, n);
+}
+
+}  // namespace rtk

@@ -7,6 +7,8 @@
 
 #include <cstdint>
 
+#include "rt_bvh.h"
+
 #pragma clang fp contract(off)
 
 namespace rtk {
@@ -256,6 +258,57 @@ struct Work {
 #endif
 // stamp slots: 0 bound, 1 cull, 2 candidate tests, 3 per-light setup, 4 shading, 5 whole wave
 
+// ---------------------------------------------------------------------------
+// Per-lane BVH traversal (the fallback for groups whose cull bound is loose).
+// Stackless: nodes in preorder with skip pointers (rt_bvh.h).  The LINE
+// o + t d is tested against each box (both directions of t, so the reference's
+// disc == 0 negative-root hits behind the origin are still found), in fp32
+// relative to the scene centre c0, with every box grown by `margin` =
+// 1e-6 * (scene diameter + largest radius) -- at least the 1e-6 (|oc| + r) that
+// the cull proof above needs, and far above the fp32 rounding (~1e-7 of the
+// diameter) of the slab arithmetic.  Closest-hit prunes a box only when its
+// entry t exceeds the current best by a margin; any-hit prunes beyond T.
+struct BvhArgs {
+  const BvhNode *nodes;
+  const int32_t *prims;
+  int nnodes;
+  float margin;
+  double c0x, c0y, c0z;
+  double diam;          // scene diameter bound used for the t margins
+  int min_cands;        // switch a group to the BVH above this many cull candidates
+  int always;           // 1: skip the cull and traverse for every group
+};
+
+// Visits every leaf whose (grown) box the line meets and whose entry does not
+// exceed tmax_fn() (re-read per node: closest-hit tightens it); calls
+// leaf_fn(sphere index) for each sphere of such leaves.  leaf_fn returns
+// false to stop the walk (any-hit found).
+template <typename T, typename F>
+__device__ __forceinline__ void bvh_walk(const BvhArgs &bv, D3 o, D3 d, T &&tmax_fn, Work &work, F &&leaf_fn) {
+  const float ox = (float)(o.x - bv.c0x), oy = (float)(o.y - bv.c0y), oz = (float)(o.z - bv.c0z);
+  const float ix = 1.0f / (float)d.x, iy = 1.0f / (float)d.y, iz = 1.0f / (float)d.z;
+  const float m = bv.margin;
+  int i = 0;
+  while (i < bv.nnodes) {
+    const BvhNode nd = bv.nodes[i];
+    const float ax = (nd.lo[0] - m - ox) * ix, bx = (nd.hi[0] + m - ox) * ix;
+    const float ay = (nd.lo[1] - m - oy) * iy, by = (nd.hi[1] + m - oy) * iy;
+    const float az = (nd.lo[2] - m - oz) * iz, bz = (nd.hi[2] + m - oz) * iz;
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    const bool in = tn <= tf && !((double)tn > tmax_fn());
+    work.cull += 1;
+    if (in && nd.leaf >= 0) {
+      const int first = nd.leaf >> 4, cnt = nd.leaf & 15;
+      for (int k = 0; k < cnt; ++k)
+        if (!leaf_fn((int)bv.prims[first + k])) return;
+      i = nd.skip;
+    } else {
+      i = in ? i + 1 : nd.skip;
+    }
+  }
+}
+
 // Lanes of a wave are swept in coherent groups: lanes whose rays leave the
 // same sphere (`key` = that sphere's index; -1 for camera rays) share one
 // bound, so a wave whose secondary rays leave several spheres does not pay the
@@ -272,13 +325,39 @@ __device__ __forceinline__ unsigned long long next_group(unsigned long long todo
 // order, strict '<' (so ties keep the lowest index), t starts at 1e20.
 template <bool kCull>
 __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
-                                             bool act, D3 o, D3 d, int key, double &best_t, Work &work) {
+                                             bool act, D3 o, D3 d, int key, const BvhArgs &bv, double &best_t,
+                                             Work &work) {
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
   double bt = kInf, bn = __builtin_inf();
   int bi = -1;
   const bool fast = a2_ok(a2);
   const int lane = (int)(threadIdx.x & 63);
+  // Lexicographic (t, index) minimum == the reference's strict-< scan in file
+  // order (scene.h:50-58); in file order the index tie-break never fires.
+  // A numerator >= the best's with a larger index cannot win, so it skips the
+  // division.
+  auto test = [&](int i) {
+    double num;
+    const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+    if (r == 1) {
+      if (num < bn || i < bi) {
+        const double t = num / a2;
+        if (t < bt || (t == bt && i < bi)) {
+          bt = t;
+          bn = num;
+          bi = i;
+        }
+      }
+    } else if (r == 2) {
+      double t;
+      if (intersect(g[i], o, d, a4, a2, t) && (t < bt || (t == bt && i < bi))) {
+        bt = t;
+        bn = __builtin_inf();  // no numerator for this best: every later candidate divides
+        bi = i;
+      }
+    }
+  };
   unsigned long long todo = __ballot(act);
   RT_CNT(work, sw_closest, 1);
   while (todo) {
@@ -286,51 +365,60 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
     todo &= ~grp;
     const bool gact = (grp >> lane) & 1ull;
     const unsigned live = (unsigned)__popcll(grp);
-    Bound B;
-    RT_T0(tb);
-    if (kCull) {
+    bool use_bvh = kCull && bv.always;
+    if (kCull && !use_bvh) {
+      Bound B;
+      RT_T0(tb);
       const int fl = __builtin_ctzll(grp);
       B = make_bound(gact, o, d, mk(lane_bcast(o.x, fl), lane_bcast(o.y, fl), lane_bcast(o.z, fl)));
-    }
-    RT_ACC(work, 0, tb);
-    RT_CNT(work, sweeps, 1);
-    for (int base = 0; base < n; base += 64) {
-      RT_T0(tc);
-      unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
-      RT_ACC(work, 1, tc);
-      RT_T0(tt);
-      if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
-      work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
-      if (gact) {
-        while (mask) {
-          const int i = base + __builtin_ctzll(mask);
-          mask &= mask - 1;
-          // A candidate whose numerator is >= the best's cannot have a strictly
-          // smaller t = fl(num/a2); only would-be new bests pay the division.
-          RT_CNT(work, iters, 1);
-          RT_CNT(work, it_closest, 1);
-          double num;
-          const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
-          if (r == 1) {
-            if (num < bn) {
-              const double t = num / a2;
-              if (t < bt) {
-                bt = t;
-                bn = num;
-                bi = i;
-              }
-            }
-          } else if (r == 2) {
-            double t;
-            if (intersect(g[i], o, d, a4, a2, t) && t < bt) {
-              bt = t;
-              bn = __builtin_inf();  // no numerator for this best: every later candidate divides
-              bi = i;
-            }
+      RT_ACC(work, 0, tb);
+      RT_CNT(work, sweeps, 1);
+      int seen = 0;
+      for (int base = 0; base < n; base += 64) {
+        RT_T0(tc);
+        unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+        RT_ACC(work, 1, tc);
+        work.cull += (unsigned)(n - base < 64 ? n - base : 64);
+        seen += __popcll(mask);
+        if (bv.nnodes > 0 && seen > bv.min_cands) {  // loose bound: finish this group on the BVH
+          use_bvh = true;
+          break;
+        }
+        RT_T0(tt);
+        work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
+        if (gact) {
+          while (mask) {
+            const int i = base + __builtin_ctzll(mask);
+            mask &= mask - 1;
+            RT_CNT(work, iters, 1);
+            RT_CNT(work, it_closest, 1);
+            test(i);
+          }
+        }
+        RT_ACC(work, 2, tt);
+      }
+    } else if (!kCull) {
+      for (int base = 0; base < n; base += 64) {
+        unsigned long long mask = candidates<false>(g, rad, n, base, Bound{});
+        work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
+        if (gact) {
+          while (mask) {
+            const int i = base + __builtin_ctzll(mask);
+            mask &= mask - 1;
+            test(i);
           }
         }
       }
-      RT_ACC(work, 2, tt);
+    }
+    if (use_bvh && gact) {
+      RT_T0(tv);
+      // a box whose entry is beyond the best t (by the margin) holds no closer root
+      bvh_walk(bv, o, d, [&] { return bt + 2e-6 * (bv.diam + __builtin_fabs(bt)); }, work, [&](int i) {
+        work.exact += 1;
+        test(i);
+        return true;
+      });
+      RT_ACC(work, 6, tv);
     }
   }
   best_t = bt;
@@ -344,7 +432,8 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
 // the light for every group; the key still splits lanes by surface sphere.
 template <bool kCull>
 __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
-                                             bool act, D3 o, D3 d, D3 P, int key, double dist, Work &work) {
+                                             bool act, D3 o, D3 d, D3 P, int key, double dist, const BvhArgs &bv,
+                                             Work &work) {
   unsigned long long todo = __ballot(act);
   if (todo == 0) return false;
   const double a = dot(d, d);
@@ -358,45 +447,69 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
   const double q = a2 * T, qlo = q * (1.0 - 0x1p-48), qhi = q * (1.0 + 0x1p-48);
   const int lane = (int)(threadIdx.x & 63);
   bool occ = false;
+  auto test = [&](int i) {
+    double num;
+    const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+    if (r == 1) {
+      if (num < qlo) occ = true;
+      else if (!(num > qhi)) {
+        const double t = num / a2;
+        occ = t < kInf && t < dist;
+      }
+    } else if (r == 2) {
+      double t;
+      occ = intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist;
+    }
+  };
   while (todo) {
     const unsigned long long grp = kCull ? next_group(todo, key) : todo;
     todo &= ~grp;
     const bool gact = (grp >> lane) & 1ull;
     unsigned long long live = grp;
-    Bound B;
-    RT_T0(tb);
-    if (kCull) B = make_bound(gact, o, d, P);
-    RT_ACC(work, 0, tb);
-    RT_CNT(work, sweeps, 1);
-    for (int base = 0; base < n && live; base += 64) {
-      RT_T0(tc);
-      unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
-      RT_ACC(work, 1, tc);
-      RT_T0(tt);
-      if (kCull) work.cull += (unsigned)(n - base < 64 ? n - base : 64);
-      while (mask) {
-        const int i = base + __builtin_ctzll(mask);
-        mask &= mask - 1;
-        work.exact += (unsigned)__popcll(live);
-        RT_CNT(work, iters, 1);
-        if (gact && !occ) {
-          double num;
-          const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
-          if (r == 1) {
-            if (num < qlo) occ = true;
-            else if (!(num > qhi)) {
-              const double t = num / a2;
-              occ = t < kInf && t < dist;
-            }
-          } else if (r == 2) {
-            double t;
-            occ = intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist;
+    bool use_bvh = kCull && bv.always;
+    if (!use_bvh) {
+      Bound B;
+      RT_T0(tb);
+      if (kCull) B = make_bound(gact, o, d, P);
+      RT_ACC(work, 0, tb);
+      RT_CNT(work, sweeps, 1);
+      int seen = 0;
+      for (int base = 0; base < n && live; base += 64) {
+        RT_T0(tc);
+        unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+        RT_ACC(work, 1, tc);
+        if (kCull) {
+          work.cull += (unsigned)(n - base < 64 ? n - base : 64);
+          seen += __popcll(mask);
+          if (bv.nnodes > 0 && seen > bv.min_cands) {
+            use_bvh = true;
+            break;
           }
         }
-        live = __ballot(gact && !occ);
-        if (live == 0) break;
+        RT_T0(tt);
+        while (mask) {
+          const int i = base + __builtin_ctzll(mask);
+          mask &= mask - 1;
+          work.exact += (unsigned)__popcll(live);
+          RT_CNT(work, iters, 1);
+          if (gact && !occ) test(i);
+          live = __ballot(gact && !occ);
+          if (live == 0) break;
+        }
+        RT_ACC(work, 2, tt);
       }
-      RT_ACC(work, 2, tt);
+    }
+    if (use_bvh && gact && !occ) {
+      RT_T0(tv);
+      // boxes entirely beyond T (by the margin) cannot occlude; boxes behind the
+      // origin are still visited (negative tangent roots count, sphere.h:43-47)
+      const double tmax = T + 2e-6 * (bv.diam + T);
+      bvh_walk(bv, o, d, [&] { return tmax; }, work, [&](int i) {
+        work.exact += 1;
+        test(i);
+        return !occ;
+      });
+      RT_ACC(work, 6, tv);
     }
   }
   return act && occ;

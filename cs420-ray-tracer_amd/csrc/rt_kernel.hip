@@ -30,6 +30,9 @@
 #include "rt_device.h"
 #include "rt_wavefront.h"
 
+#include <cmath>
+#include <vector>
+
 namespace rtk {
 
 #ifdef RT_STAMPS
@@ -49,7 +52,7 @@ template <int MAXS, bool kLdsGeo, bool kCull, int kWaves, bool kLdsStack = (MAXS
 __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kernel(const SphGeo *__restrict__ geo, const double *__restrict__ radius,
                                                         const SphMat *__restrict__ mat,
                                                         const LightD *__restrict__ lights, int n, int nl, D3 amb,
-                                                        Cam cam, int W, int H, int depth, Rows rows,
+                                                        Cam cam, int W, int H, int depth, Rows rows, BvhArgs bv,
                                                         uint8_t *__restrict__ out,
                                                         unsigned long long *__restrict__ counters) {
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
 #ifdef RT_STAMPS
     const unsigned long long it_before = work.it_closest;
 #endif
-    const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, key, bt, work);
+    const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, key, bv, bt, work);
 #ifdef RT_STAMPS
     if (dleft == depth) work.it_prim += work.it_closest - it_before;
 #endif
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
         const D3 ldir = normalized(to_light);
         const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
         RT_ACC(work, 3, t_setup);
-        if (sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, hi, dist, work)) occm |= 1ull << (l - l0);
+        if (sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, hi, dist, bv, work)) occm |= 1ull << (l - l0);
       }
       RT_T0(t_shade);
       if (hit && occm != ~0ull >> (64 - (lend - l0))) {
@@ -246,6 +249,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
       tl[6] = work.st[4];  // shading
       tl[7] = work.st[5];  // total
       tl[8] = work.iters | (work.sweeps << 32);
+      tl[4] = work.st[6];  // (timeline) bvh cycles in place of cull
       tl[9] = (unsigned long long)__popcll(__ballot(in_img)) | ((unsigned long long)depth << 32);
     }
   }
@@ -254,6 +258,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
     unsigned long long *sc = counter_shard(counters);
 #ifdef RT_STAMPS
     for (int q = 0; q < 6; q++) atomicAdd(&sc[8 + q], work.st[q]);
+    atomicAdd(&sc[20], work.st[6]);
     atomicAdd(&sc[14], 1ull);
     atomicAdd(&sc[15], work.iters);
     atomicAdd(&sc[16], work.sweeps);
@@ -295,6 +300,14 @@ struct rt_ctx {
   double *d_rad = nullptr;  // |radius|, for the conservative cull only
   SphMat *d_mat = nullptr;
   bool cull = true;
+  // BVH over the spheres (fallback for incoherent groups), built at upload
+  BvhNode *d_bvh = nullptr;
+  int32_t *d_prims = nullptr;
+  int bvh_nodes = 0;
+  double c0[3] = {0, 0, 0};
+  double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
+  double rmax = 0;
+  int bvh_min = 24, bvh_always = 0, bvh_on = 1;
   int wg_waves = 1;  // megakernel waves per workgroup (tuning knob RT_HIP_WG_WAVES = 1 | 4)
   int pipeline = 0;  // 0 = megakernel (default), 1 = wavefront queues (knob RT_HIP_PIPELINE)
   int n_cu = 256;
@@ -335,6 +348,11 @@ void free_scene(rt_ctx *c) {
   if (c->d_rad) (void)hipFree(c->d_rad);
   if (c->d_mat) (void)hipFree(c->d_mat);
   if (c->d_lights) (void)hipFree(c->d_lights);
+  if (c->d_bvh) (void)hipFree(c->d_bvh);
+  if (c->d_prims) (void)hipFree(c->d_prims);
+  c->d_bvh = nullptr;
+  c->d_prims = nullptr;
+  c->bvh_nodes = 0;
   c->d_geo = nullptr;
   c->d_rad = nullptr;
   c->d_mat = nullptr;
@@ -342,20 +360,46 @@ void free_scene(rt_ctx *c) {
   c->has_scene = false;
 }
 
+// BVH arguments for one render: the scene extent includes the camera (the
+// origin of primary rays); margin = 1e-6 * (diameter + largest radius).
+BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
+  BvhArgs b;
+  b.nodes = c->d_bvh;
+  b.prims = c->d_prims;
+  b.nnodes = (c->bvh_on && c->cull) ? c->bvh_nodes : 0;
+  b.c0x = c->c0[0];
+  b.c0y = c->c0[1];
+  b.c0z = c->c0[2];
+  const double cp[3] = {cam.px, cam.py, cam.pz};
+  double d2 = 0.0;
+  for (int k = 0; k < 3; k++) {
+    const double l = std::min(c->lo[k], cp[k]), h = std::max(c->hi[k], cp[k]);
+    d2 += (h - l) * (h - l);
+  }
+  b.diam = std::sqrt(d2) + 0.01;  // + the 0.001 origin offsets of secondary rays
+  const double m = 1e-6 * (b.diam + c->rmax);
+  b.margin = std::isfinite(m) ? (float)(m * (1.0 + 1e-6)) : INFINITY;
+  if (!std::isfinite(b.diam)) b.diam = INFINITY;
+  b.min_cands = c->bvh_min;
+  b.always = c->bvh_always;
+  return b;
+}
+
 template <int MAXS, bool kCull, int kWaves>
 void launch_render3(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
                     uint8_t *out) {
+  const BvhArgs bv = bvh_args(c, cam);
   constexpr int kWx = kWaves == 4 ? 2 : 1, kWy = kWaves / kWx;
   dim3 grid((W + 8 * kWx - 1) / (8 * kWx), (rows.count + 8 * kWy - 1) / (8 * kWy));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   if (MAXS <= 4) lds = ((lds + 31) & ~(size_t)31) + (size_t)kWaves * 64 * MAXS * sizeof(StackEnt);
   if (lds_geo)
     hipLaunchKernelGGL((render_kernel<MAXS, true, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out,
+                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, out,
                        c->d_counters);
   else
     hipLaunchKernelGGL((render_kernel<MAXS, false, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, out,
+                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, out,
                        c->d_counters);
 }
 
@@ -451,6 +495,7 @@ int launch_wavefront(rt_ctx *c, const Cam &cam, int W, int H, int depth, const R
   a.npx = r.count * W;
   a.out = dst;
   a.counters = c->d_counters;
+  a.bv = bvh_args(c, cam);
   const size_t wgs = (size_t)((W + 15) / 16) * (size_t)((r.count + 15) / 16);
   const size_t seg_cap = (wgs + kShards - 1) / kShards * 256;
   int rc = ensure_wf(c, (size_t)a.npx, depth, seg_cap, a);
@@ -528,6 +573,9 @@ int rt_create(int device, rt_ctx **out) {
   c->device = device;
   if (const char *e = std::getenv("RT_HIP_WG_WAVES")) c->wg_waves = std::atoi(e) == 4 ? 4 : 1;
   if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::atoi(e) == 1 ? 1 : 0;
+  if (const char *e = std::getenv("RT_HIP_BVH")) c->bvh_on = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_BVH_MIN")) c->bvh_min = std::atoi(e);
+  if (const char *e = std::getenv("RT_HIP_BVH_ALWAYS")) c->bvh_always = std::atoi(e) != 0;
   auto bail = [&](int rc) {
     rt_destroy(c);
     return rc;
@@ -603,8 +651,56 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     const rt_light &L = s->lights[i];
     hl[i] = LightD{L.position[0], L.position[1], L.position[2], L.color[0], L.color[1], L.color[2]};
   }
+  // scene bounds (spheres and lights), centre, largest radius; BVH relative to the centre
+  double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300}, rmax = 0.0;
+  auto grow = [&](const double *p, double r) {
+    for (int k = 0; k < 3; k++) {
+      lo[k] = std::min(lo[k], p[k] - r);
+      hi[k] = std::max(hi[k], p[k] + r);
+    }
+  };
+  for (int i = 0; i < n; i++) {
+    const double r = std::fabs(s->spheres[i].radius);
+    grow(s->spheres[i].center, r);
+    if (r > rmax || r != r) rmax = r != r ? INFINITY : r;
+  }
+  for (int i = 0; i < nl; i++) grow(s->lights[i].position, 0.0);
+  double c0[3] = {0, 0, 0};
+  if (n + nl > 0)
+    for (int k = 0; k < 3; k++) c0[k] = std::isfinite(lo[k] + hi[k]) ? 0.5 * (lo[k] + hi[k]) : 0.0;
+  std::vector<double> bx(n), by(n), bz(n), br(n);
+  for (int i = 0; i < n; i++) {
+    bx[i] = s->spheres[i].center[0] - c0[0];
+    by[i] = s->spheres[i].center[1] - c0[1];
+    bz[i] = s->spheres[i].center[2] - c0[2];
+    br[i] = s->spheres[i].radius;
+  }
+  std::vector<BvhNode> nodes;
+  std::vector<int32_t> prims;
+  build_bvh(bx.data(), by.data(), bz.data(), br.data(), n, 4, nodes, prims);
   int rc = RT_OK;
   hipError_t e = hipSuccess;
+  if ((e = hipMalloc(&c->d_bvh, sizeof(BvhNode) * (nodes.size() + 1))) != hipSuccess ||
+      (e = hipMalloc(&c->d_prims, sizeof(int32_t) * (prims.size() + 1))) != hipSuccess ||
+      (!nodes.empty() &&
+       (e = hipMemcpy(c->d_bvh, nodes.data(), sizeof(BvhNode) * nodes.size(), hipMemcpyHostToDevice)) != hipSuccess) ||
+      (!prims.empty() &&
+       (e = hipMemcpy(c->d_prims, prims.data(), sizeof(int32_t) * prims.size(), hipMemcpyHostToDevice)) != hipSuccess)) {
+    rc = fail(c, e, "rt_upload_scene(bvh)");
+    free_scene(c);
+    delete[] hg;
+    delete[] hr;
+    delete[] hm;
+    delete[] hl;
+    return rc;
+  }
+  c->bvh_nodes = (int)nodes.size();
+  for (int k = 0; k < 3; k++) {
+    c->c0[k] = c0[k];
+    c->lo[k] = lo[k];
+    c->hi[k] = hi[k];
+  }
+  c->rmax = rmax;
   if ((e = hipMalloc(&c->d_geo, sizeof(SphGeo) * (n + 1))) != hipSuccess ||
       (e = hipMalloc(&c->d_rad, sizeof(double) * (n + 1))) != hipSuccess ||
       (e = hipMalloc(&c->d_mat, sizeof(SphMat) * (n + 1))) != hipSuccess ||
@@ -669,10 +765,12 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
     for (int sh = 0; sh < kShards; sh++)
       for (int q = 0; q < 12; q++) d[q] += c->h_counters[sh * kShardStride + 8 + q];
     const double nw = (double)(d[6] ? d[6] : 1);
+    unsigned long long bvh = 0;
+    for (int sh = 0; sh < kShards; sh++) bvh += c->h_counters[sh * kShardStride + 20];
     std::fprintf(stderr,
                  "RT_STAMPS per wave: candidate iterations %.1f (closest %.1f, of which primary %.1f), sweeps %.2f "
-                 "(closest %.2f)\n",
-                 d[7] / nw, d[9] / nw, d[11] / nw, d[8] / nw, d[10] / nw);
+                 "(closest %.2f), bvh cycles %.0f\n",
+                 d[7] / nw, d[9] / nw, d[11] / nw, d[8] / nw, d[10] / nw, bvh / nw);
     std::fprintf(stderr, "RT_STAMPS waves=%llu cycles/wave: bound %.0f cull %.0f cand %.0f setup %.0f shade %.0f total %.0f\n",
                  d[6], (double)d[0] / (d[6] ? d[6] : 1), (double)d[1] / (d[6] ? d[6] : 1),
                  (double)d[2] / (d[6] ? d[6] : 1), (double)d[3] / (d[6] ? d[6] : 1),

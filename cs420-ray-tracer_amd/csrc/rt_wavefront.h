@@ -81,6 +81,7 @@ struct WfArgs {
   StackEnt *stack;    // [(depth-1) * npx]
   uint8_t *out;
   unsigned long long *counters;
+  BvhArgs bv;
 };
 
 // Stage sphere geometry/radii (if they fit) and lights into LDS.
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(256) void wf_primary(WfArgs a) {
   const bool alive = in_img && a.depth >= 1;
   Work work;
   double bt;
-  const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, -1, bt, work);
+  const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, -1, a.bv, bt, work);
   const bool hit = alive && bi >= 0;
   if (in_img && !hit) {
     const D3 c = alive ? sky(d) : mk(0.0, 0.0, 0.0);  // depth <= 0 is black (main.cpp:17-18)
@@ -202,7 +203,8 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
       const double dist = length(to_light);
       const D3 ldir = normalized(to_light);
       const bool occ =
-          sweep_shadow<kCull>(g, rad, a.n, hit, add(hp, scale(ldir, kEps)), normalized(ldir), lp, h.sph, dist, work);
+          sweep_shadow<kCull>(g, rad, a.n, hit, add(hp, scale(ldir, kEps)), normalized(ldir), lp, h.sph, dist, a.bv,
+                              work);
       if (hit && !occ) {
         const double ndl = max0(dot(nrm, ldir));
         const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
@@ -269,7 +271,7 @@ __global__ __launch_bounds__(256) void wf_reflect(WfArgs a, int level) {
     const RayRec r = rq[alive ? idx : base];
     const D3 o = mk(r.ox, r.oy, r.oz), d = mk(r.dx, r.dy, r.dz);
     double bt;
-    const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, r.key, bt, work);
+    const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, r.key, a.bv, bt, work);
     const bool hit = alive && bi >= 0;
     if (alive && !hit) {
       const D3 c = sky(d);

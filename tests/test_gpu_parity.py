@@ -270,3 +270,57 @@ def test_cull_equals_bruteforce_at_4k(gpu_renderer):
         gpu_renderer.set_culling(True)
     assert bytes(a) == bytes(b)
     assert sa.rays == sb.rays
+
+
+@pytest.fixture(params=[{"RT_HIP_BVH_ALWAYS": "1"}, {"RT_HIP_BVH_MIN": "0"}, {"RT_HIP_BVH": "0"}],
+                ids=["bvh-always", "bvh-min0", "bvh-off"])
+def bvh_renderer(request, monkeypatch):
+    """A fresh context per BVH policy (the knobs are read at rt_create)."""
+    import rt_hip
+
+    for k, v in request.param.items():
+        monkeypatch.setenv(k, v)
+    r = rt_hip.Renderer(0)
+    yield r
+    r.close()
+
+
+@pytest.mark.parametrize("name", ["complex_97x61_d4", "medium_1280x720_d10", "synth200_1920x1080_d4",
+                                  "synth10k_384x216_d6", "simple_1x1_d10"])
+def test_bvh_policies_golden(bvh_renderer, name):
+    rgb, st, m = _render(bvh_renderer, name)
+    assert rgb == golden_rgb(name), diff_summary(rgb, golden_rgb(name))
+    assert {"primary": st.rays_primary, "shadow": st.rays_shadow, "reflect": st.rays_reflect} == m["rays"]
+
+
+@pytest.mark.parametrize("seed", range(0, 12, 3))
+def test_bvh_policies_random_scenes(bvh_renderer, seed):
+    import orc
+    import rt_hip
+
+    text = _random_scene(seed, 60 + 40 * seed)
+    W, H, D = 96, 64, 5
+    sc = rt_hip.Scene.parse(text)
+    bvh_renderer.upload(sc)
+    ref, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=4)
+    rgb, st = bvh_renderer.render(sc.camera(), W, H, D)
+    assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
+
+
+def test_bvh_far_from_origin(bvh_renderer):
+    """Scene translated far from the origin: the fp32 BVH works relative to the scene centre."""
+    import orc
+    import rt_hip
+
+    lines = []
+    for i in range(40):
+        lines.append("sphere %d %d %d 0.7 0.5 0.5 0.9 0.3 0.5 20" % (100000 + (i % 7) * 2, 100000 + (i // 7),
+                                                                     -100020 - (i % 5) * 3))
+    lines += ["light 100010 100020 -100000 1 1 1 1", "light 99990 100010 -100005 0.5 0.6 0.7 1",
+              "camera 100004 100003 -99990 100004 100003 -100020 50"]
+    text = "\n".join(lines) + "\n"
+    sc = rt_hip.Scene.parse(text)
+    bvh_renderer.upload(sc)
+    ref, _, _ = orc.OracleScene(text=text).render(80, 60, 6, threads=4)
+    rgb, _ = bvh_renderer.render(sc.camera(), 80, 60, 6)
+    assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
