@@ -248,8 +248,17 @@ struct Work {
 #endif
 };
 #ifdef RT_STAMPS
-#define RT_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define RT_ACC(w, slot, v) (w).st[slot] += __builtin_amdgcn_s_memtime() - (v)
+// Each stamp first drains outstanding memory operations and fences the
+// scheduler, so a phase's latency is charged to that phase.
+__device__ __forceinline__ unsigned long long rt_stamp() {
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define RT_T0(v) const unsigned long long v = rt_stamp()
+#define RT_ACC(w, slot, v) (w).st[slot] += rt_stamp() - (v)
 #define RT_CNT(w, f, n) (w).f += (n)
 #else
 #define RT_CNT(w, f, n)
@@ -277,6 +286,7 @@ struct BvhArgs {
   double diam;          // scene diameter bound used for the t margins
   int min_cands;        // switch a group to the BVH above this many cull candidates
   int always;           // 1: skip the cull and traverse for every group
+  int max_groups;       // lanes of groups beyond this many go straight to the BVH
 };
 
 // Visits every leaf whose (grown) box the line meets and whose entry does not
@@ -296,8 +306,13 @@ __device__ __forceinline__ void bvh_walk(const BvhArgs &bv, D3 o, D3 d, T &&tmax
     const float az = (nd.lo[2] - m - oz) * iz, bz = (nd.hi[2] + m - oz) * iz;
     const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+#ifdef RT_EXPERIMENT_FWD  // diagnostic only (not exact): skip boxes wholly behind the origin
+    const bool in = tn <= tf && tf >= -m && !((double)tn > tmax_fn());
+#else
     const bool in = tn <= tf && !((double)tn > tmax_fn());
+#endif
     work.cull += 1;
+    RT_CNT(work, st[7], 1);
     if (in && nd.leaf >= 0) {
       const int first = nd.leaf >> 4, cnt = nd.leaf & 15;
       for (int k = 0; k < cnt; ++k)
@@ -306,6 +321,59 @@ __device__ __forceinline__ void bvh_walk(const BvhArgs &bv, D3 o, D3 d, T &&tmax
     } else {
       i = in ? i + 1 : nd.skip;
     }
+  }
+}
+
+// LDS layout of a staged scene: sphere geometry, radii, lights and, when the
+// scene is staged (lds_geo) and has a BVH, its nodes and leaf sphere indices.
+// The host sizes the dynamic LDS with the same function.
+struct LdsLayout {
+  size_t rad, light, nodes, prims, end;
+};
+__host__ __device__ inline LdsLayout lds_layout(bool lds_geo, int n, int nl, int nnodes) {
+  LdsLayout L;
+  L.rad = lds_geo ? (size_t)n * sizeof(SphGeo) : 0;
+  L.light = lds_geo ? (size_t)n * (sizeof(SphGeo) + sizeof(double)) : 0;
+  size_t e = (L.light + (size_t)nl * sizeof(LightD) + 15) & ~(size_t)15;
+  L.nodes = e;
+  if (lds_geo && nnodes > 0) e += (size_t)nnodes * sizeof(BvhNode);
+  L.prims = e;
+  if (lds_geo && nnodes > 0) e += (size_t)n * sizeof(int32_t);
+  L.end = e;
+  return L;
+}
+
+// Copies the scene (and, with kLdsGeo, its BVH) into LDS; g/rad/lights and
+// bv.nodes/bv.prims then point at the LDS copies.  Ends with a barrier.
+template <bool kLdsGeo>
+__device__ __forceinline__ void stage_scene(unsigned char *smem, const SphGeo *geo, const double *radius,
+                                            const LightD *lights, int n, int nl, BvhArgs &bv, const SphGeo *&g,
+                                            const double *&rad, const LightD *&sl) {
+  const LdsLayout L = lds_layout(kLdsGeo, n, nl, bv.nnodes);
+  SphGeo *sgeo = reinterpret_cast<SphGeo *>(smem);
+  double *srad = reinterpret_cast<double *>(smem + L.rad);
+  LightD *slight = reinterpret_cast<LightD *>(smem + L.light);
+  BvhNode *snodes = reinterpret_cast<BvhNode *>(smem + L.nodes);
+  int32_t *sprims = reinterpret_cast<int32_t *>(smem + L.prims);
+  const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
+  if (kLdsGeo) {
+    for (int i = tid; i < n; i += nt) {
+      sgeo[i] = geo[i];
+      srad[i] = radius[i];
+    }
+    if (bv.nnodes > 0) {
+      for (int i = tid; i < bv.nnodes; i += nt) snodes[i] = bv.nodes[i];
+      for (int i = tid; i < n; i += nt) sprims[i] = bv.prims[i];
+    }
+  }
+  for (int i = tid; i < nl; i += nt) slight[i] = lights[i];
+  __syncthreads();
+  g = kLdsGeo ? sgeo : geo;
+  rad = kLdsGeo ? srad : radius;
+  sl = slight;
+  if (kLdsGeo) {
+    bv.nodes = snodes;
+    bv.prims = sprims;
   }
 }
 
@@ -360,13 +428,23 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
   };
   unsigned long long todo = __ballot(act);
   RT_CNT(work, sw_closest, 1);
+  // Lanes whose group bound is loose (or that come after max_groups groups)
+  // are collected in `need` and walk the BVH together after the group passes,
+  // so the divergent walks of different groups overlap instead of queueing.
+  const bool have_bvh = kCull && bv.nnodes > 0;
+  bool need = false;
+  int groups = 0;
   while (todo) {
+    if (have_bvh && (bv.always || groups >= bv.max_groups)) {
+      need = need || ((todo >> lane) & 1ull);
+      break;
+    }
     const unsigned long long grp = kCull ? next_group(todo, key) : todo;
     todo &= ~grp;
+    ++groups;
     const bool gact = (grp >> lane) & 1ull;
     const unsigned live = (unsigned)__popcll(grp);
-    bool use_bvh = kCull && bv.always;
-    if (kCull && !use_bvh) {
+    if (kCull) {
       Bound B;
       RT_T0(tb);
       const int fl = __builtin_ctzll(grp);
@@ -380,8 +458,8 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
         RT_ACC(work, 1, tc);
         work.cull += (unsigned)(n - base < 64 ? n - base : 64);
         seen += __popcll(mask);
-        if (bv.nnodes > 0 && seen > bv.min_cands) {  // loose bound: finish this group on the BVH
-          use_bvh = true;
+        if (have_bvh && seen > bv.min_cands) {  // loose bound: this group walks the BVH
+          need = need || gact;
           break;
         }
         RT_T0(tt);
@@ -397,7 +475,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
         }
         RT_ACC(work, 2, tt);
       }
-    } else if (!kCull) {
+    } else {
       for (int base = 0; base < n; base += 64) {
         unsigned long long mask = candidates<false>(g, rad, n, base, Bound{});
         work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
@@ -410,16 +488,17 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
         }
       }
     }
-    if (use_bvh && gact) {
-      RT_T0(tv);
-      // a box whose entry is beyond the best t (by the margin) holds no closer root
-      bvh_walk(bv, o, d, [&] { return bt + 2e-6 * (bv.diam + __builtin_fabs(bt)); }, work, [&](int i) {
-        work.exact += 1;
-        test(i);
-        return true;
-      });
-      RT_ACC(work, 6, tv);
-    }
+  }
+  if (have_bvh && need) {
+    RT_T0(tv);
+    // a box whose entry is beyond the best t (by the margin) holds no closer root;
+    // spheres a group pass already tested are harmless to test again
+    bvh_walk(bv, o, d, [&] { return bt + 2e-6 * (bv.diam + __builtin_fabs(bt)); }, work, [&](int i) {
+      work.exact += 1;
+      test(i);
+      return true;
+    });
+    RT_ACC(work, 6, tv);
   }
   best_t = bt;
   return bi;
@@ -461,56 +540,61 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
       occ = intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist;
     }
   };
+  const bool have_bvh = kCull && bv.nnodes > 0;
+  bool need = false;
+  int groups = 0;
   while (todo) {
+    if (have_bvh && (bv.always || groups >= bv.max_groups)) {
+      need = need || ((todo >> lane) & 1ull);
+      break;
+    }
     const unsigned long long grp = kCull ? next_group(todo, key) : todo;
     todo &= ~grp;
+    ++groups;
     const bool gact = (grp >> lane) & 1ull;
     unsigned long long live = grp;
-    bool use_bvh = kCull && bv.always;
-    if (!use_bvh) {
-      Bound B;
-      RT_T0(tb);
-      if (kCull) B = make_bound(gact, o, d, P);
-      RT_ACC(work, 0, tb);
-      RT_CNT(work, sweeps, 1);
-      int seen = 0;
-      for (int base = 0; base < n && live; base += 64) {
-        RT_T0(tc);
-        unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
-        RT_ACC(work, 1, tc);
-        if (kCull) {
-          work.cull += (unsigned)(n - base < 64 ? n - base : 64);
-          seen += __popcll(mask);
-          if (bv.nnodes > 0 && seen > bv.min_cands) {
-            use_bvh = true;
-            break;
-          }
+    Bound B;
+    RT_T0(tb);
+    if (kCull) B = make_bound(gact, o, d, P);
+    RT_ACC(work, 0, tb);
+    RT_CNT(work, sweeps, 1);
+    int seen = 0;
+    for (int base = 0; base < n && live; base += 64) {
+      RT_T0(tc);
+      unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
+      RT_ACC(work, 1, tc);
+      if (kCull) {
+        work.cull += (unsigned)(n - base < 64 ? n - base : 64);
+        seen += __popcll(mask);
+        if (have_bvh && seen > bv.min_cands) {
+          need = need || (gact && !occ);
+          break;
         }
-        RT_T0(tt);
-        while (mask) {
-          const int i = base + __builtin_ctzll(mask);
-          mask &= mask - 1;
-          work.exact += (unsigned)__popcll(live);
-          RT_CNT(work, iters, 1);
-          if (gact && !occ) test(i);
-          live = __ballot(gact && !occ);
-          if (live == 0) break;
-        }
-        RT_ACC(work, 2, tt);
       }
+      RT_T0(tt);
+      while (mask) {
+        const int i = base + __builtin_ctzll(mask);
+        mask &= mask - 1;
+        work.exact += (unsigned)__popcll(live);
+        RT_CNT(work, iters, 1);
+        if (gact && !occ) test(i);
+        live = __ballot(gact && !occ);
+        if (live == 0) break;
+      }
+      RT_ACC(work, 2, tt);
     }
-    if (use_bvh && gact && !occ) {
-      RT_T0(tv);
-      // boxes entirely beyond T (by the margin) cannot occlude; boxes behind the
-      // origin are still visited (negative tangent roots count, sphere.h:43-47)
-      const double tmax = T + 2e-6 * (bv.diam + T);
-      bvh_walk(bv, o, d, [&] { return tmax; }, work, [&](int i) {
-        work.exact += 1;
-        test(i);
-        return !occ;
-      });
-      RT_ACC(work, 6, tv);
-    }
+  }
+  if (have_bvh && need && !occ) {
+    RT_T0(tv);
+    // boxes entirely beyond T (by the margin) cannot occlude; boxes behind the
+    // origin are still visited (negative tangent roots count, sphere.h:43-47)
+    const double tmax = T + 2e-6 * (bv.diam + T);
+    bvh_walk(bv, o, d, [&] { return tmax; }, work, [&](int i) {
+      work.exact += 1;
+      test(i);
+      return !occ;
+    });
+    RT_ACC(work, 6, tv);
   }
   return act && occ;
 }

@@ -39,7 +39,7 @@ namespace rtk {
 // Diagnostic timeline: per wave {start, end} (s_memrealtime, 100 MHz) and
 // {HW_ID, XCC_ID}; dumped by rt_render_stats when RT_HIP_STAMPS_FILE is set.
 constexpr int kTimelineWaves = 1 << 17;
-constexpr int kTl = 10;  // u64 per wave
+constexpr int kTl = 12;  // u64 per wave
 __device__ unsigned long long g_timeline[kTimelineWaves * kTl];
 #endif
 
@@ -52,27 +52,18 @@ template <int MAXS, bool kLdsGeo, bool kCull, int kWaves, bool kLdsStack = (MAXS
 __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kernel(const SphGeo *__restrict__ geo, const double *__restrict__ radius,
                                                         const SphMat *__restrict__ mat,
                                                         const LightD *__restrict__ lights, int n, int nl, D3 amb,
-                                                        Cam cam, int W, int H, int depth, Rows rows, BvhArgs bv,
+                                                        Cam cam, int W, int H, int depth, Rows rows, BvhArgs bv_in,
                                                         uint8_t *__restrict__ out,
                                                         unsigned long long *__restrict__ counters) {
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
-  SphGeo *sgeo = reinterpret_cast<SphGeo *>(smem);
-  double *srad = reinterpret_cast<double *>(smem + (kLdsGeo ? (size_t)n * sizeof(SphGeo) : 0));
-  LightD *slight = reinterpret_cast<LightD *>(smem + (kLdsGeo ? (size_t)n * (sizeof(SphGeo) + sizeof(double)) : 0));
-  // per-wave reflection stack after the scene, 32-B aligned
-  const size_t stack_off = ((kLdsGeo ? (size_t)n * (sizeof(SphGeo) + sizeof(double)) : 0) +
-                            (size_t)nl * sizeof(LightD) + 31) & ~(size_t)31;
   const int tid = threadIdx.x;
-  constexpr int kThreads = 64 * kWaves;
-  if (kLdsGeo)
-    for (int i = tid; i < n; i += kThreads) {
-      sgeo[i] = geo[i];
-      srad[i] = radius[i];
-    }
-  for (int i = tid; i < nl; i += kThreads) slight[i] = lights[i];
-  __syncthreads();
-  const SphGeo *g = kLdsGeo ? sgeo : geo;
-  const double *rad = kLdsGeo ? srad : radius;
+  const SphGeo *g;
+  const double *rad;
+  const LightD *slight;
+  BvhArgs bv = bv_in;
+  stage_scene<kLdsGeo>(smem, geo, radius, lights, n, nl, bv, g, rad, slight);
+  // per-wave reflection stack after the staged scene, 32-B aligned
+  const size_t stack_off = (lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31;
 
   // Workgroup = kWaves waves, each an 8x8 pixel tile (2x2 waves for kWaves = 4).
   constexpr int kWx = kWaves == 4 ? 2 : 1;
@@ -234,6 +225,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
                            sn = wave_sum(c_neg);
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
+  const unsigned long long bvh_steps_max = (unsigned long long)wmax((double)work.st[7]);
   if (lane == 0) {
     const unsigned wid = (blockIdx.x + blockIdx.y * gridDim.x) * kWaves + wave;
     if (wid < (unsigned)kTimelineWaves) {
@@ -249,8 +241,9 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
       tl[6] = work.st[4];  // shading
       tl[7] = work.st[5];  // total
       tl[8] = work.iters | (work.sweeps << 32);
-      tl[4] = work.st[6];  // (timeline) bvh cycles in place of cull
-      tl[9] = (unsigned long long)__popcll(__ballot(in_img)) | ((unsigned long long)depth << 32);
+      tl[10] = work.st[6];  // bvh walks
+      tl[11] = work.st[3];  // per-light setup
+      tl[9] = bvh_steps_max;  // most BVH node visits of one lane
     }
   }
 #endif
@@ -307,8 +300,8 @@ struct rt_ctx {
   double c0[3] = {0, 0, 0};
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
   double rmax = 0;
-  int bvh_min = 24, bvh_always = 0, bvh_on = 1;
-  int wg_waves = 1;  // megakernel waves per workgroup (tuning knob RT_HIP_WG_WAVES = 1 | 4)
+  int bvh_min = 24, bvh_always = 0, bvh_on = 1, bvh_groups = 2;
+  int wg_waves = 4;  // megakernel waves per workgroup (tuning knob RT_HIP_WG_WAVES = 1 | 4)
   int pipeline = 0;  // 0 = megakernel (default), 1 = wavefront queues (knob RT_HIP_PIPELINE)
   int n_cu = 256;
   // wavefront scratch: queues, per-pixel terminal colours / stack (grown on demand)
@@ -382,6 +375,7 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   if (!std::isfinite(b.diam)) b.diam = INFINITY;
   b.min_cands = c->bvh_min;
   b.always = c->bvh_always;
+  b.max_groups = c->bvh_groups;
   return b;
 }
 
@@ -467,11 +461,17 @@ int launch_wavefront2(rt_ctx *c, WfArgs &a, size_t lds) {
   const size_t want = (npx + 255) / 256, resident = (size_t)c->n_cu * blocks_per_cu;
   const size_t per_shard = std::max<size_t>(1, (std::min(want, resident) + kShards - 1) / kShards);
   const unsigned persist = (unsigned)(per_shard * kShards);
-  hipLaunchKernelGGL((wf_primary<kLds, kCull>), dim3((W + 15) / 16, (a.rows.count + 15) / 16), dim3(256), lds,
-                     c->stream, a);
+  if (c->pipeline == 2) {  // hybrid: fused coherent level 0, queues from level 1 on
+    hipLaunchKernelGGL((wf_level0<kLds, kCull>), dim3((W + 7) / 8, (a.rows.count + 7) / 8), dim3(64), lds,
+                       c->stream, a);
+  } else {
+    hipLaunchKernelGGL((wf_primary<kLds, kCull>), dim3((W + 15) / 16, (a.rows.count + 15) / 16), dim3(256), lds,
+                       c->stream, a);
+  }
   for (int level = 0; level < a.depth; ++level) {
     if (level > 0) hipLaunchKernelGGL((wf_reflect<kLds, kCull>), dim3(persist), dim3(256), lds, c->stream, a, level);
-    hipLaunchKernelGGL((wf_shade<kLds, kCull>), dim3(persist), dim3(256), lds, c->stream, a, level);
+    if (level > 0 || c->pipeline != 2)
+      hipLaunchKernelGGL((wf_shade<kLds, kCull>), dim3(persist), dim3(256), lds, c->stream, a, level);
   }
   hipLaunchKernelGGL(wf_resolve, dim3((W + 63) / 64, (a.rows.count + 3) / 4), dim3(256), 0, c->stream, a);
   return RT_OK;
@@ -496,8 +496,11 @@ int launch_wavefront(rt_ctx *c, const Cam &cam, int W, int H, int depth, const R
   a.out = dst;
   a.counters = c->d_counters;
   a.bv = bvh_args(c, cam);
-  const size_t wgs = (size_t)((W + 15) / 16) * (size_t)((r.count + 15) / 16);
-  const size_t seg_cap = (wgs + kShards - 1) / kShards * 256;
+  // queue segment capacity: a segment receives at most one entry per pixel of
+  // the workgroups mapped to it (16x16 workgroups of wf_primary, 8x8 of wf_level0)
+  const size_t wgs16 = (size_t)((W + 15) / 16) * (size_t)((r.count + 15) / 16);
+  const size_t wgs8 = (size_t)((W + 7) / 8) * (size_t)((r.count + 7) / 8);
+  const size_t seg_cap = std::max((wgs16 + kShards - 1) / kShards * 256, (wgs8 + kShards - 1) / kShards * 64);
   int rc = ensure_wf(c, (size_t)a.npx, depth, seg_cap, a);
   if (rc != RT_OK) return rc;
   if (lds_geo) return c->cull ? launch_wavefront2<true, true>(c, a, lds) : launch_wavefront2<true, false>(c, a, lds);
@@ -524,15 +527,15 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
     Cam cam{cm->position[0], cm->position[1], cm->position[2], cm->forward[0], cm->forward[1], cm->forward[2],
             cm->right[0],    cm->right[1],    cm->right[2],    cm->up[0],      cm->up[1],      cm->up[2],
             cm->scale};
-    size_t geo_bytes = (size_t)c->nsph * (sizeof(SphGeo) + sizeof(double)),
-           light_bytes = (size_t)c->nlight * sizeof(LightD);
-    bool lds_geo = geo_bytes + light_bytes <= kLdsBudget;
-    size_t lds = (lds_geo ? geo_bytes : 0) + light_bytes;
+    // the scene and its BVH are staged in LDS when they fit (lds_layout)
+    const int nn = (c->bvh_on && c->cull) ? c->bvh_nodes : 0;
+    const bool lds_geo = lds_layout(true, c->nsph, c->nlight, nn).end <= kLdsBudget;
+    const size_t lds = lds_layout(lds_geo, c->nsph, c->nlight, nn).end;
     if (lds > kLdsBudget) {
       c->err = "light list does not fit in LDS";
       return RT_ERR_INVALID_ARG;
     }
-    if (c->pipeline == 1) {
+    if (c->pipeline >= 1) {
       if ((long long)r.count * W > (1LL << 31) - 1) return RT_ERR_INVALID_ARG;
       int rc = launch_wavefront(c, cam, W, H, depth, r, dst, lds_geo, lds);
       if (rc != RT_OK) return rc;
@@ -572,10 +575,11 @@ int rt_create(int device, rt_ctx **out) {
   rt_ctx *c = new rt_ctx();
   c->device = device;
   if (const char *e = std::getenv("RT_HIP_WG_WAVES")) c->wg_waves = std::atoi(e) == 4 ? 4 : 1;
-  if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::atoi(e) == 1 ? 1 : 0;
+  if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_BVH")) c->bvh_on = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_MIN")) c->bvh_min = std::atoi(e);
   if (const char *e = std::getenv("RT_HIP_BVH_ALWAYS")) c->bvh_always = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_BVH_GROUPS")) c->bvh_groups = std::max(1, std::atoi(e));
   auto bail = [&](int rc) {
     rt_destroy(c);
     return rc;

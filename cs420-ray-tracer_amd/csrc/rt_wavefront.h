@@ -87,20 +87,9 @@ struct WfArgs {
 // Stage sphere geometry/radii (if they fit) and lights into LDS.
 template <bool kLdsGeo>
 __device__ __forceinline__ void stage(const WfArgs &a, unsigned char *smem, const SphGeo *&g, const double *&rad,
-                                      const LightD *&lights) {
-  SphGeo *sgeo = reinterpret_cast<SphGeo *>(smem);
-  double *srad = reinterpret_cast<double *>(smem + (kLdsGeo ? (size_t)a.n * sizeof(SphGeo) : 0));
-  LightD *slight = reinterpret_cast<LightD *>(smem + (kLdsGeo ? (size_t)a.n * (sizeof(SphGeo) + sizeof(double)) : 0));
-  if (kLdsGeo)
-    for (int i = threadIdx.x; i < a.n; i += blockDim.x) {
-      sgeo[i] = a.geo[i];
-      srad[i] = a.rad[i];
-    }
-  for (int i = threadIdx.x; i < a.nl; i += blockDim.x) slight[i] = a.lights[i];
-  __syncthreads();
-  g = kLdsGeo ? sgeo : a.geo;
-  rad = kLdsGeo ? srad : a.rad;
-  lights = slight;
+                                      const LightD *&lights, BvhArgs &bv) {
+  bv = a.bv;
+  stage_scene<kLdsGeo>(smem, a.geo, a.rad, a.lights, a.n, a.nl, bv, g, rad, lights);
 }
 
 __device__ __forceinline__ void flush_work(const Work &w, unsigned long long *counters) {
@@ -123,7 +112,8 @@ __global__ __launch_bounds__(256) void wf_primary(WfArgs a) {
   const SphGeo *g;
   const double *rad;
   const LightD *lights;
-  stage<kLdsGeo>(a, smem, g, rad, lights);
+  BvhArgs bv;
+  stage<kLdsGeo>(a, smem, g, rad, lights, bv);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
   const int k = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
@@ -142,7 +132,7 @@ __global__ __launch_bounds__(256) void wf_primary(WfArgs a) {
   const bool alive = in_img && a.depth >= 1;
   Work work;
   double bt;
-  const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, -1, a.bv, bt, work);
+  const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, -1, bv, bt, work);
   const bool hit = alive && bi >= 0;
   if (in_img && !hit) {
     const D3 c = alive ? sky(d) : mk(0.0, 0.0, 0.0);  // depth <= 0 is black (main.cpp:17-18)
@@ -168,6 +158,121 @@ __global__ __launch_bounds__(256) void wf_primary(WfArgs a) {
   flush_work(work, a.counters);
 }
 
+// ---- hybrid pass 0: camera rays + their whole first level, per 8x8 tile -----
+// The coherent part of the frame stays in one kernel (one wave per 8x8 tile,
+// like the megakernel); reflection rays leave through the level-1 queue, so
+// the incoherent levels are spread over many waves by wf_reflect / wf_shade.
+template <bool kLdsGeo, bool kCull>
+__global__ __launch_bounds__(64) void wf_level0(WfArgs a) {
+  extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
+  const SphGeo *g;
+  const double *rad;
+  const LightD *lights;
+  BvhArgs bv;
+  stage<kLdsGeo>(a, smem, g, rad, lights, bv);
+  const int lane = threadIdx.x & 63;
+  const int x = blockIdx.x * 8 + (lane & 7);
+  const int k = blockIdx.y * 8 + (lane >> 3);
+  const long long y = (long long)(k / a.rows.band) * a.rows.band * a.rows.stride +
+                      (long long)a.rows.first * a.rows.band + (k % a.rows.band);
+  const bool in_img = x < a.W && k < a.rows.count && y < a.H;
+  const int pix = k * a.W + x;
+  const int j = a.H - 1 - (int)(in_img ? y : 0);  // camera.h:17-25, main.cpp:151-154
+  const double u = (double)x / (a.W - 1), v = (double)j / (a.H - 1);
+  const double su = ((u - 0.5) * a.cam.scale) * 1.0, sv = (v - 0.5) * a.cam.scale;
+  const D3 dir = add(add(mk(a.cam.fx, a.cam.fy, a.cam.fz), scale(mk(a.cam.rx, a.cam.ry, a.cam.rz), su)),
+                     scale(mk(a.cam.ux, a.cam.uy, a.cam.uz), sv));
+  const D3 d = normalized(normalized(dir));
+  const D3 o = mk(a.cam.px, a.cam.py, a.cam.pz);
+  const bool alive = in_img && a.depth >= 1;
+  Work work;
+  double bt;
+  const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, -1, bv, bt, work);
+  const bool hit = alive && bi >= 0;
+  if (in_img && !hit) {
+    const D3 c = alive ? sky(d) : mk(0.0, 0.0, 0.0);  // depth <= 0 is black (main.cpp:17-18)
+    a.term[pix] = Term{c.x, c.y, c.z};
+    a.nlev[pix] = 0;
+  }
+  const int hi = hit ? bi : 0;
+  const D3 hp = add(o, scale(d, bt));  // main.cpp:32
+  D3 col;
+  {
+    const SphMat m0 = a.mat[hi];
+    col = mul(a.amb, mk(m0.cr, m0.cg, m0.cb));  // scene.h:91
+  }
+  // scene.h:94-120 in two phases per block of 64 lights (see render_kernel)
+  for (int l0 = 0; l0 < a.nl; l0 += 64) {
+    const int lend = a.nl - l0 < 64 ? a.nl : l0 + 64;
+    unsigned long long occm = 0;
+    for (int l = l0; l < lend; ++l) {
+      const LightD L = lights[l];
+      const D3 lp = mk(L.px, L.py, L.pz);
+      const D3 to_light = sub(lp, hp);
+      const double dist = length(to_light);
+      const D3 ldir = normalized(to_light);
+      const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
+      if (sweep_shadow<kCull>(g, rad, a.n, hit, so, sd, lp, hi, dist, bv, work)) occm |= 1ull << (l - l0);
+    }
+    if (hit && occm != ~0ull >> (64 - (lend - l0))) {
+      const SphGeo sg = g[hi];
+      const SphMat m = a.mat[hi];
+      const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
+      const D3 view = normalized(sub(o, hp));                       // main.cpp:38
+      const D3 mc = mk(m.cr, m.cg, m.cb);
+      for (int l = l0; l < lend; ++l) {
+        if (occm >> (l - l0) & 1ull) continue;
+        const LightD L = lights[l];
+        const D3 ldir = normalized(sub(mk(L.px, L.py, L.pz), hp));
+        const double ndl = max0(dot(nrm, ldir));
+        const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
+        const D3 nl2 = scale(ldir, -1.0);
+        const D3 rdir = sub(nl2, scale(scale(nrm, 2.0), dot(nl2, nrm)));  // reflect(), vec3.h:31-33
+        const double rdv = max0(dot(rdir, view));
+        const double spec = (rdv == 0.0 && m.shin > 0.0) ? 0.0 : pow_call(rdv, m.shin);
+        const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
+        col = add(add(specular, diffuse), col);  // scene.h:117
+      }
+    }
+  }
+  bool spawn = false;
+  D3 ro = mk(0.0, 0.0, 0.0), rd = ro;
+  if (hit) {
+    const SphMat m = a.mat[hi];
+    if (m.refl > 0.0) {  // main.cpp:43-55
+      const double w = 1.0 - m.refl;
+      const D3 A = mk(col.x * w, col.y * w, col.z * w);
+      if (a.depth - 1 >= 1) {
+        a.stack[pix] = StackEnt{A.x, A.y, A.z, m.refl};  // level 0
+        const SphGeo sg = g[hi];
+        const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));
+        rd = normalized(sub(d, scale(scale(nrm, 2.0), dot(d, nrm))));
+        ro = add(hp, scale(nrm, kEps));
+        spawn = true;
+      } else {
+        a.term[pix] = Term{A.x, A.y, A.z};
+        a.nlev[pix] = 0;
+      }
+    } else {
+      a.term[pix] = Term{col.x, col.y, col.z};
+      a.nlev[pix] = 0;
+    }
+  }
+  const unsigned shard = (blockIdx.x + blockIdx.y * gridDim.x) % kShards;
+  const unsigned slot = wave_append(spawn, &a.ray_cnt[1 * kShards + shard]);
+  if (spawn) a.rayq[(size_t)shard * a.seg_cap + slot] = RayRec{ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, pix, a.depth - 1, hi, 0};
+  const unsigned np = (unsigned)__popcll(__ballot(alive));
+  const unsigned nh = (unsigned)__popcll(__ballot(hit));
+  const unsigned ns = (unsigned)__popcll(__ballot(spawn));
+  if (lane == 0) {
+    unsigned long long *sc = counter_shard(a.counters);
+    if (np) atomicAdd(&sc[0], (unsigned long long)np);
+    if (nh) atomicAdd(&sc[1], (unsigned long long)nh * (unsigned)a.nl);
+    if (ns) atomicAdd(&sc[2], (unsigned long long)ns);
+  }
+  flush_work(work, a.counters);
+}
+
 // ---- pass 2 (per level): shading + shadow rays, spawns reflection rays -------
 template <bool kLdsGeo, bool kCull>
 __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
@@ -179,7 +284,8 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
   const SphGeo *g;
   const double *rad;
   const LightD *lights;
-  stage<kLdsGeo>(a, smem, g, rad, lights);
+  BvhArgs bv;
+  stage<kLdsGeo>(a, smem, g, rad, lights, bv);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   Work work;
   unsigned long long n_shadow = 0, n_reflect = 0;
@@ -261,7 +367,8 @@ __global__ __launch_bounds__(256) void wf_reflect(WfArgs a, int level) {
   const SphGeo *g;
   const double *rad;
   const LightD *lights;
-  stage<kLdsGeo>(a, smem, g, rad, lights);
+  BvhArgs bv;
+  stage<kLdsGeo>(a, smem, g, rad, lights, bv);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   Work work;
   const unsigned stride = nj * 256u;
@@ -271,7 +378,7 @@ __global__ __launch_bounds__(256) void wf_reflect(WfArgs a, int level) {
     const RayRec r = rq[alive ? idx : base];
     const D3 o = mk(r.ox, r.oy, r.oz), d = mk(r.dx, r.dy, r.dz);
     double bt;
-    const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, r.key, a.bv, bt, work);
+    const int bi = sweep_closest<kCull>(g, rad, a.n, alive, o, d, r.key, bv, bt, work);
     const bool hit = alive && bi >= 0;
     if (alive && !hit) {
       const D3 c = sky(d);

@@ -7,7 +7,7 @@ import sys
 
 if len(sys.argv) > 2 and sys.argv[1] == "--analyse":
     import numpy as np
-    a = np.fromfile(sys.argv[2], dtype=np.uint64).reshape(-1, 10)
+    a = np.fromfile(sys.argv[2], dtype=np.uint64).reshape(-1, 12)
     n = int(sys.argv[3]) if len(sys.argv) > 3 else (a[:, 1] > 0).sum()
     a = a[:n]
     t0 = a[:, 0].min()
@@ -29,13 +29,13 @@ if len(sys.argv) > 2 and sys.argv[1] == "--analyse":
     per_row = [d[rows == r].mean() for r in range(rows.max() + 1)]
     print("  mean wave duration per tile row (us):", " ".join(f"{x:.0f}" for x in per_row))
     order = np.argsort(-d)[:12]
-    print("  slowest waves: id(tile x,y) dur_us | cycles: bound cull cand shade total | iters sweeps")
+    print("  slowest waves: id(tile x,y) dur_us | cycles: bound cull cand shade bvh total | iters sweeps")
     for w in order:
         it, sw = int(a[w, 8]) & 0xFFFFFFFF, int(a[w, 8]) >> 32
-        print(f"   {w:6d} ({w % W_tiles:3d},{w // W_tiles:3d}) {d[w]:7.1f} | {a[w,3]:8d} {a[w,4]:8d} {a[w,5]:9d} {a[w,6]:8d} {a[w,7]:9d} | {it:5d} {sw:4d}")
+        print(f"   {w:6d} ({w % W_tiles:3d},{w // W_tiles:3d}) {d[w]:7.1f} bvhmax {a[w,9]:5d} | {a[w,3]:8d} {a[w,4]:8d} {a[w,5]:9d} {a[w,6]:8d} {a[w,10]:8d} {a[w,7]:9d} | {it:5d} {sw:4d}")
     med = np.argsort(d)[len(d)//2]
     w = med
-    print(f"  median wave {w}: {d[w]:.1f} us | {a[w,3]} {a[w,4]} {a[w,5]} {a[w,6]} {a[w,7]} | {int(a[w,8]) & 0xFFFFFFFF} {int(a[w,8]) >> 32}")
+    print(f"  median wave {w}: {d[w]:.1f} us | {a[w,3]} {a[w,4]} {a[w,5]} {a[w,6]} {a[w,10]} {a[w,7]} | {int(a[w,8]) & 0xFFFFFFFF} {int(a[w,8]) >> 32}")
     sys.exit(0)
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -324,3 +324,74 @@ def test_bvh_far_from_origin(bvh_renderer):
     ref, _, _ = orc.OracleScene(text=text).render(80, 60, 6, threads=4)
     rgb, _ = bvh_renderer.render(sc.camera(), 80, 60, 6)
     assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
+
+
+@pytest.fixture(params=["1", "2"], ids=["queues", "hybrid"])
+def pipeline_renderer(request, monkeypatch):
+    """The queue-based pipelines (RT_HIP_PIPELINE=1: every level through the
+    ray/hit queues; 2: fused coherent level 0, queues from level 1 on)."""
+    import rt_hip
+
+    monkeypatch.setenv("RT_HIP_PIPELINE", request.param)
+    r = rt_hip.Renderer(0)
+    yield r
+    r.close()
+
+
+@pytest.mark.parametrize("name", ["complex_97x61_d4", "medium_1280x720_d10", "synth200_1920x1080_d4",
+                                  "synth10k_384x216_d6", "simple_2x2_d10", "simple_1x1_d10"])
+def test_pipelines_golden(pipeline_renderer, name):
+    for cull in (True, False):
+        pipeline_renderer.set_culling(cull)
+        rgb, st, m = _render(pipeline_renderer, name)
+        assert rgb == golden_rgb(name), (cull, diff_summary(rgb, golden_rgb(name)))
+        assert {"primary": st.rays_primary, "shadow": st.rays_shadow, "reflect": st.rays_reflect} == m["rays"]
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2, 5, 64])
+def test_pipelines_depth_edges(pipeline_renderer, depth):
+    import orc
+    import rt_hip
+
+    W, H = 67, 45
+    sc = rt_hip.Scene.load(scene_path("medium"))
+    pipeline_renderer.upload(sc)
+    rgb, st = pipeline_renderer.render(sc.camera(), W, H, depth)
+    ref, counts, _ = orc.OracleScene(scene_path("medium")).render(W, H, depth, threads=4)
+    assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
+    assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
+                                                                   counts["reflect"])
+
+
+@pytest.mark.parametrize("G,band", [(3, 8), (5, 1)])
+def test_pipelines_row_shards(pipeline_renderer, G, band):
+    import rt_hip
+
+    name = "complex_97x61_d4"
+    m = manifest()[name]
+    W, H = m["width"], m["height"]
+    want = np.frombuffer(golden_rgb(name), np.uint8).reshape(H, W, 3)
+    for r in range(G):
+        rows = rt_hip.rows_for_shard(H, band, r, G)
+        rgb, _, _ = _render(pipeline_renderer, name, rows)
+        got = np.frombuffer(rgb, np.uint8).reshape(rows.count, W, 3)
+        for k in range(rows.count):
+            y = (k // band) * band * G + r * band + k % band
+            if y < H:
+                assert np.array_equal(got[k], want[y]), (r, k, y)
+            else:
+                assert not got[k].any()
+
+
+@pytest.mark.parametrize("seed", range(0, 12, 4))
+def test_pipelines_random_scenes(pipeline_renderer, seed):
+    import orc
+    import rt_hip
+
+    text = _random_scene(seed, 60 + 40 * seed)
+    W, H, D = 96, 64, 5
+    sc = rt_hip.Scene.parse(text)
+    pipeline_renderer.upload(sc)
+    ref, _, _ = orc.OracleScene(text=text).render(W, H, D, threads=4)
+    rgb, _ = pipeline_renderer.render(sc.camera(), W, H, D)
+    assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
