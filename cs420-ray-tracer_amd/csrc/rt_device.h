@@ -8,6 +8,7 @@
 #include <cstdint>
 
 #include "rt_bvh.h"
+#include "rt_lightgrid.h"
 
 #pragma clang fp contract(off)
 
@@ -243,7 +244,7 @@ struct Work {
   unsigned long long exact = 0, cull = 0;
 #ifdef RT_STAMPS
   // Diagnostic build only (-DRT_STAMPS): s_memtime cycles per phase, per wave.
-  unsigned long long st[8] = {};
+  unsigned long long st[12] = {};
   unsigned long long iters = 0, sweeps = 0, it_closest = 0, sw_closest = 0, it_prim = 0;
 #endif
 };
@@ -313,6 +314,9 @@ __device__ __forceinline__ void bvh_walk(const BvhArgs &bv, D3 o, D3 d, T &&tmax
 #endif
     work.cull += 1;
     RT_CNT(work, st[7], 1);
+#ifdef RT_STAMPS
+    if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63)) == (int)(threadIdx.x & 63)) work.st[10] += 1;
+#endif
     if (in && nd.leaf >= 0) {
       const int first = nd.leaf >> 4, cnt = nd.leaf & 15;
       for (int k = 0; k < cnt; ++k)
@@ -489,8 +493,11 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       }
     }
   }
+#ifdef RT_STAMPS
+  const bool any_need = have_bvh && __ballot(need) != 0;
+  RT_T0(tv);
+#endif
   if (have_bvh && need) {
-    RT_T0(tv);
     // a box whose entry is beyond the best t (by the margin) holds no closer root;
     // spheres a group pass already tested are harmless to test again
     bvh_walk(bv, o, d, [&] { return bt + 2e-6 * (bv.diam + __builtin_fabs(bt)); }, work, [&](int i) {
@@ -498,8 +505,10 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       test(i);
       return true;
     });
-    RT_ACC(work, 6, tv);
   }
+#ifdef RT_STAMPS
+  if (any_need) RT_ACC(work, 6, tv);
+#endif
   best_t = bt;
   return bi;
 }
@@ -584,8 +593,11 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
       RT_ACC(work, 2, tt);
     }
   }
+#ifdef RT_STAMPS
+  const bool any_need = have_bvh && __ballot(need && !occ) != 0;
+  RT_T0(tv);
+#endif
   if (have_bvh && need && !occ) {
-    RT_T0(tv);
     // boxes entirely beyond T (by the margin) cannot occlude; boxes behind the
     // origin are still visited (negative tangent roots count, sphere.h:43-47)
     const double tmax = T + 2e-6 * (bv.diam + T);
@@ -594,7 +606,78 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
       test(i);
       return !occ;
     });
-    RT_ACC(work, 6, tv);
+  }
+#ifdef RT_STAMPS
+  if (any_need) RT_ACC(work, 6, tv);
+#endif
+  return act && occ;
+}
+
+// Shadow query through the light's direction grid (rt_lightgrid.h): each lane
+// tests the global list and the list of the cell its direction -d (from the
+// light towards the shaded point) falls in, with the same exact test and early
+// exit as sweep_shadow.  A lane whose direction cannot be binned (degenerate or
+// non-finite) or whose line misses the light by more than max_off tests every
+// sphere.
+struct LgArgs {
+  const int32_t *start;
+  const int32_t *ids;
+  int N;
+  int on;          // 0: shadow rays use sweep_shadow
+  double max_off;  // largest distance of a ray's line from its light the grid margins cover
+};
+
+__device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d, D3 lp,
+                                             double dist, const LgArgs &lg, int l, Work &work) {
+  if (__ballot(act) == 0) return false;
+  const double a = dot(d, d);
+  const double a4 = 4.0 * a, a2 = 2.0 * a;
+  const double T = dist < kInf ? dist : kInf;
+  const bool fast = a2_ok(a2) && dist == dist && T >= 0x1p-900;
+  const double q = a2 * T, qlo = q * (1.0 - 0x1p-48), qhi = q * (1.0 + 0x1p-48);
+  bool occ = false;
+  auto test = [&](int i) {
+    double num;
+    const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+    if (r == 1) {
+      if (num < qlo) occ = true;
+      else if (!(num > qhi)) {
+        const double t = num / a2;
+        occ = t < kInf && t < dist;
+      }
+    } else if (r == 2) {
+      double t;
+      occ = intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist;
+    }
+  };
+  if (act) {
+    const int N = lg.N, cells = 6 * N * N;
+    const int32_t *st = lg.start + (size_t)l * (size_t)(cells + 2);
+    // The line o + t d passes (up to rounding) through the light; the grid's
+    // margins assume it does within max_off -- checked here, per ray.
+    const D3 w = sub(lp, o);
+    const double off = __builtin_fabs(w.y * d.z - w.z * d.y) + __builtin_fabs(w.z * d.x - w.x * d.z) +
+                       __builtin_fabs(w.x * d.y - w.y * d.x);
+    const int c = (off <= lg.max_off) ? lg_cell((float)-d.x, (float)-d.y, (float)-d.z, N) : -1;
+    if (c < 0) {
+      for (int i = 0; i < n && !occ; ++i) {
+        work.exact += 1;
+        test(i);
+      }
+    } else {
+      // global list, then the cell's list; the next id is loaded ahead
+      const int gb = st[cells], ge = st[cells + 1], cb = st[c], ce = st[c + 1];
+      const int len0 = ge - gb, len = len0 + (ce - cb);
+      int k = 0;
+      int nxt = len > 0 ? lg.ids[len0 > 0 ? gb : cb] : 0;
+      while (k < len && !occ) {
+        const int i = nxt;
+        ++k;
+        if (k < len) nxt = lg.ids[k < len0 ? gb + k : cb + (k - len0)];
+        work.exact += 1;
+        test(i);
+      }
+    }
   }
   return act && occ;
 }

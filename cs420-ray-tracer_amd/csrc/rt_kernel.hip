@@ -39,7 +39,7 @@ namespace rtk {
 // Diagnostic timeline: per wave {start, end} (s_memrealtime, 100 MHz) and
 // {HW_ID, XCC_ID}; dumped by rt_render_stats when RT_HIP_STAMPS_FILE is set.
 constexpr int kTimelineWaves = 1 << 17;
-constexpr int kTl = 12;  // u64 per wave
+constexpr int kTl = 16;  // u64 per wave
 __device__ unsigned long long g_timeline[kTimelineWaves * kTl];
 #endif
 
@@ -52,7 +52,7 @@ template <int MAXS, bool kLdsGeo, bool kCull, int kWaves, bool kLdsStack = (MAXS
 __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kernel(const SphGeo *__restrict__ geo, const double *__restrict__ radius,
                                                         const SphMat *__restrict__ mat,
                                                         const LightD *__restrict__ lights, int n, int nl, D3 amb,
-                                                        Cam cam, int W, int H, int depth, Rows rows, BvhArgs bv_in,
+                                                        Cam cam, int W, int H, int depth, Rows rows, BvhArgs bv_in, LgArgs lg,
                                                         uint8_t *__restrict__ out,
                                                         unsigned long long *__restrict__ counters) {
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
@@ -106,7 +106,9 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
 #ifdef RT_STAMPS
     const unsigned long long it_before = work.it_closest;
 #endif
+    RT_T0(t_cl);
     const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, key, bv, bt, work);
+    RT_ACC(work, 8, t_cl);
 #ifdef RT_STAMPS
     if (dleft == depth) work.it_prim += work.it_closest - it_before;
 #endif
@@ -139,7 +141,11 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
         const D3 ldir = normalized(to_light);
         const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
         RT_ACC(work, 3, t_setup);
-        if (sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, hi, dist, bv, work)) occm |= 1ull << (l - l0);
+        RT_T0(t_sh);
+        const bool occ = lg.on ? shadow_cells(g, n, hit, so, sd, lp, dist, lg, l, work)
+                               : sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, hi, dist, bv, work);
+        if (occ) occm |= 1ull << (l - l0);
+        RT_ACC(work, 9, t_sh);
       }
       RT_T0(t_shade);
       if (hit && occm != ~0ull >> (64 - (lend - l0))) {
@@ -226,6 +232,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
   const unsigned long long bvh_steps_max = (unsigned long long)wmax((double)work.st[7]);
+  const unsigned long long wave_trips = wave_sum((unsigned)work.st[10]);
   if (lane == 0) {
     const unsigned wid = (blockIdx.x + blockIdx.y * gridDim.x) * kWaves + wave;
     if (wid < (unsigned)kTimelineWaves) {
@@ -243,6 +250,9 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
       tl[8] = work.iters | (work.sweeps << 32);
       tl[10] = work.st[6];  // bvh walks
       tl[11] = work.st[3];  // per-light setup
+      tl[12] = work.st[8];  // closest sweeps
+      tl[13] = work.st[9];  // shadow sweeps
+      tl[14] = wave_trips;  // bvh loop trips of the wave
       tl[9] = bvh_steps_max;  // most BVH node visits of one lane
     }
   }
@@ -297,6 +307,10 @@ struct rt_ctx {
   BvhNode *d_bvh = nullptr;
   int32_t *d_prims = nullptr;
   int bvh_nodes = 0;
+  // per-light direction grids for shadow rays (rt_lightgrid.h), built at upload
+  int32_t *d_lg_start = nullptr, *d_lg_ids = nullptr;
+  int lg_n = 64, lg_on = 1;
+  double lg_max_off = 0.0;
   double c0[3] = {0, 0, 0};
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
   double rmax = 0;
@@ -343,6 +357,9 @@ void free_scene(rt_ctx *c) {
   if (c->d_lights) (void)hipFree(c->d_lights);
   if (c->d_bvh) (void)hipFree(c->d_bvh);
   if (c->d_prims) (void)hipFree(c->d_prims);
+  if (c->d_lg_start) (void)hipFree(c->d_lg_start);
+  if (c->d_lg_ids) (void)hipFree(c->d_lg_ids);
+  c->d_lg_start = c->d_lg_ids = nullptr;
   c->d_bvh = nullptr;
   c->d_prims = nullptr;
   c->bvh_nodes = 0;
@@ -379,21 +396,32 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   return b;
 }
 
+LgArgs lg_args(const rt_ctx *c) {
+  LgArgs g;
+  g.start = c->d_lg_start;
+  g.ids = c->d_lg_ids;
+  g.N = c->lg_n;
+  g.on = (c->lg_on && c->cull && c->d_lg_start) ? 1 : 0;
+  g.max_off = c->lg_max_off;
+  return g;
+}
+
 template <int MAXS, bool kCull, int kWaves>
 void launch_render3(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
                     uint8_t *out) {
   const BvhArgs bv = bvh_args(c, cam);
+  const LgArgs lg = lg_args(c);
   constexpr int kWx = kWaves == 4 ? 2 : 1, kWy = kWaves / kWx;
   dim3 grid((W + 8 * kWx - 1) / (8 * kWx), (rows.count + 8 * kWy - 1) / (8 * kWy));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   if (MAXS <= 4) lds = ((lds + 31) & ~(size_t)31) + (size_t)kWaves * 64 * MAXS * sizeof(StackEnt);
   if (lds_geo)
     hipLaunchKernelGGL((render_kernel<MAXS, true, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, out,
+                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, out,
                        c->d_counters);
   else
     hipLaunchKernelGGL((render_kernel<MAXS, false, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, out,
+                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, out,
                        c->d_counters);
 }
 
@@ -496,6 +524,7 @@ int launch_wavefront(rt_ctx *c, const Cam &cam, int W, int H, int depth, const R
   a.out = dst;
   a.counters = c->d_counters;
   a.bv = bvh_args(c, cam);
+  a.lg = lg_args(c);
   // queue segment capacity: a segment receives at most one entry per pixel of
   // the workgroups mapped to it (16x16 workgroups of wf_primary, 8x8 of wf_level0)
   const size_t wgs16 = (size_t)((W + 15) / 16) * (size_t)((r.count + 15) / 16);
@@ -580,6 +609,8 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH_MIN")) c->bvh_min = std::atoi(e);
   if (const char *e = std::getenv("RT_HIP_BVH_ALWAYS")) c->bvh_always = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_GROUPS")) c->bvh_groups = std::max(1, std::atoi(e));
+  if (const char *e = std::getenv("RT_HIP_SHADOW_GRID")) c->lg_on = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n = std::max(1, std::min(256, std::atoi(e)));
   auto bail = [&](int rc) {
     rt_destroy(c);
     return rc;
@@ -699,6 +730,40 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     return rc;
   }
   c->bvh_nodes = (int)nodes.size();
+  {
+    double d2 = 0.0;
+    for (int k = 0; k < 3; k++) d2 += (hi[k] - lo[k]) * (hi[k] - lo[k]);
+    const double diam = n + nl > 0 ? std::sqrt(d2) : 0.0;
+    std::vector<double> sx(n), sy(n), sz(n), lx(nl), ly(nl), lz(nl);
+    for (int i = 0; i < n; i++) {
+      sx[i] = s->spheres[i].center[0];
+      sy[i] = s->spheres[i].center[1];
+      sz[i] = s->spheres[i].center[2];
+    }
+    for (int i = 0; i < nl; i++) {
+      lx[i] = s->lights[i].position[0];
+      ly[i] = s->lights[i].position[1];
+      lz[i] = s->lights[i].position[2];
+    }
+    std::vector<int32_t> lg_start, lg_ids;
+    build_light_grid(sx.data(), sy.data(), sz.data(), br.data(), n, lx.data(), ly.data(), lz.data(), nl, diam,
+                     c->lg_n, lg_start, lg_ids);
+    c->lg_max_off = std::isfinite(diam) ? 1e-7 * diam : 0.0;
+    if ((e = hipMalloc(&c->d_lg_start, sizeof(int32_t) * (lg_start.size() + 1))) != hipSuccess ||
+        (e = hipMalloc(&c->d_lg_ids, sizeof(int32_t) * (lg_ids.size() + 1))) != hipSuccess ||
+        (!lg_start.empty() && (e = hipMemcpy(c->d_lg_start, lg_start.data(), sizeof(int32_t) * lg_start.size(),
+                                             hipMemcpyHostToDevice)) != hipSuccess) ||
+        (!lg_ids.empty() && (e = hipMemcpy(c->d_lg_ids, lg_ids.data(), sizeof(int32_t) * lg_ids.size(),
+                                           hipMemcpyHostToDevice)) != hipSuccess)) {
+      rc = fail(c, e, "rt_upload_scene(light grid)");
+      free_scene(c);
+      delete[] hg;
+      delete[] hr;
+      delete[] hm;
+      delete[] hl;
+      return rc;
+    }
+  }
   for (int k = 0; k < 3; k++) {
     c->c0[k] = c0[k];
     c->lo[k] = lo[k];

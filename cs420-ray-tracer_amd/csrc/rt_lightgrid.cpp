@@ -1,0 +1,110 @@
+// rt_lightgrid.cpp -- host builder of the per-light direction grids (see rt_lightgrid.h).
+#include "rt_lightgrid.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace rtk {
+namespace {
+
+struct Dir {
+  double x, y, z;
+};
+
+Dir face_dir(int face, double a, double b) {
+  Dir d;
+  switch (face) {
+    case 0: d = {1.0, a, b}; break;
+    case 1: d = {-1.0, a, b}; break;
+    case 2: d = {a, 1.0, b}; break;
+    case 3: d = {a, -1.0, b}; break;
+    case 4: d = {a, b, 1.0}; break;
+    default: d = {a, b, -1.0}; break;
+  }
+  const double l = std::sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
+  return {d.x / l, d.y / l, d.z / l};
+}
+
+double angle(const Dir &u, const Dir &v) {  // robust for small angles
+  const double cx = u.y * v.z - u.z * v.y, cy = u.z * v.x - u.x * v.z, cz = u.x * v.y - u.y * v.x;
+  return std::atan2(std::sqrt(cx * cx + cy * cy + cz * cz), u.x * v.x + u.y * v.y + u.z * v.z);
+}
+
+// A square patch [i0, i1) x [j0, j1) of a face: centre direction and the
+// largest angle from it to the patch (attained at a corner: the patch is
+// geodesically convex and the distance to a point is convex on it).
+struct Patch {
+  Dir c;
+  double rad;
+};
+Patch make_patch(int face, int N, int i0, int i1, int j0, int j1) {
+  const double a0 = -1.0 + 2.0 * i0 / N, a1 = -1.0 + 2.0 * i1 / N;
+  const double b0 = -1.0 + 2.0 * j0 / N, b1 = -1.0 + 2.0 * j1 / N;
+  Patch p;
+  p.c = face_dir(face, 0.5 * (a0 + a1), 0.5 * (b0 + b1));
+  p.rad = std::max(std::max(angle(p.c, face_dir(face, a0, b0)), angle(p.c, face_dir(face, a1, b0))),
+                   std::max(angle(p.c, face_dir(face, a0, b1)), angle(p.c, face_dir(face, a1, b1))));
+  return p;
+}
+
+}  // namespace
+
+void build_light_grid(const double *cx, const double *cy, const double *cz, const double *r, int n,
+                      const double *lx, const double *ly, const double *lz, int nl, double diam, int N,
+                      std::vector<int32_t> &start, std::vector<int32_t> &ids) {
+  const int cells = 6 * N * N;
+  const size_t stride = (size_t)cells + 2;
+  start.assign(stride * (size_t)nl, 0);
+  ids.clear();
+  constexpr int kT = 8;  // patches of kT x kT cells for the coarse pass
+  const int NT = (N + kT - 1) / kT;
+  std::vector<Patch> cellp((size_t)cells), tilep((size_t)6 * NT * NT);
+  for (int f = 0; f < 6; f++)
+    for (int j = 0; j < N; j++)
+      for (int i = 0; i < N; i++) cellp[(size_t)(f * N + j) * N + i] = make_patch(f, N, i, i + 1, j, j + 1);
+  for (int f = 0; f < 6; f++)
+    for (int tj = 0; tj < NT; tj++)
+      for (int ti = 0; ti < NT; ti++)
+        tilep[(size_t)(f * NT + tj) * NT + ti] =
+            make_patch(f, N, ti * kT, std::min(N, ti * kT + kT), tj * kT, std::min(N, tj * kT + kT));
+  const double dm = std::isfinite(diam) ? diam : 0.0;
+  std::vector<std::vector<int32_t>> lists((size_t)cells);
+  std::vector<int32_t> global;
+  for (int l = 0; l < nl; l++) {
+    for (auto &v : lists) v.clear();
+    global.clear();
+    const bool light_ok = std::isfinite(lx[l]) && std::isfinite(ly[l]) && std::isfinite(lz[l]);
+    for (int s = 0; s < n; s++) {
+      const double vx = cx[s] - lx[l], vy = cy[s] - ly[l], vz = cz[s] - lz[l];
+      const double D = std::sqrt(vx * vx + vy * vy + vz * vz);
+      const double R = std::fabs(r[s]) * (1.0 + 1e-6) + 1e-6 * (D + dm);  // >= r + max_off + rounding
+      if (!light_ok || !std::isfinite(D) || !std::isfinite(R) || !(D > R) || !std::isfinite(dm)) {
+        global.push_back(s);  // contains (or nearly) the light, or non-finite: every direction
+        continue;
+      }
+      const Dir v{vx / D, vy / D, vz / D};
+      const double alpha = std::asin(R / D) + kLgSlack;
+      for (int f = 0; f < 6; f++)
+        for (int tj = 0; tj < NT; tj++)
+          for (int ti = 0; ti < NT; ti++) {
+            const Patch &tp = tilep[(size_t)(f * NT + tj) * NT + ti];
+            if (angle(v, tp.c) > alpha + tp.rad + kLgSlack) continue;
+            for (int j = tj * kT; j < std::min(N, tj * kT + kT); j++)
+              for (int i = ti * kT; i < std::min(N, ti * kT + kT); i++) {
+                const size_t c = (size_t)(f * N + j) * N + i;
+                if (angle(v, cellp[c].c) <= alpha + cellp[c].rad + kLgSlack) lists[c].push_back(s);
+              }
+          }
+    }
+    int32_t *st = start.data() + stride * (size_t)l;
+    for (int c = 0; c < cells; c++) {
+      st[c] = (int32_t)ids.size();
+      ids.insert(ids.end(), lists[c].begin(), lists[c].end());
+    }
+    st[cells] = (int32_t)ids.size();
+    ids.insert(ids.end(), global.begin(), global.end());
+    st[cells + 1] = (int32_t)ids.size();
+  }
+}
+
+}  // namespace rtk

@@ -1,0 +1,67 @@
+// rt_lightgrid.h -- per-light direction grids ("light buffers") for shadow rays.
+//
+// Every shadow ray of light L runs (up to rounding) along the line through L
+// and the shaded point p, and only spheres that meet the half-line
+// {L + s*u : s >= 0}, u = (p - L)/|p - L|, can report a root t < |L - p| on
+// it (scene.h:65-86 / sphere.h:26-59; negative tangent roots behind p lie on
+// the same half-line).  Seen from L such a sphere covers a disk of directions
+// around (C - L) of angular radius asin(R/|C - L|), R = radius + margin.
+//
+// Directions from L are binned on a cube map (6 faces x N x N cells).  A cell
+// lists every sphere whose grown disk meets the cell; spheres that contain L
+// (or come within R of it) and spheres with non-finite data are on a "global"
+// list tested for every direction.  A shadow query tests the global list and
+// its cell's list with the reference's exact intersection; the candidate set
+// is a superset of the spheres that can occlude, so the result is the
+// reference's.  Margins: R = |r|(1 + 1e-6) + 1e-6 (|C - L| + scene diameter)
+// covers the line's offset from L and the rounding of the reference's test
+// (same argument as the cull bound in rt_device.h) as long as the line passes
+// within max_off = 1e-7 * diameter of L, which the device checks per ray
+// (falling back to testing every sphere); directions are binned in fp32
+// (angle error < 1e-6 rad) and every disk is grown by kLgSlack = 4e-6 rad.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace rtk {
+
+constexpr double kLgSlack = 4e-6;
+
+// Cell of direction (ux, uy, uz) on an N x N cube map: face 0..5 = +X -X +Y -Y
+// +Z -Z, (a, b) = the two minor coordinates divided by the major one, in
+// [-1, 1].  Returns -1 for a zero or non-finite direction.  Shared by the host
+// builder and the device lookup so both bin identically.
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline int lg_cell(float ux, float uy, float uz, int N) {
+  const float ax = ux < 0 ? -ux : ux, ay = uy < 0 ? -uy : uy, az = uz < 0 ? -uz : uz;
+  int face;
+  float m, p, q;
+  if (ax >= ay && ax >= az) {
+    face = ux >= 0 ? 0 : 1;
+    m = ax, p = uy, q = uz;
+  } else if (ay >= az) {
+    face = uy >= 0 ? 2 : 3;
+    m = ay, p = ux, q = uz;
+  } else {
+    face = uz >= 0 ? 4 : 5;
+    m = az, p = ux, q = uy;
+  }
+  if (!(m > 1e-30f) || !(m <= 3.4e38f) || p != p || q != q) return -1;
+  const float fa = (p / m + 1.0f) * 0.5f * (float)N, fb = (q / m + 1.0f) * 0.5f * (float)N;
+  int i = (int)(fa < 0.f ? 0.f : fa), j = (int)(fb < 0.f ? 0.f : fb);
+  i = i > N - 1 ? N - 1 : i;
+  j = j > N - 1 ? N - 1 : j;
+  return (face * N + j) * N + i;
+}
+
+// Host builder.  For light l the lists are at
+//   cell c (0 <= c < 6N^2): ids[start[l*stride + c] .. start[l*stride + c + 1])
+//   global list:           ids[start[l*stride + 6N^2] .. start[l*stride + 6N^2 + 1])
+// with stride = 6N^2 + 2; ids within a list ascend (sphere order).
+void build_light_grid(const double *cx, const double *cy, const double *cz, const double *r, int n,
+                      const double *lx, const double *ly, const double *lz, int nl, double diam, int N,
+                      std::vector<int32_t> &start, std::vector<int32_t> &ids);
+
+}  // namespace rtk

@@ -82,6 +82,7 @@ struct WfArgs {
   uint8_t *out;
   unsigned long long *counters;
   BvhArgs bv;
+  LgArgs lg;
 };
 
 // Stage sphere geometry/radii (if they fit) and lights into LDS.
@@ -212,7 +213,9 @@ __global__ __launch_bounds__(64) void wf_level0(WfArgs a) {
       const double dist = length(to_light);
       const D3 ldir = normalized(to_light);
       const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
-      if (sweep_shadow<kCull>(g, rad, a.n, hit, so, sd, lp, hi, dist, bv, work)) occm |= 1ull << (l - l0);
+      const bool occ = a.lg.on ? shadow_cells(g, a.n, hit, so, sd, lp, dist, a.lg, l, work)
+                               : sweep_shadow<kCull>(g, rad, a.n, hit, so, sd, lp, hi, dist, bv, work);
+      if (occ) occm |= 1ull << (l - l0);
     }
     if (hit && occm != ~0ull >> (64 - (lend - l0))) {
       const SphGeo sg = g[hi];
@@ -308,9 +311,9 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
       const D3 to_light = sub(lp, hp);
       const double dist = length(to_light);
       const D3 ldir = normalized(to_light);
-      const bool occ =
-          sweep_shadow<kCull>(g, rad, a.n, hit, add(hp, scale(ldir, kEps)), normalized(ldir), lp, h.sph, dist, a.bv,
-                              work);
+      const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
+      const bool occ = a.lg.on ? shadow_cells(g, a.n, hit, so, sd, lp, dist, a.lg, l, work)
+                               : sweep_shadow<kCull>(g, rad, a.n, hit, so, sd, lp, h.sph, dist, bv, work);
       if (hit && !occ) {
         const double ndl = max0(dot(nrm, ldir));
         const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);

@@ -1,0 +1,291 @@
+// bvh_sim.cpp -- CPU model of the render loop's BVH traversal cost (tuning
+// tool, not part of the product).  Traces a frame in fp64, groups lanes into
+// 8x8-pixel waves as the megakernel does, and for every closest-hit / shadow
+// query counts per-lane node visits and sphere tests under several traversal
+// strategies; the "wave trips" column is the per-query maximum over the
+// wave's lanes (what a divergent SIMD loop pays).
+//
+//   g++ -O2 -std=c++17 -I include -o /tmp/bvh_sim scripts/bvh_sim.cpp \
+//       cs420-ray-tracer_amd/csrc/rt_bvh.cpp cs420-ray-tracer_amd/csrc/rt_host.cpp
+//   /tmp/bvh_sim scene.txt W H depth [max_leaf]
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../cs420-ray-tracer_amd/csrc/rt_bvh.h"
+#include "rt_hip.h"
+
+using rtk::BvhNode;
+struct V {
+  double x, y, z;
+};
+static V operator+(V a, V b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static V operator-(V a, V b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static V operator*(V a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+static double dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static V nrmz(V a) { return a * (1.0 / std::sqrt(dot(a, a))); }
+
+struct Scene {
+  std::vector<V> c;
+  std::vector<double> r, refl;
+  std::vector<V> lights;
+};
+
+static bool hit_sphere(const Scene &s, int i, V o, V d, double &t) {
+  V oc = o - s.c[i];
+  double a = dot(d, d), b = 2 * dot(oc, d), cc = dot(oc, oc) - s.r[i] * s.r[i];
+  double disc = b * b - 4 * a * cc;
+  if (disc < 0) return false;
+  double sq = std::sqrt(disc), t1 = (-b - sq) / (2 * a), t2 = (-b + sq) / (2 * a);
+  if (std::max(t1, t2) < 0) return false;
+  t = t1 < 0 ? t2 : t1;
+  return true;
+}
+
+struct Stats {
+  double lane_nodes = 0, lane_tests = 0, wave_nodes = 0, wave_tests = 0, wave_trips = 0;
+  long queries = 0, wq = 0;
+};
+
+// one strategy; returns per-lane (nodes, tests) for a query
+struct Strategy {
+  const char *name;
+  int kind;      // 0 stackless preorder, 1 ordered stack BVH2, 2 ordered BVH4
+  bool forward;  // prune boxes wholly behind the origin
+};
+
+struct Bvh4 {
+  struct Node {
+    float lo[4][3], hi[4][3];
+    int child[4];  // >=0 inner node, <0: leaf -(first<<4|count)-1, INT_MIN empty
+  };
+  std::vector<Node> n;
+};
+
+static const std::vector<BvhNode> *g_nodes;
+static const std::vector<int32_t> *g_prims;
+
+static bool box(const float *lo, const float *hi, V o, V inv, double &tn, double &tf) {
+  double a[3] = {(lo[0] - o.x) * inv.x, (lo[1] - o.y) * inv.y, (lo[2] - o.z) * inv.z};
+  double b[3] = {(hi[0] - o.x) * inv.x, (hi[1] - o.y) * inv.y, (hi[2] - o.z) * inv.z};
+  tn = std::max({std::min(a[0], b[0]), std::min(a[1], b[1]), std::min(a[2], b[2])});
+  tf = std::min({std::max(a[0], b[0]), std::max(a[1], b[1]), std::max(a[2], b[2])});
+  return tn <= tf;
+}
+
+// Children of BVH2 node i (preorder + skip): left = i+1, right = nodes[i+1].skip
+static void walk2(const Scene &s, const Strategy &st, V o, V d, bool shadow, double T, double &bt, int &bi,
+                  long &nodes, long &tests) {
+  const auto &N = *g_nodes;
+  const auto &P = *g_prims;
+  V inv{1 / d.x, 1 / d.y, 1 / d.z};
+  auto leaf = [&](const BvhNode &nd) -> bool {
+    int first = nd.leaf >> 4, cnt = nd.leaf & 15;
+    for (int k = 0; k < cnt; k++) {
+      int i = P[first + k];
+      tests++;
+      double t;
+      if (hit_sphere(s, i, o, d, t)) {
+        if (shadow) {
+          if (t < T) return false;
+        } else if (t < bt || (t == bt && i < bi)) {
+          bt = t;
+          bi = i;
+        }
+      }
+    }
+    return true;
+  };
+  auto lim = [&]() { return shadow ? T : bt; };
+  if (st.kind == 0) {
+    int i = 0, n = (int)N.size();
+    while (i < n) {
+      nodes++;
+      double tn, tf;
+      bool in = box(N[i].lo, N[i].hi, o, inv, tn, tf) && !(tn > lim()) && (!st.forward || tf >= 0);
+      if (in && N[i].leaf >= 0) {
+        if (!leaf(N[i])) return;
+        i = N[i].skip;
+      } else
+        i = in ? i + 1 : N[i].skip;
+    }
+    return;
+  }
+  // ordered: stack of (node, tn)
+  std::vector<std::pair<int, double>> stk;
+  double tn0, tf0;
+  nodes++;
+  if (!box(N[0].lo, N[0].hi, o, inv, tn0, tf0)) return;
+  stk.push_back({0, tn0});
+  while (!stk.empty()) {
+    auto [i, tn] = stk.back();
+    stk.pop_back();
+    if (tn > lim()) continue;
+    if (N[i].leaf >= 0) {
+      if (!leaf(N[i])) return;
+      continue;
+    }
+    int l = i + 1, r = N[i + 1].skip;
+    double tnl, tfl, tnr, tfr;
+    nodes++;  // one visit tests both children (child boxes stored in the parent)
+    bool hl = box(N[l].lo, N[l].hi, o, inv, tnl, tfl) && !(tnl > lim()) && (!st.forward || tfl >= 0);
+    bool hr = box(N[r].lo, N[r].hi, o, inv, tnr, tfr) && !(tnr > lim()) && (!st.forward || tfr >= 0);
+    if (hl && hr) {
+      if (tnl <= tnr) {
+        stk.push_back({r, tnr});
+        stk.push_back({l, tnl});
+      } else {
+        stk.push_back({l, tnl});
+        stk.push_back({r, tnr});
+      }
+    } else if (hl)
+      stk.push_back({l, tnl});
+    else if (hr)
+      stk.push_back({r, tnr});
+  }
+}
+
+int main(int argc, char **argv) {
+  if (argc < 5) {
+    std::fprintf(stderr, "usage: bvh_sim scene W H depth [max_leaf]\n");
+    return 2;
+  }
+  rt_scene sc;
+  if (rt_scene_load(argv[1], &sc, 0) != 0) return 1;
+  rt_camera cam;
+  rt_camera_from_scene(&sc, &cam);
+  const int W = std::atoi(argv[2]), H = std::atoi(argv[3]), D = std::atoi(argv[4]);
+  const int max_leaf = argc > 5 ? std::atoi(argv[5]) : 4;
+  Scene s;
+  std::vector<double> cx, cy, cz, rr;
+  for (int i = 0; i < sc.num_spheres; i++) {
+    const rt_sphere &q = sc.spheres[i];
+    s.c.push_back({q.center[0], q.center[1], q.center[2]});
+    s.r.push_back(q.radius);
+    s.refl.push_back(q.reflectivity);
+    cx.push_back(q.center[0]);
+    cy.push_back(q.center[1]);
+    cz.push_back(q.center[2]);
+    rr.push_back(q.radius);
+  }
+  for (int l = 0; l < sc.num_lights; l++)
+    s.lights.push_back({sc.lights[l].position[0], sc.lights[l].position[1], sc.lights[l].position[2]});
+  std::vector<BvhNode> nodes;
+  std::vector<int32_t> prims;
+  rtk::build_bvh(cx.data(), cy.data(), cz.data(), rr.data(), (int)s.r.size(), max_leaf, nodes, prims);
+  g_nodes = &nodes;
+  g_prims = &prims;
+  std::printf("spheres %zu nodes %zu\n", s.r.size(), nodes.size());
+  const Strategy strats[] = {{"preorder-line", 0, false}, {"preorder-fwd", 0, true}, {"ordered-line", 1, false},
+                             {"ordered-fwd", 1, true}};
+  const int NS = 4;
+  // stats[strategy][class]: class 0 primary closest, 1 primary shadow, 2 secondary closest, 3 secondary shadow
+  Stats stats[NS][4];
+  V P{cam.position[0], cam.position[1], cam.position[2]};
+  V F{cam.forward[0], cam.forward[1], cam.forward[2]}, R{cam.right[0], cam.right[1], cam.right[2]},
+      U{cam.up[0], cam.up[1], cam.up[2]};
+  for (int ty = 0; ty < H; ty += 8)
+    for (int tx = 0; tx < W; tx += 8) {
+      // lanes
+      V o[64], d[64];
+      bool alive[64];
+      for (int l = 0; l < 64; l++) {
+        int x = tx + (l & 7), y = ty + (l >> 3);
+        alive[l] = x < W && y < H;
+        if (!alive[l]) continue;
+        int j = H - 1 - y;
+        double u = (double)x / (W - 1), v = (double)j / (H - 1);
+        V dir = F + R * ((u - 0.5) * cam.scale) + U * ((v - 0.5) * cam.scale);
+        d[l] = nrmz(dir);
+        o[l] = P;
+      }
+      for (int lev = 0; lev < D; lev++) {
+        int cls = lev == 0 ? 0 : 2;
+        double bt[64];
+        int bi[64];
+        // closest per strategy (results must agree; use strategy 0's)
+        for (int k = 0; k < NS; k++) {
+          long mx_n = 0, mx_t = 0, any = 0;
+          for (int l = 0; l < 64; l++) {
+            if (!alive[l]) continue;
+            any = 1;
+            long nn = 0, nt = 0;
+            double t = INFINITY;
+            int b = -1;
+            walk2(s, strats[k], o[l], d[l], false, 0, t, b, nn, nt);
+            if (k == 0) {
+              bt[l] = t;
+              bi[l] = b;
+            }
+            stats[k][cls].lane_nodes += nn;
+            stats[k][cls].lane_tests += nt;
+            stats[k][cls].queries++;
+            mx_n = std::max(mx_n, nn);
+            mx_t = std::max(mx_t, nt);
+          }
+          if (any) {
+            stats[k][cls].wave_nodes += mx_n;
+            stats[k][cls].wave_tests += mx_t;
+            stats[k][cls].wq++;
+          }
+        }
+        bool hit[64];
+        V hp[64], nrm[64];
+        for (int l = 0; l < 64; l++) {
+          hit[l] = alive[l] && bi[l] >= 0;
+          if (!hit[l]) continue;
+          hp[l] = o[l] + d[l] * bt[l];
+          nrm[l] = nrmz(hp[l] - s.c[bi[l]]);
+        }
+        for (size_t L = 0; L < s.lights.size(); L++) {
+          for (int k = 0; k < NS; k++) {
+            long mx_n = 0, mx_t = 0, any = 0;
+            for (int l = 0; l < 64; l++) {
+              if (!hit[l]) continue;
+              any = 1;
+              V tl = s.lights[L] - hp[l];
+              double dist = std::sqrt(dot(tl, tl));
+              V ld = nrmz(tl);
+              long nn = 0, nt = 0;
+              double t = 0;
+              int b = 0;
+              walk2(s, strats[k], hp[l] + ld * 0.001, ld, true, dist, t, b, nn, nt);
+              stats[k][cls + 1].lane_nodes += nn;
+              stats[k][cls + 1].lane_tests += nt;
+              stats[k][cls + 1].queries++;
+              mx_n = std::max(mx_n, nn);
+              mx_t = std::max(mx_t, nt);
+            }
+            if (any) {
+              stats[k][cls + 1].wave_nodes += mx_n;
+              stats[k][cls + 1].wave_tests += mx_t;
+              stats[k][cls + 1].wq++;
+            }
+          }
+        }
+        for (int l = 0; l < 64; l++) {
+          if (!hit[l] || s.refl[bi[l]] <= 0 || lev + 1 >= D) {
+            alive[l] = false;
+            continue;
+          }
+          V rd = d[l] - nrm[l] * (2 * dot(d[l], nrm[l]));
+          o[l] = hp[l] + nrm[l] * 0.001;
+          d[l] = nrmz(rd);
+        }
+      }
+    }
+  const char *cn[4] = {"primary", "prim-shadow", "secondary", "sec-shadow"};
+  for (int c = 0; c < 4; c++) {
+    std::printf("%-12s queries %ld waves %ld\n", cn[c], stats[0][c].queries, stats[0][c].wq);
+    for (int k = 0; k < NS; k++) {
+      const Stats &q = stats[k][c];
+      std::printf("   %-15s lane nodes/q %6.2f tests/q %6.2f | wave-max nodes/wq %7.2f tests/wq %6.2f | tot wave "
+                  "node-trips %.3g test-trips %.3g\n",
+                  strats[k].name, q.lane_nodes / q.queries, q.lane_tests / q.queries, q.wave_nodes / q.wq,
+                  q.wave_tests / q.wq, q.wave_nodes, q.wave_tests);
+    }
+  }
+  return 0;
+}

@@ -7,7 +7,7 @@ import sys
 
 if len(sys.argv) > 2 and sys.argv[1] == "--analyse":
     import numpy as np
-    a = np.fromfile(sys.argv[2], dtype=np.uint64).reshape(-1, 12)
+    a = np.fromfile(sys.argv[2], dtype=np.uint64).reshape(-1, 16)
     n = int(sys.argv[3]) if len(sys.argv) > 3 else (a[:, 1] > 0).sum()
     a = a[:n]
     t0 = a[:, 0].min()
@@ -33,6 +33,9 @@ if len(sys.argv) > 2 and sys.argv[1] == "--analyse":
     for w in order:
         it, sw = int(a[w, 8]) & 0xFFFFFFFF, int(a[w, 8]) >> 32
         print(f"   {w:6d} ({w % W_tiles:3d},{w // W_tiles:3d}) {d[w]:7.1f} bvhmax {a[w,9]:5d} | {a[w,3]:8d} {a[w,4]:8d} {a[w,5]:9d} {a[w,6]:8d} {a[w,10]:8d} {a[w,7]:9d} | {it:5d} {sw:4d}")
+    print("  slowest waves: closest-sweep shadow-sweep bvh cycles | bvh wave trips, max lane steps")
+    for w in order:
+        print(f"   {w:6d} {a[w,12]:9d} {a[w,13]:9d} {a[w,10]:9d} | {a[w,14]:6d} {a[w,9]:6d}")
     med = np.argsort(d)[len(d)//2]
     w = med
     print(f"  median wave {w}: {d[w]:.1f} us | {a[w,3]} {a[w,4]} {a[w,5]} {a[w,6]} {a[w,10]} {a[w,7]} | {int(a[w,8]) & 0xFFFFFFFF} {int(a[w,8]) >> 32}")
