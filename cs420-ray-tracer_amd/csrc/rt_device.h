@@ -281,6 +281,8 @@ __device__ __forceinline__ unsigned long long rt_stamp() {
 struct BvhArgs {
   const BvhNode *nodes;
   const int32_t *prims;
+  const float4 *pf;     // per leaf slot: sphere centre - c0 (fp32) and |radius| rounded up
+  float pmargin;        // prefilter margin (4x the box margin)
   int nnodes;
   float margin;
   double c0x, c0y, c0z;
@@ -297,7 +299,9 @@ struct BvhArgs {
 template <typename T, typename F>
 __device__ __forceinline__ void bvh_walk(const BvhArgs &bv, D3 o, D3 d, T &&tmax_fn, Work &work, F &&leaf_fn) {
   const float ox = (float)(o.x - bv.c0x), oy = (float)(o.y - bv.c0y), oz = (float)(o.z - bv.c0z);
-  const float ix = 1.0f / (float)d.x, iy = 1.0f / (float)d.y, iz = 1.0f / (float)d.z;
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+  const float dd = (dx * dx + dy * dy + dz * dz) * (1.0f + 1e-5f);
   const float m = bv.margin;
   int i = 0;
   while (i < bv.nnodes) {
@@ -319,8 +323,17 @@ __device__ __forceinline__ void bvh_walk(const BvhArgs &bv, D3 o, D3 d, T &&tmax
 #endif
     if (in && nd.leaf >= 0) {
       const int first = nd.leaf >> 4, cnt = nd.leaf & 15;
-      for (int k = 0; k < cnt; ++k)
+      for (int k = 0; k < cnt; ++k) {
+        // fp32 prefilter: the line misses the sphere grown by pmargin (fp32
+        // rounding of the distance is < 6e-7 * diameter, the fp64 test can
+        // only hit within 2e-8 * diameter of the surface; NaN passes)
+        const float4 q = bv.pf[first + k];
+        const float wx = q.x - ox, wy = q.y - oy, wz = q.z - oz;
+        const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
+        const float R = q.w + bv.pmargin;
+        if (cx * cx + cy * cy + cz * cz > R * R * dd) continue;
         if (!leaf_fn((int)bv.prims[first + k])) return;
+      }
       i = nd.skip;
     } else {
       i = in ? i + 1 : nd.skip;
@@ -332,17 +345,20 @@ __device__ __forceinline__ void bvh_walk(const BvhArgs &bv, D3 o, D3 d, T &&tmax
 // scene is staged (lds_geo) and has a BVH, its nodes and leaf sphere indices.
 // The host sizes the dynamic LDS with the same function.
 struct LdsLayout {
-  size_t rad, light, nodes, prims, end;
+  size_t rad, light, nodes, pf, prims, end;
 };
 __host__ __device__ inline LdsLayout lds_layout(bool lds_geo, int n, int nl, int nnodes) {
   LdsLayout L;
   L.rad = lds_geo ? (size_t)n * sizeof(SphGeo) : 0;
   L.light = lds_geo ? (size_t)n * (sizeof(SphGeo) + sizeof(double)) : 0;
   size_t e = (L.light + (size_t)nl * sizeof(LightD) + 15) & ~(size_t)15;
+  const bool bvh = lds_geo && nnodes > 0;
   L.nodes = e;
-  if (lds_geo && nnodes > 0) e += (size_t)nnodes * sizeof(BvhNode);
+  if (bvh) e += (size_t)nnodes * sizeof(BvhNode);
+  L.pf = e;
+  if (bvh) e += (size_t)n * sizeof(float4);
   L.prims = e;
-  if (lds_geo && nnodes > 0) e += (size_t)n * sizeof(int32_t);
+  if (bvh) e += (size_t)n * sizeof(int32_t);
   L.end = e;
   return L;
 }
@@ -359,6 +375,7 @@ __device__ __forceinline__ void stage_scene(unsigned char *smem, const SphGeo *g
   LightD *slight = reinterpret_cast<LightD *>(smem + L.light);
   BvhNode *snodes = reinterpret_cast<BvhNode *>(smem + L.nodes);
   int32_t *sprims = reinterpret_cast<int32_t *>(smem + L.prims);
+  float4 *spf = reinterpret_cast<float4 *>(smem + L.pf);
   const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
   if (kLdsGeo) {
     for (int i = tid; i < n; i += nt) {
@@ -367,7 +384,10 @@ __device__ __forceinline__ void stage_scene(unsigned char *smem, const SphGeo *g
     }
     if (bv.nnodes > 0) {
       for (int i = tid; i < bv.nnodes; i += nt) snodes[i] = bv.nodes[i];
-      for (int i = tid; i < n; i += nt) sprims[i] = bv.prims[i];
+      for (int i = tid; i < n; i += nt) {
+        sprims[i] = bv.prims[i];
+        spf[i] = bv.pf[i];
+      }
     }
   }
   for (int i = tid; i < nl; i += nt) slight[i] = lights[i];
@@ -378,6 +398,7 @@ __device__ __forceinline__ void stage_scene(unsigned char *smem, const SphGeo *g
   if (kLdsGeo) {
     bv.nodes = snodes;
     bv.prims = sprims;
+    bv.pf = spf;
   }
 }
 

@@ -306,6 +306,7 @@ struct rt_ctx {
   // BVH over the spheres (fallback for incoherent groups), built at upload
   BvhNode *d_bvh = nullptr;
   int32_t *d_prims = nullptr;
+  float4 *d_pf = nullptr;
   int bvh_nodes = 0;
   // per-light direction grids for shadow rays (rt_lightgrid.h), built at upload
   int32_t *d_lg_start = nullptr, *d_lg_ids = nullptr;
@@ -314,7 +315,7 @@ struct rt_ctx {
   double c0[3] = {0, 0, 0};
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
   double rmax = 0;
-  int bvh_min = 24, bvh_always = 0, bvh_on = 1, bvh_groups = 2;
+  int bvh_min = 24, bvh_always = 0, bvh_on = 1, bvh_groups = 2, bvh_leaf = 4;
   int wg_waves = 4;  // megakernel waves per workgroup (tuning knob RT_HIP_WG_WAVES = 1 | 4)
   int pipeline = 0;  // 0 = megakernel (default), 1 = wavefront queues (knob RT_HIP_PIPELINE)
   int n_cu = 256;
@@ -357,6 +358,8 @@ void free_scene(rt_ctx *c) {
   if (c->d_lights) (void)hipFree(c->d_lights);
   if (c->d_bvh) (void)hipFree(c->d_bvh);
   if (c->d_prims) (void)hipFree(c->d_prims);
+  if (c->d_pf) (void)hipFree(c->d_pf);
+  c->d_pf = nullptr;
   if (c->d_lg_start) (void)hipFree(c->d_lg_start);
   if (c->d_lg_ids) (void)hipFree(c->d_lg_ids);
   c->d_lg_start = c->d_lg_ids = nullptr;
@@ -376,6 +379,7 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   BvhArgs b;
   b.nodes = c->d_bvh;
   b.prims = c->d_prims;
+  b.pf = c->d_pf;
   b.nnodes = (c->bvh_on && c->cull) ? c->bvh_nodes : 0;
   b.c0x = c->c0[0];
   b.c0y = c->c0[1];
@@ -389,6 +393,7 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   b.diam = std::sqrt(d2) + 0.01;  // + the 0.001 origin offsets of secondary rays
   const double m = 1e-6 * (b.diam + c->rmax);
   b.margin = std::isfinite(m) ? (float)(m * (1.0 + 1e-6)) : INFINITY;
+  b.pmargin = 4.0f * b.margin;
   if (!std::isfinite(b.diam)) b.diam = INFINITY;
   b.min_cands = c->bvh_min;
   b.always = c->bvh_always;
@@ -610,6 +615,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH_ALWAYS")) c->bvh_always = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_GROUPS")) c->bvh_groups = std::max(1, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID")) c->lg_on = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n = std::max(1, std::min(256, std::atoi(e)));
   auto bail = [&](int rc) {
     rt_destroy(c);
@@ -712,10 +718,21 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
   }
   std::vector<BvhNode> nodes;
   std::vector<int32_t> prims;
-  build_bvh(bx.data(), by.data(), bz.data(), br.data(), n, 4, nodes, prims);
+  build_bvh(bx.data(), by.data(), bz.data(), br.data(), n, c->bvh_leaf, nodes, prims);
+  // prefilter records in leaf order (centre - c0 in fp32, |radius| rounded up)
+  std::vector<float4> pf(prims.size());
+  for (size_t k = 0; k < prims.size(); k++) {
+    const int id = prims[k];
+    float rr = (float)std::fabs(br[id]);
+    if ((double)rr < std::fabs(br[id])) rr = std::nextafter(rr, INFINITY);
+    pf[k] = make_float4((float)bx[id], (float)by[id], (float)bz[id], rr);
+  }
   int rc = RT_OK;
   hipError_t e = hipSuccess;
-  if ((e = hipMalloc(&c->d_bvh, sizeof(BvhNode) * (nodes.size() + 1))) != hipSuccess ||
+  if ((e = hipMalloc(&c->d_pf, sizeof(float4) * (pf.size() + 1))) != hipSuccess ||
+      (!pf.empty() && (e = hipMemcpy(c->d_pf, pf.data(), sizeof(float4) * pf.size(), hipMemcpyHostToDevice)) !=
+                          hipSuccess) ||
+      (e = hipMalloc(&c->d_bvh, sizeof(BvhNode) * (nodes.size() + 1))) != hipSuccess ||
       (e = hipMalloc(&c->d_prims, sizeof(int32_t) * (prims.size() + 1))) != hipSuccess ||
       (!nodes.empty() &&
        (e = hipMemcpy(c->d_bvh, nodes.data(), sizeof(BvhNode) * nodes.size(), hipMemcpyHostToDevice)) != hipSuccess) ||
