@@ -43,33 +43,21 @@ constexpr int kTl = 16;  // u64 per wave
 __device__ unsigned long long g_timeline[kTimelineWaves * kTl];
 #endif
 
-// One lane per pixel; the whole wave walks the reflection levels together
-// (uniform control flow around every sweep, lanes masked by `alive`/`hit`).
-#ifndef RT_MIN_WAVES_PER_EU
-#define RT_MIN_WAVES_PER_EU 1
-#endif
-template <int MAXS, bool kLdsGeo, bool kCull, int kWaves, bool kLdsStack = (MAXS <= 4)>
-__global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kernel(const SphGeo *__restrict__ geo, const double *__restrict__ radius,
-                                                        const SphMat *__restrict__ mat,
-                                                        const LightD *__restrict__ lights, int n, int nl, D3 amb,
-                                                        Cam cam, int W, int H, int depth, Rows rows, BvhArgs bv_in, LgArgs lg,
-                                                        uint8_t *__restrict__ out,
-                                                        unsigned long long *__restrict__ counters) {
-  extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
-  const int tid = threadIdx.x;
-  const SphGeo *g;
-  const double *rad;
-  const LightD *slight;
-  BvhArgs bv = bv_in;
-  stage_scene<kLdsGeo>(smem, geo, radius, lights, n, nl, bv, g, rad, slight);
-  // per-wave reflection stack after the staged scene, 32-B aligned
-  const size_t stack_off = (lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31;
+constexpr int kMaxLdsStack = 4;  // levels of the LDS reflection stack (render_kernel)
 
-  // Workgroup = kWaves waves, each an 8x8 pixel tile (2x2 waves for kWaves = 4).
-  constexpr int kWx = kWaves == 4 ? 2 : 1;
-  const int wave = tid >> 6, lane = tid & 63;
-  const int x = blockIdx.x * (8 * kWx) + (wave % kWx) * 8 + (lane & 7);
-  const int k = blockIdx.y * (8 * (kWaves / kWx)) + (wave / kWx) * 8 + (lane >> 3);
+// One 8x8 tile, one lane per pixel; the whole wave walks the reflection
+// levels together (uniform control flow around every sweep, lanes masked by
+// `alive`/`hit`).  `stk` is this wave's reflection stack, [level][lane]
+// (depth - 1 levels).  Adds the tile's ray counts to the wave sums.
+template <bool kCull>
+__device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                           const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
+                                           int nl, D3 amb, const Cam &cam, int W, int H, int depth, const Rows &rows,
+                                           const BvhArgs &bv, const LgArgs &lg, uint8_t *__restrict__ out, int x0,
+                                           int k0, StackEnt *stk, Work &work, unsigned long long (&sums)[4]) {
+  const int lane = threadIdx.x & 63;
+  const int x = x0 + (lane & 7);
+  const int k = k0 + (lane >> 3);
   const bool in_tile = x < W && k < rows.count;
   const long long y = (long long)(k / rows.band) * rows.band * rows.stride + (long long)rows.first * rows.band +
                       (k % rows.band);
@@ -85,21 +73,11 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   D3 o = mk(cam.px, cam.py, cam.pz);
   int key = -1;  // sphere the current ray leaves (-1: camera), groups lanes in sweeps
 
-  // Reflection stack, one slot per level and lane, in LDS (kLdsStack: after
-  // the staged scene) or in per-lane private memory for the deepest variant.
-  double stA[3][kLdsStack ? 1 : MAXS];
-  double stR[kLdsStack ? 1 : MAXS];
-  StackEnt *lstack = reinterpret_cast<StackEnt *>(smem + stack_off) + (size_t)wave * MAXS * 64;
   int lev = 0;
   int dleft = depth;
   D3 res = mk(0.0, 0.0, 0.0);     // depth <= 0 -> black (main.cpp:17-18)
   bool alive = in_img && depth >= 1;
   unsigned c_prim = alive ? 1u : 0u, c_shadow = 0, c_reflect = 0, c_neg = 0;
-  Work work;
-  RT_T0(t_wave);
-#ifdef RT_STAMPS
-  const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
-#endif
 
   while (__ballot(alive)) {
     double bt;
@@ -177,15 +155,8 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
       if (m.refl > 0.0) {                                         // main.cpp:43-55
         const double w = 1.0 - m.refl;
         const D3 A = mk(col.x * w, col.y * w, col.z * w);
-        if (dleft - 1 >= 1) {  // host picks MAXS >= depth-1, so lev < MAXS here
-          if (kLdsStack) {
-            lstack[lev * 64 + lane] = StackEnt{A.x, A.y, A.z, m.refl};
-          } else {
-            stA[0][lev] = A.x;
-            stA[1][lev] = A.y;
-            stA[2][lev] = A.z;
-            stR[lev] = m.refl;
-          }
+        if (dleft - 1 >= 1) {  // the stack holds depth-1 levels, so lev < depth-1 here
+          stk[lev * 64 + lane] = StackEnt{A.x, A.y, A.z, m.refl};
           ++lev;
           const SphGeo sg = g[hi];
           const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));
@@ -207,13 +178,8 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   }
   while (lev > 0) {  // unwind: shade*(1-refl) + reflected*refl, innermost first
     --lev;
-    if (kLdsStack) {
-      const StackEnt e = lstack[lev * 64 + lane];
-      res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
-    } else {
-      const double r = stR[lev];
-      res = mk(stA[0][lev] + res.x * r, stA[1][lev] + res.y * r, stA[2][lev] + res.z * r);
-    }
+    const StackEnt e = stk[lev * 64 + lane];
+    res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
   }
   if (in_tile) {
     uint8_t *px = out + ((size_t)k * W + x) * 3;
@@ -227,14 +193,41 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
       px[0] = px[1] = px[2] = 0;
     }
   }
-  const unsigned long long sp = wave_sum(c_prim), ss = wave_sum(c_shadow), sr = wave_sum(c_reflect),
-                           sn = wave_sum(c_neg);
-  RT_ACC(work, 5, t_wave);
+  sums[0] += wave_sum(c_prim);
+  sums[1] += wave_sum(c_shadow);
+  sums[2] += wave_sum(c_reflect);
+  sums[3] += wave_sum(c_neg);
+}
+
+// Flushes a wave's ray counts and work counters into its counter shard.
+__device__ __forceinline__ void flush_counts(unsigned long long *counters, const unsigned long long (&sums)[4],
+                                             const Work &work) {
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long *sc = counter_shard(counters);
 #ifdef RT_STAMPS
+    for (int q = 0; q < 6; q++) atomicAdd(&sc[8 + q], work.st[q]);
+    atomicAdd(&sc[20], work.st[6]);
+    atomicAdd(&sc[14], 1ull);
+    atomicAdd(&sc[15], work.iters);
+    atomicAdd(&sc[16], work.sweeps);
+    atomicAdd(&sc[17], work.it_closest);
+    atomicAdd(&sc[18], work.sw_closest);
+    atomicAdd(&sc[19], work.it_prim);
+#endif
+    for (int q = 0; q < 4; q++)
+      if (sums[q]) atomicAdd(&sc[q], sums[q]);
+    if (work.exact) atomicAdd(&sc[4], work.exact);
+    if (work.cull) atomicAdd(&sc[5], work.cull);
+  }
+}
+
+#ifdef RT_STAMPS
+__device__ __forceinline__ void record_timeline(unsigned wave_id, unsigned long long t_real0, const Work &work) {
+  const int lane = threadIdx.x & 63;
   const unsigned long long bvh_steps_max = (unsigned long long)wmax((double)work.st[7]);
   const unsigned long long wave_trips = wave_sum((unsigned)work.st[10]);
   if (lane == 0) {
-    const unsigned wid = (blockIdx.x + blockIdx.y * gridDim.x) * kWaves + wave;
+    const unsigned wid = wave_id;
     if (wid < (unsigned)kTimelineWaves) {
       unsigned long long *tl = g_timeline + (size_t)kTl * wid;
       tl[0] = t_real0;
@@ -256,26 +249,104 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
       tl[9] = bvh_steps_max;  // most BVH node visits of one lane
     }
   }
+}
 #endif
-  if (lane == 0) {
-    unsigned long long *sc = counter_shard(counters);
+
+#ifndef RT_MIN_WAVES_PER_EU
+#define RT_MIN_WAVES_PER_EU 1
+#endif
+// One wave per 8x8 tile (2x2 tiles per workgroup for kWaves = 4); the
+// reflection stack (depth <= 5) lives in LDS after the staged scene.
+template <bool kLdsGeo, bool kCull, int kWaves>
+__global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kernel(
+    const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
+    const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
+    BvhArgs bv_in, LgArgs lg, uint8_t *__restrict__ out, unsigned long long *__restrict__ counters) {
+  extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
+  const SphGeo *g;
+  const double *rad;
+  const LightD *slight;
+  BvhArgs bv = bv_in;
+  stage_scene<kLdsGeo>(smem, geo, radius, lights, n, nl, bv, g, rad, slight);
+  const size_t stack_off = (lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31;
+  constexpr int kWx = kWaves == 4 ? 2 : 1;
+  const int wave = threadIdx.x >> 6;
+  StackEnt *stk = reinterpret_cast<StackEnt *>(smem + stack_off) + (size_t)wave * kMaxLdsStack * 64;
+  Work work;
+  unsigned long long sums[4] = {0, 0, 0, 0};
+  RT_T0(t_wave);
 #ifdef RT_STAMPS
-    for (int q = 0; q < 6; q++) atomicAdd(&sc[8 + q], work.st[q]);
-    atomicAdd(&sc[20], work.st[6]);
-    atomicAdd(&sc[14], 1ull);
-    atomicAdd(&sc[15], work.iters);
-    atomicAdd(&sc[16], work.sweeps);
-    atomicAdd(&sc[17], work.it_closest);
-    atomicAdd(&sc[18], work.sw_closest);
-    atomicAdd(&sc[19], work.it_prim);
+  const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (sp) atomicAdd(&sc[0], sp);
-    if (ss) atomicAdd(&sc[1], ss);
-    if (sr) atomicAdd(&sc[2], sr);
-    if (sn) atomicAdd(&sc[3], sn);
-    if (work.exact) atomicAdd(&sc[4], work.exact);
-    if (work.cull) atomicAdd(&sc[5], work.cull);
+  trace_tile<kCull>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, out,
+                    blockIdx.x * (8 * kWx) + (wave % kWx) * 8, blockIdx.y * (8 * (kWaves / kWx)) + (wave / kWx) * 8,
+                    stk, work, sums);
+  RT_ACC(work, 5, t_wave);
+#ifdef RT_STAMPS
+  record_timeline((blockIdx.x + blockIdx.y * gridDim.x) * kWaves + wave, t_real0, work);
+#endif
+  flush_counts(counters, sums, work);
+}
+
+// Persistent variant: a resident grid whose waves take 8x8 tiles from 64
+// sharded tile counters (tiles in scanline order; a wave moves to the next
+// shard when its own is drained), so the scene is staged once per workgroup
+// and the reflection stack of any depth sits in global memory, one
+// [level][lane] slice per wave.
+constexpr int kTileShards = 64;
+#ifndef RT_PERSIST_WAVES_PER_EU
+#define RT_PERSIST_WAVES_PER_EU 3
+#endif
+template <bool kLdsGeo, bool kCull, int kWaves>
+__global__ __launch_bounds__(64 * kWaves, RT_PERSIST_WAVES_PER_EU) void render_persist(
+    const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
+    const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
+    BvhArgs bv_in, LgArgs lg, uint8_t *__restrict__ out, unsigned long long *__restrict__ counters,
+    StackEnt *__restrict__ gstack, unsigned *__restrict__ tile_ctr, int ntx, int ntiles) {
+  extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
+  const SphGeo *g;
+  const double *rad;
+  const LightD *slight;
+  BvhArgs bv = bv_in;
+  stage_scene<kLdsGeo>(smem, geo, radius, lights, n, nl, bv, g, rad, slight);
+  const unsigned wave_id = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int levels = depth > 1 ? depth - 1 : 1;
+  StackEnt *stk = gstack + (size_t)wave_id * levels * 64;
+  const int per = (ntiles + kTileShards - 1) / kTileShards;
+  int shard = (int)(wave_id % kTileShards);
+  Work work;
+  unsigned long long sums[4] = {0, 0, 0, 0};
+  RT_T0(t_wave);
+#ifdef RT_STAMPS
+  const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  // The next tile index is requested before the current tile is traced, so
+  // the atomic's latency overlaps the work.
+  auto fetch = [&](int sh) -> unsigned {
+    unsigned t = 0;
+    if ((threadIdx.x & 63) == 0) t = atomicAdd(&tile_ctr[sh * 64], 1u);
+    return t;
+  };
+  unsigned pending = fetch(shard);
+  for (int tries = 0; tries < kTileShards;) {
+    const unsigned t = __builtin_amdgcn_readfirstlane(pending);
+    const long long tile = (long long)shard * per + t;
+    if ((int)t >= per || tile >= ntiles) {  // shard drained
+      shard = shard + 1 == kTileShards ? 0 : shard + 1;
+      ++tries;
+      if (tries < kTileShards) pending = fetch(shard);
+      continue;
+    }
+    pending = fetch(shard);
+    const int ty = (int)(tile / ntx), tx = (int)(tile % ntx);
+    trace_tile<kCull>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, out, tx * 8, ty * 8, stk,
+                      work, sums);
   }
+  RT_ACC(work, 5, t_wave);
+#ifdef RT_STAMPS
+  record_timeline(wave_id, t_real0, work);
+#endif
+  flush_counts(counters, sums, work);
 }
 
 // Reassemble rank-major shards into PPM row order (one workgroup per row).
@@ -335,6 +406,10 @@ struct rt_ctx {
   long long launches = 0, hist_begin = 0;
   uint8_t *d_tmp = nullptr;
   size_t tmp_bytes = 0;
+  // persistent megakernel: tile counters + per-wave reflection stacks (grown on demand)
+  unsigned char *stack_buf = nullptr;
+  size_t stack_bytes = 0;
+  int persist = 0;  // RT_HIP_PERSIST=1: persistent megakernel for every depth (always used above depth 5)
   std::string err;
 };
 
@@ -411,35 +486,76 @@ LgArgs lg_args(const rt_ctx *c) {
   return g;
 }
 
-template <int MAXS, bool kCull, int kWaves>
-void launch_render3(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                    uint8_t *out) {
+template <bool kCull, int kWaves>
+void launch_tiles(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
+                  uint8_t *out) {
   const BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
   constexpr int kWx = kWaves == 4 ? 2 : 1, kWy = kWaves / kWx;
   dim3 grid((W + 8 * kWx - 1) / (8 * kWx), (rows.count + 8 * kWy - 1) / (8 * kWy));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
-  if (MAXS <= 4) lds = ((lds + 31) & ~(size_t)31) + (size_t)kWaves * 64 * MAXS * sizeof(StackEnt);
+  lds = ((lds + 31) & ~(size_t)31) + (size_t)kWaves * 64 * kMaxLdsStack * sizeof(StackEnt);
   if (lds_geo)
-    hipLaunchKernelGGL((render_kernel<MAXS, true, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
+    hipLaunchKernelGGL((render_kernel<true, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
                        c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, out,
                        c->d_counters);
   else
-    hipLaunchKernelGGL((render_kernel<MAXS, false, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
+    hipLaunchKernelGGL((render_kernel<false, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
                        c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, out,
                        c->d_counters);
 }
 
-template <int MAXS>
-void launch_render(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                   uint8_t *out) {
-  if (c->cull) {
-    if (c->wg_waves == 4) launch_render3<MAXS, true, 4>(c, lds_geo, lds, cam, W, H, depth, rows, out);
-    else launch_render3<MAXS, true, 1>(c, lds_geo, lds, cam, W, H, depth, rows, out);
-  } else {
-    if (c->wg_waves == 4) launch_render3<MAXS, false, 4>(c, lds_geo, lds, cam, W, H, depth, rows, out);
-    else launch_render3<MAXS, false, 1>(c, lds_geo, lds, cam, W, H, depth, rows, out);
+template <bool kLds, bool kCull, int kWaves>
+int launch_persist3(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows, uint8_t *out) {
+  const BvhArgs bv = bvh_args(c, cam);
+  const LgArgs lg = lg_args(c);
+  D3 amb{c->amb[0], c->amb[1], c->amb[2]};
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_persist<kLds, kCull, kWaves>, 64 * kWaves, lds) !=
+          hipSuccess ||
+      nb < 1)
+    nb = 1;
+  const int ntx = (W + 7) / 8, nty = (rows.count + 7) / 8;
+  const long long ntiles = (long long)ntx * nty;
+  if (ntiles > (1LL << 31) - 1) return RT_ERR_INVALID_ARG;
+  const long long want = (ntiles + kWaves - 1) / kWaves;
+  const int grid = (int)std::max(1LL, std::min(want, (long long)c->n_cu * nb));
+  const size_t levels = depth > 1 ? (size_t)depth - 1 : 1;
+  const size_t need = (size_t)grid * kWaves * levels * 64 * sizeof(StackEnt) + kTileShards * 64 * sizeof(unsigned);
+  if (c->stack_bytes < need) {
+    RT_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->stack_buf) (void)hipFree(c->stack_buf);
+    c->stack_buf = nullptr;
+    c->stack_bytes = 0;
+    RT_TRY(c, hipMalloc(&c->stack_buf, need));
+    c->stack_bytes = need;
   }
+  unsigned *ctr = reinterpret_cast<unsigned *>(c->stack_buf);
+  StackEnt *gstack = reinterpret_cast<StackEnt *>(c->stack_buf + kTileShards * 64 * sizeof(unsigned));
+  RT_TRY(c, hipMemsetAsync(ctr, 0, kTileShards * 64 * sizeof(unsigned), c->stream));
+  hipLaunchKernelGGL((render_persist<kLds, kCull, kWaves>), dim3(grid), dim3(64 * kWaves), lds, c->stream, c->d_geo,
+                     c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, out,
+                     c->d_counters, gstack, ctr, ntx, (int)ntiles);
+  return RT_OK;
+}
+
+int launch_render(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
+                  uint8_t *out) {
+  if (c->persist || depth - 1 > kMaxLdsStack) {
+    if (lds_geo)
+      return c->cull ? launch_persist3<true, true, 4>(c, lds, cam, W, H, depth, rows, out)
+                     : launch_persist3<true, false, 4>(c, lds, cam, W, H, depth, rows, out);
+    return c->cull ? launch_persist3<false, true, 4>(c, lds, cam, W, H, depth, rows, out)
+                   : launch_persist3<false, false, 4>(c, lds, cam, W, H, depth, rows, out);
+  }
+  if (c->cull) {
+    if (c->wg_waves == 4) launch_tiles<true, 4>(c, lds_geo, lds, cam, W, H, depth, rows, out);
+    else launch_tiles<true, 1>(c, lds_geo, lds, cam, W, H, depth, rows, out);
+  } else {
+    if (c->wg_waves == 4) launch_tiles<false, 4>(c, lds_geo, lds, cam, W, H, depth, rows, out);
+    else launch_tiles<false, 1>(c, lds_geo, lds, cam, W, H, depth, rows, out);
+  }
+  return RT_OK;
 }
 
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -574,10 +690,8 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
       int rc = launch_wavefront(c, cam, W, H, depth, r, dst, lds_geo, lds);
       if (rc != RT_OK) return rc;
     } else {
-      int stack = depth - 1;
-      if (stack <= 4) launch_render<4>(c, lds_geo, lds, cam, W, H, depth, r, dst);
-      else if (stack <= 16) launch_render<16>(c, lds_geo, lds, cam, W, H, depth, r, dst);
-      else launch_render<RT_MAX_DEPTH>(c, lds_geo, lds, cam, W, H, depth, r, dst);
+      int rc = launch_render(c, lds_geo, lds, cam, W, H, depth, r, dst);
+      if (rc != RT_OK) return rc;
     }
     RT_TRY(c, hipGetLastError());
   }
@@ -615,6 +729,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH_ALWAYS")) c->bvh_always = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_GROUPS")) c->bvh_groups = std::max(1, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID")) c->lg_on = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_PERSIST")) c->persist = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n = std::max(1, std::min(256, std::atoi(e)));
   auto bail = [&](int rc) {
@@ -649,6 +764,7 @@ void rt_destroy(rt_ctx *c) {
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->d_tmp) (void)hipFree(c->d_tmp);
   if (c->wf_buf) (void)hipFree(c->wf_buf);
+  if (c->stack_buf) (void)hipFree(c->stack_buf);
   for (int i = 0; i < rt_ctx::kRing; i++) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
