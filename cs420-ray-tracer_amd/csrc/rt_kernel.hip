@@ -366,6 +366,8 @@ __global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__rest
 
 using namespace rtk;
 
+constexpr int kBvhAlwaysAbove = 1024;
+
 struct rt_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -381,12 +383,15 @@ struct rt_ctx {
   int bvh_nodes = 0;
   // per-light direction grids for shadow rays (rt_lightgrid.h), built at upload
   int32_t *d_lg_start = nullptr, *d_lg_ids = nullptr;
-  int lg_n = 64, lg_on = 1;
+  int lg_n = 128, lg_on = 1;
   double lg_max_off = 0.0;
   double c0[3] = {0, 0, 0};
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
   double rmax = 0;
-  int bvh_min = 24, bvh_always = 0, bvh_on = 1, bvh_groups = 2, bvh_leaf = 4;
+  int bvh_min = 24, bvh_on = 1, bvh_groups = 2, bvh_leaf = 4;
+  // -1 (auto): every group walks the BVH when the scene has more than
+  // kBvhAlwaysAbove spheres (a linear cull sweep is O(n) per group)
+  int bvh_always = -1;
   int wg_waves = 4;  // megakernel waves per workgroup (tuning knob RT_HIP_WG_WAVES = 1 | 4)
   int pipeline = 0;  // 0 = megakernel (default), 1 = wavefront queues (knob RT_HIP_PIPELINE)
   int n_cu = 256;
@@ -471,7 +476,7 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   b.pmargin = 4.0f * b.margin;
   if (!std::isfinite(b.diam)) b.diam = INFINITY;
   b.min_cands = c->bvh_min;
-  b.always = c->bvh_always;
+  b.always = c->bvh_always >= 0 ? c->bvh_always : (c->nsph > kBvhAlwaysAbove ? 1 : 0);
   b.max_groups = c->bvh_groups;
   return b;
 }

@@ -35,7 +35,7 @@ double angle(const Dir &u, const Dir &v) {  // robust for small angles
 // geodesically convex and the distance to a point is convex on it).
 struct Patch {
   Dir c;
-  double rad;
+  double rad, cb, sb;  // cos / sin of (rad + kLgSlack)
 };
 Patch make_patch(int face, int N, int i0, int i1, int j0, int j1) {
   const double a0 = -1.0 + 2.0 * i0 / N, a1 = -1.0 + 2.0 * i1 / N;
@@ -44,7 +44,17 @@ Patch make_patch(int face, int N, int i0, int i1, int j0, int j1) {
   p.c = face_dir(face, 0.5 * (a0 + a1), 0.5 * (b0 + b1));
   p.rad = std::max(std::max(angle(p.c, face_dir(face, a0, b0)), angle(p.c, face_dir(face, a1, b0))),
                    std::max(angle(p.c, face_dir(face, a0, b1)), angle(p.c, face_dir(face, a1, b1))));
+  p.cb = std::cos(p.rad + kLgSlack);
+  p.sb = std::sin(p.rad + kLgSlack);
   return p;
+}
+
+// angle(v, patch centre) <= alpha + rad + slack, with ca/sa = cos/sin(alpha):
+// dot(v, c) >= cos(alpha + beta) = ca cb - sa sb (alpha + beta < pi), the
+// threshold lowered by 1e-12 so rounding can only add cells.
+inline bool meets(const Dir &v, double ca, double sa, double alpha, const Patch &p) {
+  if (alpha + p.rad + kLgSlack >= 3.14159) return true;
+  return v.x * p.c.x + v.y * p.c.y + v.z * p.c.z >= ca * p.cb - sa * p.sb - 1e-12;
 }
 
 }  // namespace
@@ -67,6 +77,8 @@ void build_light_grid(const double *cx, const double *cy, const double *cz, cons
       for (int ti = 0; ti < NT; ti++)
         tilep[(size_t)(f * NT + tj) * NT + ti] =
             make_patch(f, N, ti * kT, std::min(N, ti * kT + kT), tj * kT, std::min(N, tj * kT + kT));
+  Patch facep[6];
+  for (int f = 0; f < 6; f++) facep[f] = make_patch(f, N, 0, N, 0, N);
   const double dm = std::isfinite(diam) ? diam : 0.0;
   std::vector<std::vector<int32_t>> lists((size_t)cells);
   std::vector<int32_t> global;
@@ -84,17 +96,19 @@ void build_light_grid(const double *cx, const double *cy, const double *cz, cons
       }
       const Dir v{vx / D, vy / D, vz / D};
       const double alpha = std::asin(R / D) + kLgSlack;
-      for (int f = 0; f < 6; f++)
+      const double ca = std::cos(alpha), sa = std::sin(alpha);
+      for (int f = 0; f < 6; f++) {
+        if (!meets(v, ca, sa, alpha, facep[f])) continue;
         for (int tj = 0; tj < NT; tj++)
           for (int ti = 0; ti < NT; ti++) {
-            const Patch &tp = tilep[(size_t)(f * NT + tj) * NT + ti];
-            if (angle(v, tp.c) > alpha + tp.rad + kLgSlack) continue;
+            if (!meets(v, ca, sa, alpha, tilep[(size_t)(f * NT + tj) * NT + ti])) continue;
             for (int j = tj * kT; j < std::min(N, tj * kT + kT); j++)
               for (int i = ti * kT; i < std::min(N, ti * kT + kT); i++) {
                 const size_t c = (size_t)(f * N + j) * N + i;
-                if (angle(v, cellp[c].c) <= alpha + cellp[c].rad + kLgSlack) lists[c].push_back(s);
+                if (meets(v, ca, sa, alpha, cellp[c])) lists[c].push_back(s);
               }
           }
+      }
     }
     int32_t *st = start.data() + stride * (size_t)l;
     for (int c = 0; c < cells; c++) {

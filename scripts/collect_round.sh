@@ -1,0 +1,22 @@
+#!/bin/bash
+# Copy a gpu_round_profile.sh result into profiles/$TAG and fold the PMC passes
+# into profiles/pmc_traffic.json.  Usage: TAG=r1_final bash scripts/collect_round.sh
+set -e
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+TAG="${TAG:-r1}"
+SRC="$ROOT/gpurun_out/round_$TAG"
+DST="$ROOT/profiles/$TAG"
+mkdir -p "$DST"
+cp "$SRC/bench.json" "$SRC/pytest_gpu.log" "$DST/"
+cp "$SRC"/trace/run_kernel_stats.csv "$DST/kernel_stats.csv"
+python3 "$ROOT/scripts/prof_summary.py" "$SRC/trace/run_kernel_trace.csv" --labels synth200 > "$DST/trace_summary.json"
+cp "$SRC/trace_bench.json" "$DST/trace_bench.json"
+for d in "$SRC"/pmc_*; do
+  w=$(basename "$d"); w=${w#pmc_}
+  mkdir -p "$DST/pmc/$w"
+  for p in "$d"/p*/; do
+    mkdir -p "$DST/pmc/$w/$(basename "$p")"
+    cp "$p"/run_counter_collection.csv "$DST/pmc/$w/$(basename "$p")/"
+  done
+  python3 "$ROOT/scripts/make_pmc_json.py" "$w" "$DST/pmc/$w"
+done

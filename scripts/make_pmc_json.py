@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Fold gpu_pmc.sh counter passes into profiles/pmc_traffic.json (read by bench.py).
+
+  python scripts/make_pmc_json.py WORKLOAD PMC_DIR [KERNEL_SUBSTR]
+
+Per render launch (mean over the profiled launches):
+  hbm_bytes_per_launch = (FETCH_SIZE + WRITE_SIZE) * 1024  (rocprofv3 reports KiB;
+      the gfx950 x2 FETCH_SIZE correction of MI355X_MICROARCH.md applies to wide
+      16-B/lane streaming reads, which this kernel does not issue, so the raw
+      value is used; fetch and write are also listed separately)
+  valu_busy = SQ_ACTIVE_INST_VALU * 4 / (SIMDs * GRBM_GUI_ACTIVE / XCDs)
+  fp64_flops_per_launch = 64 * (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions
+      (an upper bound: it assumes every lane of the wave is active)
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+SIMDS, XCDS = 1024, 8
+
+
+def main():
+    workload, base = sys.argv[1], sys.argv[2]
+    kern = sys.argv[3] if len(sys.argv) > 3 else "render_"
+    vals = {}
+    for f in sorted(glob.glob(f"{base}/p*/run_counter_collection.csv")):
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            if kern in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, v in agg.items():
+            vals[k] = sum(v) / len(v)
+    out = {}
+    if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
+        out["fetch_bytes"] = round(vals["FETCH_SIZE"] * 1024)
+        out["write_bytes"] = round(vals["WRITE_SIZE"] * 1024)
+        out["hbm_bytes_per_launch"] = out["fetch_bytes"] + out["write_bytes"]
+    if "SQ_ACTIVE_INST_VALU" in vals and "GRBM_GUI_ACTIVE" in vals:
+        cycles = vals["GRBM_GUI_ACTIVE"] / XCDS
+        out["kernel_cycles"] = round(cycles)
+        out["valu_busy"] = round(vals["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cycles), 4)
+    f64 = [vals.get("SQ_INSTS_VALU_%s_F64" % k) for k in ("ADD", "MUL", "FMA", "TRANS")]
+    if None not in f64:
+        out["fp64_flops_per_launch"] = round(64 * (f64[0] + f64[1] + 2 * f64[2] + f64[3]))
+        out["valu_insts_per_launch"] = round(vals.get("SQ_INSTS_VALU", 0))
+    out["source"] = os.path.relpath(base, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    out["counters"] = {k: round(v, 1) for k, v in sorted(vals.items())}
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+    data = json.load(open(path)) if os.path.exists(path) else {}
+    data[workload] = out
+    with open(path, "w") as fh:
+        json.dump(data, fh, indent=1, sort_keys=True)
+    print(json.dumps({workload: {k: v for k, v in out.items() if k != "counters"}}))
+
+
+if __name__ == "__main__":
+    main()

@@ -21,7 +21,7 @@ def main():
     runs = []
     for r in rows:
         name = r["Kernel_Name"]
-        if "render_kernel" not in name:
+        if "render_" not in name:
             continue
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         key = (name, r["Grid_Size_X"], r["Grid_Size_Y"], r["LDS_Block_Size"])
