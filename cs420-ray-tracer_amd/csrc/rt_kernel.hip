@@ -45,39 +45,23 @@ __device__ unsigned long long g_timeline[kTimelineWaves * kTl];
 
 constexpr int kMaxLdsStack = 4;  // levels of the LDS reflection stack (render_kernel)
 
-// One 8x8 tile, one lane per pixel; the whole wave walks the reflection
-// levels together (uniform control flow around every sweep, lanes masked by
-// `alive`/`hit`).  `stk` is this wave's reflection stack, [level][lane]
-// (depth - 1 levels).  Adds the tile's ray counts to the wave sums.
+// trace_ray (src/main.cpp:16-58) for one camera ray per lane: the whole wave
+// walks the reflection levels together (uniform control flow around every
+// sweep, lanes masked by `alive`/`hit`).  `stk` is this wave's reflection
+// stack, [level][lane] (depth - 1 levels).  Returns the lane's colour.
 template <bool kCull>
-__device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const double *__restrict__ rad,
-                                           const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
-                                           int nl, D3 amb, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                                           const BvhArgs &bv, const LgArgs &lg, uint8_t *__restrict__ out, int x0,
-                                           int k0, StackEnt *stk, Work &work, unsigned long long (&sums)[4]) {
+__device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                         const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
+                                         int nl, D3 amb, int depth, const BvhArgs &bv, const LgArgs &lg, bool live,
+                                         D3 o, D3 d, StackEnt *stk, Work &work, unsigned &c_prim, unsigned &c_shadow,
+                                         unsigned &c_reflect) {
   const int lane = threadIdx.x & 63;
-  const int x = x0 + (lane & 7);
-  const int k = k0 + (lane >> 3);
-  const bool in_tile = x < W && k < rows.count;
-  const long long y = (long long)(k / rows.band) * rows.band * rows.stride + (long long)rows.first * rows.band +
-                      (k % rows.band);
-  const bool in_img = in_tile && y < H;
-
-  // Camera ray, camera.h:17-25 and main.cpp:151-154: ((u-0.5)*scale)*aspect, aspect = 1.0.
-  const int j = H - 1 - (int)(in_img ? y : 0);  // reference row (main.cpp:74)
-  const double u = (double)x / (W - 1), v = (double)j / (H - 1);
-  const double su = ((u - 0.5) * cam.scale) * 1.0, sv = (v - 0.5) * cam.scale;
-  D3 dir = add(add(mk(cam.fx, cam.fy, cam.fz), scale(mk(cam.rx, cam.ry, cam.rz), su)),
-               scale(mk(cam.ux, cam.uy, cam.uz), sv));
-  D3 d = normalized(normalized(dir));  // get_ray normalises, Ray() normalises again
-  D3 o = mk(cam.px, cam.py, cam.pz);
-  int key = -1;  // sphere the current ray leaves (-1: camera), groups lanes in sweeps
-
   int lev = 0;
   int dleft = depth;
   D3 res = mk(0.0, 0.0, 0.0);     // depth <= 0 -> black (main.cpp:17-18)
-  bool alive = in_img && depth >= 1;
-  unsigned c_prim = alive ? 1u : 0u, c_shadow = 0, c_reflect = 0, c_neg = 0;
+  bool alive = live && depth >= 1;
+  int key = -1;  // sphere the current ray leaves (-1: camera), groups lanes in sweeps
+  c_prim += alive ? 1u : 0u;
 
   while (__ballot(alive)) {
     double bt;
@@ -181,16 +165,80 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
     const StackEnt e = stk[lev * 64 + lane];
     res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
   }
+  return res;
+}
+
+// Output of a launch.  RT_FB_RGB8 with full = 0: rows.count x W RGB8 (the
+// rows of `rows`, rt_render); RT_FB_RGB8 with full = 1: a W x H RGB8 image in
+// PPM row order; RT_FB_F32X3 / RT_FB_F64X3: the reference's framebuffer,
+// index j*W + x with j = 0 the bottom row (src/main.cpp:156, kernel.cu:112),
+// unquantised.  Pixels x0 <= x < x0 + xw are written.
+struct OutDesc {
+  void *ptr;
+  int fmt, full, x0, xw;
+};
+
+// One 8x8 tile of pixels, one lane per pixel; `samples` = 1 (the serial
+// path) or 4 (main_gpu.cu:249-333's antialias offsets, in fp64 serial
+// semantics: samples summed in order, then * 0.25).  Adds the tile's ray
+// counts to the wave sums.
+template <bool kCull>
+__device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                           const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
+                                           int nl, D3 amb, const Cam &cam, int W, int H, int depth, const Rows &rows,
+                                           const BvhArgs &bv, const LgArgs &lg, const OutDesc &od, int samples,
+                                           int x0, int k0, StackEnt *stk, Work &work,
+                                           unsigned long long (&sums)[4]) {
+  const int lane = threadIdx.x & 63;
+  const int x = x0 + (lane & 7);
+  const int k = k0 + (lane >> 3);
+  const bool in_tile = x < W && x < od.x0 + od.xw && k < rows.count;
+  const long long y = (long long)(k / rows.band) * rows.band * rows.stride + (long long)rows.first * rows.band +
+                      (k % rows.band);
+  const bool in_img = in_tile && y < H;
+  const int j = H - 1 - (int)(in_img ? y : 0);  // reference row (main.cpp:74)
+  unsigned c_prim = 0, c_shadow = 0, c_reflect = 0, c_neg = 0;
+  D3 acc = mk(0.0, 0.0, 0.0);
+  for (int s = 0; s < samples; ++s) {
+    // Camera ray, camera.h:17-25 and main.cpp:151-154: ((u-0.5)*scale)*aspect,
+    // aspect = 1.0; antialias offsets main_gpu.cu:253-256 (x + 0.0 == x exactly)
+    const double ox = (double)(s & 1) * 0.5, oy = s >= 2 ? 0.5 : 0.0;
+    const double u = ((double)x + ox) / (W - 1), v = ((double)j + oy) / (H - 1);
+    const double su = ((u - 0.5) * cam.scale) * 1.0, sv = (v - 0.5) * cam.scale;
+    const D3 dir = add(add(mk(cam.fx, cam.fy, cam.fz), scale(mk(cam.rx, cam.ry, cam.rz), su)),
+                       scale(mk(cam.ux, cam.uy, cam.uz), sv));
+    const D3 d = normalized(normalized(dir));  // get_ray normalises, Ray() normalises again
+    const D3 o = mk(cam.px, cam.py, cam.pz);
+    const D3 c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk, work, c_prim,
+                                   c_shadow, c_reflect);
+    acc = add(acc, c);  // from 0, in sample order (main_gpu.cu:250, 327)
+  }
+  const D3 res = samples == 4 ? scale(acc, 0.25) : acc;  // main_gpu.cu:331, 1/4 is exact
   if (in_tile) {
-    uint8_t *px = out + ((size_t)k * W + x) * 3;
-    if (in_img) {
-      const int q0 = quantize(res.x), q1 = quantize(res.y), q2 = quantize(res.z);
-      c_neg = (q0 < 0) + (q1 < 0) + (q2 < 0);
-      px[0] = (uint8_t)(q0 < 0 ? 0 : q0);
-      px[1] = (uint8_t)(q1 < 0 ? 0 : q1);
-      px[2] = (uint8_t)(q2 < 0 ? 0 : q2);
-    } else {
-      px[0] = px[1] = px[2] = 0;
+    if (od.fmt == RT_FB_RGB8) {
+      uint8_t *px = static_cast<uint8_t *>(od.ptr) + ((size_t)(od.full ? y : k) * W + x) * 3;
+      if (in_img) {
+        const int q0 = quantize(res.x), q1 = quantize(res.y), q2 = quantize(res.z);
+        c_neg = (q0 < 0) + (q1 < 0) + (q2 < 0);
+        px[0] = (uint8_t)(q0 < 0 ? 0 : q0);
+        px[1] = (uint8_t)(q1 < 0 ? 0 : q1);
+        px[2] = (uint8_t)(q2 < 0 ? 0 : q2);
+      } else if (!od.full) {
+        px[0] = px[1] = px[2] = 0;
+      }
+    } else if (in_img) {
+      const size_t i = ((size_t)j * W + x) * 3;
+      if (od.fmt == RT_FB_F64X3) {
+        double *f = static_cast<double *>(od.ptr) + i;
+        f[0] = res.x;
+        f[1] = res.y;
+        f[2] = res.z;
+      } else {
+        float *f = static_cast<float *>(od.ptr) + i;
+        f[0] = (float)res.x;
+        f[1] = (float)res.y;
+        f[2] = (float)res.z;
+      }
     }
   }
   sums[0] += wave_sum(c_prim);
@@ -261,7 +309,7 @@ template <bool kLdsGeo, bool kCull, int kWaves>
 __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kernel(
     const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
     const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
-    BvhArgs bv_in, LgArgs lg, uint8_t *__restrict__ out, unsigned long long *__restrict__ counters) {
+    BvhArgs bv_in, LgArgs lg, OutDesc od, int samples, unsigned long long *__restrict__ counters) {
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
   const SphGeo *g;
   const double *rad;
@@ -278,9 +326,9 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
 #ifdef RT_STAMPS
   const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  trace_tile<kCull>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, out,
-                    blockIdx.x * (8 * kWx) + (wave % kWx) * 8, blockIdx.y * (8 * (kWaves / kWx)) + (wave / kWx) * 8,
-                    stk, work, sums);
+  trace_tile<kCull>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od, samples,
+                    od.x0 + blockIdx.x * (8 * kWx) + (wave % kWx) * 8,
+                    blockIdx.y * (8 * (kWaves / kWx)) + (wave / kWx) * 8, stk, work, sums);
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
   record_timeline((blockIdx.x + blockIdx.y * gridDim.x) * kWaves + wave, t_real0, work);
@@ -301,7 +349,7 @@ template <bool kLdsGeo, bool kCull, int kWaves>
 __global__ __launch_bounds__(64 * kWaves, RT_PERSIST_WAVES_PER_EU) void render_persist(
     const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
     const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
-    BvhArgs bv_in, LgArgs lg, uint8_t *__restrict__ out, unsigned long long *__restrict__ counters,
+    BvhArgs bv_in, LgArgs lg, OutDesc od, int samples, unsigned long long *__restrict__ counters,
     StackEnt *__restrict__ gstack, unsigned *__restrict__ tile_ctr, int ntx, int ntiles) {
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
   const SphGeo *g;
@@ -339,8 +387,8 @@ __global__ __launch_bounds__(64 * kWaves, RT_PERSIST_WAVES_PER_EU) void render_p
     }
     pending = fetch(shard);
     const int ty = (int)(tile / ntx), tx = (int)(tile % ntx);
-    trace_tile<kCull>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, out, tx * 8, ty * 8, stk,
-                      work, sums);
+    trace_tile<kCull>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od, samples,
+                      od.x0 + tx * 8, ty * 8, stk, work, sums);
   }
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
@@ -414,6 +462,7 @@ struct rt_ctx {
   // persistent megakernel: tile counters + per-wave reflection stacks (grown on demand)
   unsigned char *stack_buf = nullptr;
   size_t stack_bytes = 0;
+  int samples = 1;  // 4: the antialias mode (rt_set_antialias)
   int persist = 0;  // RT_HIP_PERSIST=1: persistent megakernel for every depth (always used above depth 5)
   std::string err;
 };
@@ -493,25 +542,26 @@ LgArgs lg_args(const rt_ctx *c) {
 
 template <bool kCull, int kWaves>
 void launch_tiles(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                  uint8_t *out) {
+                  const OutDesc &od) {
   const BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
   constexpr int kWx = kWaves == 4 ? 2 : 1, kWy = kWaves / kWx;
-  dim3 grid((W + 8 * kWx - 1) / (8 * kWx), (rows.count + 8 * kWy - 1) / (8 * kWy));
+  dim3 grid((od.xw + 8 * kWx - 1) / (8 * kWx), (rows.count + 8 * kWy - 1) / (8 * kWy));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   lds = ((lds + 31) & ~(size_t)31) + (size_t)kWaves * 64 * kMaxLdsStack * sizeof(StackEnt);
   if (lds_geo)
     hipLaunchKernelGGL((render_kernel<true, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, out,
-                       c->d_counters);
+                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, od,
+                       c->samples, c->d_counters);
   else
     hipLaunchKernelGGL((render_kernel<false, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, out,
-                       c->d_counters);
+                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, od,
+                       c->samples, c->d_counters);
 }
 
 template <bool kLds, bool kCull, int kWaves>
-int launch_persist3(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows, uint8_t *out) {
+int launch_persist3(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
+                    const OutDesc &od) {
   const BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
@@ -520,7 +570,7 @@ int launch_persist3(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dep
           hipSuccess ||
       nb < 1)
     nb = 1;
-  const int ntx = (W + 7) / 8, nty = (rows.count + 7) / 8;
+  const int ntx = (od.xw + 7) / 8, nty = (rows.count + 7) / 8;
   const long long ntiles = (long long)ntx * nty;
   if (ntiles > (1LL << 31) - 1) return RT_ERR_INVALID_ARG;
   const long long want = (ntiles + kWaves - 1) / kWaves;
@@ -539,13 +589,13 @@ int launch_persist3(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dep
   StackEnt *gstack = reinterpret_cast<StackEnt *>(c->stack_buf + kTileShards * 64 * sizeof(unsigned));
   RT_TRY(c, hipMemsetAsync(ctr, 0, kTileShards * 64 * sizeof(unsigned), c->stream));
   hipLaunchKernelGGL((render_persist<kLds, kCull, kWaves>), dim3(grid), dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                     c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, out,
-                     c->d_counters, gstack, ctr, ntx, (int)ntiles);
+                     c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, od,
+                     c->samples, c->d_counters, gstack, ctr, ntx, (int)ntiles);
   return RT_OK;
 }
 
 int launch_render(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                  uint8_t *out) {
+                  const OutDesc &out) {
   if (c->persist || depth - 1 > kMaxLdsStack) {
     if (lds_geo)
       return c->cull ? launch_persist3<true, true, 4>(c, lds, cam, W, H, depth, rows, out)
@@ -673,7 +723,7 @@ int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_
   return RT_OK;
 }
 
-int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows &r, uint8_t *dst) {
+int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows &r, const OutDesc &od) {
   RT_TRY(c, hipSetDevice(c->device));
   RT_TRY(c, hipMemsetAsync(c->d_counters, 0, kShards * kShardStride * sizeof(unsigned long long), c->stream));
   const int slot = (int)(c->launches % rt_ctx::kRing);
@@ -690,12 +740,13 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
       c->err = "light list does not fit in LDS";
       return RT_ERR_INVALID_ARG;
     }
-    if (c->pipeline >= 1) {
+    // the queue pipelines write row-compact RGB8 of single-sample renders only
+    if (c->pipeline >= 1 && od.fmt == RT_FB_RGB8 && !od.full && od.x0 == 0 && od.xw == W && c->samples == 1) {
       if ((long long)r.count * W > (1LL << 31) - 1) return RT_ERR_INVALID_ARG;
-      int rc = launch_wavefront(c, cam, W, H, depth, r, dst, lds_geo, lds);
+      int rc = launch_wavefront(c, cam, W, H, depth, r, static_cast<uint8_t *>(od.ptr), lds_geo, lds);
       if (rc != RT_OK) return rc;
     } else {
-      int rc = launch_render(c, lds_geo, lds, cam, W, H, depth, r, dst);
+      int rc = launch_render(c, lds_geo, lds, cam, W, H, depth, r, od);
       if (rc != RT_OK) return rc;
     }
     RT_TRY(c, hipGetLastError());
@@ -935,7 +986,7 @@ int rt_render_async(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, co
   Rows r;
   int rc = validate(c, cam, W, H, depth, rows, out, r);
   if (rc != RT_OK) return rc;
-  return enqueue(c, cam, W, H, depth, r, out);
+  return enqueue(c, cam, W, H, depth, r, OutDesc{out, RT_FB_RGB8, 0, 0, W});
 }
 
 int rt_render_stats(rt_ctx *c, rt_stats *st) {
@@ -1006,12 +1057,34 @@ int rt_render(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt
     }
     dst = c->d_tmp;
   }
-  rc = enqueue(c, cam, W, H, depth, r, dst);
+  rc = enqueue(c, cam, W, H, depth, r, OutDesc{dst, RT_FB_RGB8, 0, 0, W});
   if (rc != RT_OK) return rc;
   if (!out_on_device && bytes) RT_TRY(c, hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, c->stream));
   rt_stats tmp;
   rc = rt_render_stats(c, st ? st : &tmp);
   return rc;
+}
+
+int rt_set_antialias(rt_ctx *c, int samples) {
+  if (!c || (samples != 1 && samples != 4)) return RT_ERR_INVALID_ARG;
+  c->samples = samples;
+  return RT_OK;
+}
+
+int rt_render_tile(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, int tile_x, int tile_y, int tile_w,
+                   int tile_h, int fb_format, void *fb_device) {
+  if (!c || !cam || !fb_device || W <= 0 || H <= 0 || tile_w < 0 || tile_h < 0 || tile_x < 0 || tile_y < 0)
+    return RT_ERR_INVALID_ARG;
+  if (fb_format != RT_FB_RGB8 && fb_format != RT_FB_F32X3 && fb_format != RT_FB_F64X3) return RT_ERR_INVALID_ARG;
+  if (!c->has_scene) return RT_ERR_NO_SCENE;
+  if (depth > RT_MAX_DEPTH) return RT_ERR_DEPTH;
+  // the reference kernel clips the tile to the image (kernel.cu:103)
+  const int xe = std::min(W, tile_x + tile_w), ye = std::min(H, tile_y + tile_h);
+  const int xw = std::max(0, xe - tile_x), th = std::max(0, ye - tile_y);
+  // framebuffer rows j = tile_y .. ye-1 (j = 0 the bottom row) are PPM rows H-ye .. H-1-tile_y
+  const Rows r{1, H - ye, 1, xw > 0 ? th : 0};
+  RT_TRY(c, hipSetDevice(c->device));
+  return enqueue(c, cam, W, H, depth, r, OutDesc{fb_device, fb_format, 1, tile_x, xw});
 }
 
 int rt_kernel_times(rt_ctx *c, double *ms_out, int max_n, int *n_out) {

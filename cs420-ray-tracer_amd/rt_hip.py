@@ -94,7 +94,13 @@ SIGNATURES = {
     "rt_render_stats": (C.c_int, [_P, C.POINTER(rt_stats)]),
     "rt_kernel_times": (C.c_int, [_P, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int)]),
     "rt_unpermute_rows": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "rt_render_tile": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.c_int, C.c_int, _P]),
+    "rt_set_antialias": (C.c_int, [_P, C.c_int]),
 }
+
+# framebuffer formats of rt_render_tile (rt_hip.h)
+RT_FB_RGB8, RT_FB_F32X3, RT_FB_F64X3 = 0, 1, 2
 
 _lib = None
 
@@ -244,6 +250,16 @@ class Renderer:
         _check(lib().rt_render_async(self._ctx, C.byref(cam), width, height, depth,
                                      C.byref(rows) if rows is not None else None, C.c_void_p(out_device_ptr)),
                "rt_render_async", self._ctx)
+
+    def set_antialias(self, samples: int):
+        """1 = the serial path, 4 = the reference GPU's `-a` mode (main_gpu.cu:249-333)."""
+        _check(lib().rt_set_antialias(self._ctx, samples), "rt_set_antialias", self._ctx)
+
+    def render_tile(self, cam: rt_camera, width: int, height: int, depth: int, tile_x: int, tile_y: int,
+                    tile_w: int, tile_h: int, fb_format: int, fb_device_ptr: int):
+        """launch_gpu_kernel tile semantics (kernel.cu:185-200) into a full-image device framebuffer."""
+        _check(lib().rt_render_tile(self._ctx, C.byref(cam), width, height, depth, tile_x, tile_y, tile_w, tile_h,
+                                    fb_format, C.c_void_p(fb_device_ptr)), "rt_render_tile", self._ctx)
 
     def stats(self) -> rt_stats:
         st = rt_stats()

@@ -18,6 +18,10 @@
  *   rt_write_ppm                    <- write_ppm()            src/main.cpp:69-91
  *   rt_kernel_times                 <- cudaEventElapsedTime around the kernel, src/main_gpu.cu:496-519
  *   rt_unpermute_rows               <- (new) reassembly of the multi-GPU row shards
+ *   rt_render_tile                  <- launch_gpu_kernel's tile semantics  src/kernel.cu:185-200 (x = tile_x + ...,
+ *                                      y = tile_y + ..., fb[y*W + x], kernel.cu:99-112), as main_hybrid.cpp:457-470
+ *                                      calls it; float3 / Vec3 / RGB8 framebuffers
+ *   rt_set_antialias                <- the `-a` flag of ray_gpu, src/main_gpu.cu:249-333, 363-370
  *
  * Errors: every call returns an rt_status (0 = ok); the library never exits
  * (the reference's CUDA_CHECK -> exit(1), src/main_gpu.cu:27-35, is not kept).
@@ -34,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 1
+#define RT_HIP_ABI_VERSION 2
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -161,6 +165,30 @@ int rt_render_stats(rt_ctx *ctx, rt_stats *stats);
  * the render launches issued since the previous call, oldest first, at most
  * max_n (and at most the 256 most recent).  Waits for the context stream. */
 int rt_kernel_times(rt_ctx *ctx, double *ms_out, int max_n, int *n_out);
+
+/* Framebuffer formats of rt_render_tile. */
+#define RT_FB_RGB8 0  /* uint8 RGB, width*height*3, PPM row order (top row first), quantised as write_ppm */
+#define RT_FB_F32X3 1 /* float RGB per pixel at index y*width + x, y = 0 the BOTTOM row: the reference's
+                         d_framebuffer of launch_gpu_kernel (kernel.cu:112), unquantised */
+#define RT_FB_F64X3 2 /* double RGB (Vec3) per pixel, same indexing: the serial framebuffer, main.cpp:156 */
+
+/* launch_gpu_kernel (src/kernel.cu:185-200) with its tile semantics: renders
+ * pixels x in [tile_x, tile_x + tile_w), y in [tile_y, tile_y + tile_h)
+ * (clipped to the image; y counts from the bottom row, v = y/(H-1)) into a
+ * full-image DEVICE framebuffer of the given format; other pixels are not
+ * touched.  Asynchronous on the context stream, like the reference; the
+ * caller synchronises (rt_render_stats waits and returns this tile's counts).
+ * The colours are the serial path's (fp64, A1-A13), not the reference CUDA
+ * kernel's fp32 approximation. */
+int rt_render_tile(rt_ctx *ctx, const rt_camera *cam, int image_width, int image_height, int depth, int tile_x,
+                   int tile_y, int tile_width, int tile_height, int fb_format, void *fb_device);
+
+/* Samples per pixel for later renders: 1 (default, the serial path) or 4 (the
+ * reference GPU's `-a` antialias mode, main_gpu.cu:249-333: offsets
+ * (0,0) (0.5,0) (0,0.5) (0.5,0.5) added to (x, y) before u = x/(W-1),
+ * v = y/(H-1); the 4 colours summed in that order and scaled by 1/4, all in
+ * the serial fp64 semantics).  Ray counts include every sample. */
+int rt_set_antialias(rt_ctx *ctx, int samples);
 
 /* Reassemble G shards gathered rank-major ([G][rows_per_rank][W][3], rank r
  * rendered with rt_rows{band, r, G, rows_per_rank}) into a PPM-ordered

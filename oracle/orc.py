@@ -65,6 +65,8 @@ def lib():
         L.orc_intersect.argtypes = [C.POINTER(orc_sphere), orc_vec3, orc_vec3, C.POINTER(C.c_double)]
         L.orc_render.argtypes = [C.POINTER(orc_scene), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.c_void_p, C.c_void_p, C.POINTER(orc_counts), C.c_int]
+        L.orc_render_aa.argtypes = [C.POINTER(orc_scene), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                    C.c_void_p, C.POINTER(orc_counts), C.c_int]
         L.orc_quantize.argtypes = [C.c_double]
         _lib = L
     return _lib
@@ -106,6 +108,22 @@ class OracleScene:
         dt = time.perf_counter() - t0
         if rc != 0:
             raise ValueError("orc_render rejected its arguments")
+        out = (bytes(rgb), cnt.as_dict(), dt)
+        return out + (list(fb),) if want_fb else out
+
+
+    def render_aa(self, W, H, depth, samples=4, threads=1, want_fb=False):
+        """Antialias mode (main_gpu.cu:249-333, serial fp64 semantics), full frame.
+        Returns (rgb bytes, counts dict, seconds[, fb doubles in PPM row order])."""
+        rgb = (C.c_uint8 * (H * W * 3))()
+        fb = (C.c_double * (H * W * 3))() if want_fb else None
+        cnt = orc_counts()
+        t0 = time.perf_counter()
+        rc = lib().orc_render_aa(C.byref(self.s), W, H, depth, samples, C.cast(rgb, C.c_void_p),
+                                 C.cast(fb, C.c_void_p) if fb is not None else None, C.byref(cnt), threads)
+        dt = time.perf_counter() - t0
+        if rc != 0:
+            raise ValueError("orc_render_aa rejected its arguments")
         out = (bytes(rgb), cnt.as_dict(), dt)
         return out + (list(fb),) if want_fb else out
 

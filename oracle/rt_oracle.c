@@ -222,6 +222,66 @@ int orc_render(const orc_scene *s, int W, int H, int depth, int band, int first,
     return 0;
 }
 
+/* The reference GPU's antialias mode (src/main_gpu.cu:249-333) restated in the
+ * serial fp64 semantics: sample s = 0..samples-1 offsets (x, j) by
+ * ((s % 2) * 0.5, s >= 2 ? 0.5 : 0) (main_gpu.cu:253-256), each sample is a
+ * full trace_ray, the colours are summed in sample order from 0
+ * (main_gpu.cu:249-327) and scaled by 1/samples (:331).  Full frame, PPM
+ * row order. */
+int orc_render_aa(const orc_scene *s, int W, int H, int depth, int samples, uint8_t *rgb, double *fb,
+                  orc_counts *counts, int nthreads) {
+    if (W <= 0 || H <= 0 || (samples != 1 && samples != 4)) return -1;
+    orc_camera cam;
+    orc_make_camera(s, &cam);
+    orc_counts total = {0, 0, 0, 0};
+    long long npx = (long long)H * W;
+    if (nthreads < 1) nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        orc_counts local = {0, 0, 0, 0};
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 64)
+#endif
+        for (long long p = 0; p < npx; p++) {
+            int y = (int)(p / W), i = (int)(p % W);
+            int j = H - 1 - y;
+            orc_vec3 acc = {0.0, 0.0, 0.0};
+            for (int smp = 0; smp < samples; smp++) {
+                double ox = (double)(smp % 2) * 0.5, oy = smp >= 2 ? 0.5 : 0.0;
+                double u = ((double)i + ox) / (W - 1);
+                double v = ((double)j + oy) / (H - 1);
+                orc_ray r = get_ray(&cam, u, v);
+                if (depth >= 1) local.primary++;
+                orc_vec3 c = trace_ray(s, &r, depth, &local);
+                acc.x = acc.x + c.x;
+                acc.y = acc.y + c.y;
+                acc.z = acc.z + c.z;
+            }
+            double inv = 1.0 / (double)samples;
+            double ch[3] = {acc.x * inv, acc.y * inv, acc.z * inv};
+            for (int q = 0; q < 3; q++) {
+                if (fb) fb[p * 3 + q] = ch[q];
+                int qv = orc_quantize(ch[q]);
+                if (qv < 0) { local.negative++; qv = 0; }
+                if (rgb) rgb[p * 3 + q] = (uint8_t)qv;
+            }
+        }
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        {
+            total.primary += local.primary;
+            total.shadow += local.shadow;
+            total.reflect += local.reflect;
+            total.negative += local.negative;
+        }
+    }
+    if (counts) *counts = total;
+    return 0;
+}
+
 /* ------------------------------------------------------- scene_loader.h */
 /* Emulates `std::istream >> double` (libstdc++ num_get): greedy accumulation of
  * [sign] digits [. digits] [e [sign] digits], then strtod over exactly that

@@ -92,6 +92,11 @@ int orc_render(const orc_scene *s, int W, int H, int depth,
                int band, int first, int stride, int row_count,
                uint8_t *rgb, double *fb, orc_counts *counts, int nthreads);
 
+/* Antialias mode of src/main_gpu.cu:249-333 in serial fp64 semantics: samples
+ * = 1 or 4, full frame in PPM row order (see rt_oracle.c). */
+int orc_render_aa(const orc_scene *s, int W, int H, int depth, int samples, uint8_t *rgb, double *fb,
+                  orc_counts *counts, int nthreads);
+
 /* Quantiser of main.cpp:85-87: int(255.99 * std::min(1.0, c)). */
 int orc_quantize(double c);
 

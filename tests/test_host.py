@@ -24,7 +24,7 @@ def header_functions():
 
 def test_library_exports_every_declared_symbol():
     names = header_functions()
-    assert len(names) >= 18
+    assert len(names) >= 20
     out = subprocess.check_output(["nm", "-D", "--defined-only", rt_hip.LIB_PATH], text=True)
     exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
     missing = [n for n in names if n not in exported]
@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     lib = rt_hip.lib()
     for n in names:
         getattr(lib, n)
-    assert lib.rt_abi_version() == 1
+    assert lib.rt_abi_version() == 2
 
 
 def test_error_strings():

@@ -117,3 +117,16 @@ def test_quantizer():
     assert orc.quantize(math.nan) == 255  # std::min(1.0, NaN) returns 1.0
     assert orc.quantize(-0.001) == 0      # truncation toward zero
     assert orc.quantize(-0.5) == -127     # no lower clamp upstream
+
+
+def test_oracle_antialias_single_sample_is_the_serial_path():
+    """orc_render_aa(samples=1) == orc_render; samples=4 renders 4x the primary rays
+    and averages in sample order (main_gpu.cu:249-333 restated in fp64)."""
+    import orc
+
+    o = orc.OracleScene(scene_path("complex"))
+    a, ca, _ = o.render(97, 61, 4, threads=2)
+    b, cb, _ = o.render_aa(97, 61, 4, samples=1, threads=2)
+    assert a == b and ca == cb
+    _, c4, _ = o.render_aa(9, 7, 3, samples=4, threads=1)
+    assert c4["primary"] == 4 * 9 * 7
