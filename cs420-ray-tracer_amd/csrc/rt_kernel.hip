@@ -211,7 +211,7 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
     const D3 o = mk(cam.px, cam.py, cam.pz);
     const D3 c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk, work, c_prim,
                                    c_shadow, c_reflect);
-    acc = add(acc, c);  // from 0, in sample order (main_gpu.cu:250, 327)
+    acc = samples == 1 ? c : add(acc, c);  // serial: the colour itself; AA: from 0 in sample order (main_gpu.cu:250, 327)
   }
   const D3 res = samples == 4 ? scale(acc, 0.25) : acc;  // main_gpu.cu:331, 1/4 is exact
   if (in_tile) {
