@@ -14,7 +14,8 @@
 // Extra options (defaults equal the reference's hard-coded values,
 // main.cpp:95-97): --width W --height H --depth D, --gpus G (rows sharded over
 // G devices in cyclic 8-row bands, gathered to device 0 with ncclGather over
-// xGMI), --device N, --out FILE, --p6 (binary PPM), --repeat N, --json.
+// xGMI), --device N, --out FILE, --p6 (binary PPM), --repeat N, --json, and
+// -a (4-sample antialias, the ray_cuda flag of src/main_gpu.cu:363-370).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -38,11 +39,12 @@ struct Opts {
   int gpus = 1, device = 0, repeat = 1;
   std::string out;
   bool p6 = false, json = false;
+  int samples = 1;
 };
 
 int usage(const char *argv0) {
   std::fprintf(stderr,
-               "usage: %s [--openmp] [--width W] [--height H] [--depth D] [--gpus G] [--device N]\n"
+               "usage: %s [--openmp] [-a] [--width W] [--height H] [--depth D] [--gpus G] [--device N]\n"
                "          [--out FILE] [--p6] [--repeat N] [--json] [scene.txt]\n",
                argv0);
   return 2;
@@ -84,6 +86,7 @@ int render_single(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::
   rt_ctx *ctx = nullptr;
   CK(rt_create(o.device, &ctx));
   CK(rt_upload_scene(ctx, &sc));
+  CK(rt_set_antialias(ctx, o.samples));
   rt_stats st{};
   for (int it = 0; it < o.repeat; it++) {
     auto t0 = std::chrono::high_resolution_clock::now();
@@ -114,6 +117,7 @@ int render_multi(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::v
     devs[g] = g;
     CK(rt_create(g, &ctx[g]));
     CK(rt_upload_scene(ctx[g], &sc));
+    CK(rt_set_antialias(ctx[g], o.samples));
     HK(hipSetDevice(g));
     HK(hipStreamCreateWithFlags(&streams[g], hipStreamNonBlocking));
     CK(rt_set_stream(ctx[g], streams[g]));
@@ -227,6 +231,7 @@ int main(int argc, char **argv) {
     else if (a == "--repeat") { if (!next(o.repeat)) return usage(argv[0]); }
     else if (a == "--out") { if (i + 1 >= argc) return usage(argv[0]); o.out = argv[++i]; }
     else if (a == "--p6") o.p6 = true;
+    else if (a == "-a") o.samples = 4;
     else if (a == "--json") o.json = true;
     else if (a == "-h" || a == "--help") return usage(argv[0]);
     else o.scene = a;  // any other argument is the scene path, as main.cpp:103-110
