@@ -91,10 +91,15 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
     // shading state is live across the shadow sweeps: (A) occlusion bits for
     // every light, (B) Phong terms in light order for the unoccluded ones.
     // Phase B recomputes to_light / ldir with the same operations (same bits).
-    for (int l0 = 0; l0 < nl; l0 += 64) {
-      const int lend = nl - l0 < 64 ? nl : l0 + 64;
-      unsigned long long occm = 0;
-      for (int l = l0; l < lend; ++l) {
+    // scene.h:94-120: per light in file order, the shadow query then (if lit)
+    // the Phong terms with the same ldir
+    {
+      const SphGeo sg = g[hi];
+      const SphMat m = mat[hi];
+      const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
+      const D3 view = normalized(sub(o, hp));                       // main.cpp:38
+      const D3 mc = mk(m.cr, m.cg, m.cb);
+      for (int l = 0; l < nl; ++l) {
         RT_T0(t_setup);
         const LightD L = slight[l];
         const D3 lp = mk(L.px, L.py, L.pz);
@@ -106,20 +111,9 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
         RT_T0(t_sh);
         const bool occ = lg.on ? shadow_cells(g, n, hit, so, sd, lp, dist, lg, l, work)
                                : sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, hi, dist, bv, work);
-        if (occ) occm |= 1ull << (l - l0);
         RT_ACC(work, 9, t_sh);
-      }
-      RT_T0(t_shade);
-      if (hit && occm != ~0ull >> (64 - (lend - l0))) {
-        const SphGeo sg = g[hi];
-        const SphMat m = mat[hi];
-        const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
-        const D3 view = normalized(sub(o, hp));                       // main.cpp:38
-        const D3 mc = mk(m.cr, m.cg, m.cb);
-        for (int l = l0; l < lend; ++l) {
-          if (occm >> (l - l0) & 1ull) continue;
-          const LightD L = slight[l];
-          const D3 ldir = normalized(sub(mk(L.px, L.py, L.pz), hp));
+        RT_T0(t_shade);
+        if (hit && !occ) {
           const double ndl = max0(dot(nrm, ldir));
           const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
           const D3 nl2 = scale(ldir, -1.0);
@@ -130,8 +124,8 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
           const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
           col = add(add(specular, diffuse), col);                  // scene.h:117
         }
+        RT_ACC(work, 4, t_shade);
       }
-      RT_ACC(work, 4, t_shade);
     }
     if (hit) {
       c_shadow += (unsigned)nl;
@@ -182,12 +176,11 @@ struct OutDesc {
 // path) or 4 (main_gpu.cu:249-333's antialias offsets, in fp64 serial
 // semantics: samples summed in order, then * 0.25).  Adds the tile's ray
 // counts to the wave sums.
-template <bool kCull>
+template <bool kCull, int kSamples>
 __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                            const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                            int nl, D3 amb, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                                           const BvhArgs &bv, const LgArgs &lg, const OutDesc &od, int samples,
-                                           int x0, int k0, StackEnt *stk, Work &work,
+                                           const BvhArgs &bv, const LgArgs &lg, const OutDesc &od, int x0, int k0, StackEnt *stk, Work &work,
                                            unsigned long long (&sums)[4]) {
   const int lane = threadIdx.x & 63;
   const int x = x0 + (lane & 7);
@@ -199,7 +192,8 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
   const int j = H - 1 - (int)(in_img ? y : 0);  // reference row (main.cpp:74)
   unsigned c_prim = 0, c_shadow = 0, c_reflect = 0, c_neg = 0;
   D3 acc = mk(0.0, 0.0, 0.0);
-  for (int s = 0; s < samples; ++s) {
+#pragma unroll 1
+  for (int s = 0; s < kSamples; ++s) {
     // Camera ray, camera.h:17-25 and main.cpp:151-154: ((u-0.5)*scale)*aspect,
     // aspect = 1.0; antialias offsets main_gpu.cu:253-256 (x + 0.0 == x exactly)
     const double ox = (double)(s & 1) * 0.5, oy = s >= 2 ? 0.5 : 0.0;
@@ -211,9 +205,9 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
     const D3 o = mk(cam.px, cam.py, cam.pz);
     const D3 c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk, work, c_prim,
                                    c_shadow, c_reflect);
-    acc = samples == 1 ? c : add(acc, c);  // serial: the colour itself; AA: from 0 in sample order (main_gpu.cu:250, 327)
+    acc = kSamples == 1 ? c : add(acc, c);  // serial: the colour itself; AA: from 0 in sample order (main_gpu.cu:250, 327)
   }
-  const D3 res = samples == 4 ? scale(acc, 0.25) : acc;  // main_gpu.cu:331, 1/4 is exact
+  const D3 res = kSamples == 4 ? scale(acc, 0.25) : acc;  // main_gpu.cu:331, 1/4 is exact
   if (in_tile) {
     if (od.fmt == RT_FB_RGB8) {
       uint8_t *px = static_cast<uint8_t *>(od.ptr) + ((size_t)(od.full ? y : k) * W + x) * 3;
@@ -301,15 +295,16 @@ __device__ __forceinline__ void record_timeline(unsigned wave_id, unsigned long 
 #endif
 
 #ifndef RT_MIN_WAVES_PER_EU
-#define RT_MIN_WAVES_PER_EU 1
+#define RT_MIN_WAVES_PER_EU 3  // caps VGPRs at 168: three waves per SIMD
 #endif
 // One wave per 8x8 tile (2x2 tiles per workgroup for kWaves = 4); the
 // reflection stack (depth <= 5) lives in LDS after the staged scene.
-template <bool kLdsGeo, bool kCull, int kWaves>
+constexpr int kWaves = 4;  // 2x2 tiles of 8x8 pixels per workgroup
+template <bool kLdsGeo, bool kCull, int kSamples>
 __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kernel(
     const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
     const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
-    BvhArgs bv_in, LgArgs lg, OutDesc od, int samples, unsigned long long *__restrict__ counters) {
+    BvhArgs bv_in, LgArgs lg, OutDesc od, unsigned long long *__restrict__ counters) {
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
   const SphGeo *g;
   const double *rad;
@@ -326,7 +321,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
 #ifdef RT_STAMPS
   const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  trace_tile<kCull>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od, samples,
+  trace_tile<kCull, kSamples>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
                     od.x0 + blockIdx.x * (8 * kWx) + (wave % kWx) * 8,
                     blockIdx.y * (8 * (kWaves / kWx)) + (wave / kWx) * 8, stk, work, sums);
   RT_ACC(work, 5, t_wave);
@@ -345,11 +340,11 @@ constexpr int kTileShards = 64;
 #ifndef RT_PERSIST_WAVES_PER_EU
 #define RT_PERSIST_WAVES_PER_EU 3
 #endif
-template <bool kLdsGeo, bool kCull, int kWaves>
+template <bool kLdsGeo, bool kCull, int kSamples>
 __global__ __launch_bounds__(64 * kWaves, RT_PERSIST_WAVES_PER_EU) void render_persist(
     const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
     const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
-    BvhArgs bv_in, LgArgs lg, OutDesc od, int samples, unsigned long long *__restrict__ counters,
+    BvhArgs bv_in, LgArgs lg, OutDesc od, unsigned long long *__restrict__ counters,
     StackEnt *__restrict__ gstack, unsigned *__restrict__ tile_ctr, int ntx, int ntiles) {
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
   const SphGeo *g;
@@ -387,7 +382,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_PERSIST_WAVES_PER_EU) void render_p
     }
     pending = fetch(shard);
     const int ty = (int)(tile / ntx), tx = (int)(tile % ntx);
-    trace_tile<kCull>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od, samples,
+    trace_tile<kCull, kSamples>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
                       od.x0 + tx * 8, ty * 8, stk, work, sums);
   }
   RT_ACC(work, 5, t_wave);
@@ -440,7 +435,6 @@ struct rt_ctx {
   // -1 (auto): every group walks the BVH when the scene has more than
   // kBvhAlwaysAbove spheres (a linear cull sweep is O(n) per group)
   int bvh_always = -1;
-  int wg_waves = 4;  // megakernel waves per workgroup (tuning knob RT_HIP_WG_WAVES = 1 | 4)
   int pipeline = 0;  // 0 = megakernel (default), 1 = wavefront queues (knob RT_HIP_PIPELINE)
   int n_cu = 256;
   // wavefront scratch: queues, per-pixel terminal colours / stack (grown on demand)
@@ -540,33 +534,27 @@ LgArgs lg_args(const rt_ctx *c) {
   return g;
 }
 
-template <bool kCull, int kWaves>
-void launch_tiles(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
+template <bool kLds, bool kCull, int kSamples>
+void launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
                   const OutDesc &od) {
   const BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
-  constexpr int kWx = kWaves == 4 ? 2 : 1, kWy = kWaves / kWx;
-  dim3 grid((od.xw + 8 * kWx - 1) / (8 * kWx), (rows.count + 8 * kWy - 1) / (8 * kWy));
+  dim3 grid((od.xw + 15) / 16, (rows.count + 15) / 16);
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   lds = ((lds + 31) & ~(size_t)31) + (size_t)kWaves * 64 * kMaxLdsStack * sizeof(StackEnt);
-  if (lds_geo)
-    hipLaunchKernelGGL((render_kernel<true, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, od,
-                       c->samples, c->d_counters);
-  else
-    hipLaunchKernelGGL((render_kernel<false, kCull, kWaves>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                       c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, od,
-                       c->samples, c->d_counters);
+  hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
+                     c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, od,
+                     c->d_counters);
 }
 
-template <bool kLds, bool kCull, int kWaves>
+template <bool kLds, bool kCull, int kSamples>
 int launch_persist3(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
                     const OutDesc &od) {
   const BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_persist<kLds, kCull, kWaves>, 64 * kWaves, lds) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_persist<kLds, kCull, kSamples>, 64 * kWaves, lds) !=
           hipSuccess ||
       nb < 1)
     nb = 1;
@@ -588,29 +576,34 @@ int launch_persist3(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dep
   unsigned *ctr = reinterpret_cast<unsigned *>(c->stack_buf);
   StackEnt *gstack = reinterpret_cast<StackEnt *>(c->stack_buf + kTileShards * 64 * sizeof(unsigned));
   RT_TRY(c, hipMemsetAsync(ctr, 0, kTileShards * 64 * sizeof(unsigned), c->stream));
-  hipLaunchKernelGGL((render_persist<kLds, kCull, kWaves>), dim3(grid), dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                     c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, od,
-                     c->samples, c->d_counters, gstack, ctr, ntx, (int)ntiles);
+  hipLaunchKernelGGL((render_persist<kLds, kCull, kSamples>), dim3(grid), dim3(64 * kWaves), lds, c->stream,
+                     c->d_geo, c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv,
+                     lg, od, c->d_counters, gstack, ctr, ntx, (int)ntiles);
+  return RT_OK;
+}
+
+template <bool kLds, bool kCull, int kSamples>
+int launch_render4(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
+                   const OutDesc &od) {
+  if (c->persist || depth - 1 > kMaxLdsStack) return launch_persist3<kLds, kCull, kSamples>(c, lds, cam, W, H, depth,
+                                                                                           rows, od);
+  launch_tiles<kLds, kCull, kSamples>(c, lds, cam, W, H, depth, rows, od);
   return RT_OK;
 }
 
 int launch_render(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                  const OutDesc &out) {
-  if (c->persist || depth - 1 > kMaxLdsStack) {
-    if (lds_geo)
-      return c->cull ? launch_persist3<true, true, 4>(c, lds, cam, W, H, depth, rows, out)
-                     : launch_persist3<true, false, 4>(c, lds, cam, W, H, depth, rows, out);
-    return c->cull ? launch_persist3<false, true, 4>(c, lds, cam, W, H, depth, rows, out)
-                   : launch_persist3<false, false, 4>(c, lds, cam, W, H, depth, rows, out);
+                  const OutDesc &od) {
+  const bool aa = c->samples == 4;
+  if (lds_geo) {
+    if (c->cull) return aa ? launch_render4<true, true, 4>(c, lds, cam, W, H, depth, rows, od)
+                           : launch_render4<true, true, 1>(c, lds, cam, W, H, depth, rows, od);
+    return aa ? launch_render4<true, false, 4>(c, lds, cam, W, H, depth, rows, od)
+              : launch_render4<true, false, 1>(c, lds, cam, W, H, depth, rows, od);
   }
-  if (c->cull) {
-    if (c->wg_waves == 4) launch_tiles<true, 4>(c, lds_geo, lds, cam, W, H, depth, rows, out);
-    else launch_tiles<true, 1>(c, lds_geo, lds, cam, W, H, depth, rows, out);
-  } else {
-    if (c->wg_waves == 4) launch_tiles<false, 4>(c, lds_geo, lds, cam, W, H, depth, rows, out);
-    else launch_tiles<false, 1>(c, lds_geo, lds, cam, W, H, depth, rows, out);
-  }
-  return RT_OK;
+  if (c->cull) return aa ? launch_render4<false, true, 4>(c, lds, cam, W, H, depth, rows, od)
+                         : launch_render4<false, true, 1>(c, lds, cam, W, H, depth, rows, od);
+  return aa ? launch_render4<false, false, 4>(c, lds, cam, W, H, depth, rows, od)
+            : launch_render4<false, false, 1>(c, lds, cam, W, H, depth, rows, od);
 }
 
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -778,7 +771,6 @@ int rt_create(int device, rt_ctx **out) {
   if (device < 0 || device >= n) return RT_ERR_INVALID_ARG;
   rt_ctx *c = new rt_ctx();
   c->device = device;
-  if (const char *e = std::getenv("RT_HIP_WG_WAVES")) c->wg_waves = std::atoi(e) == 4 ? 4 : 1;
   if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_BVH")) c->bvh_on = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_MIN")) c->bvh_min = std::atoi(e);

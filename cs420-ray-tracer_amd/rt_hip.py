@@ -121,6 +121,8 @@ def lib(path: str = LIB_PATH):
             raise FileNotFoundError(f"{path} missing: run __graft_entry__.build() (no CPU fallback exists)")
         L = C.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("RT_HIP_LIB") and not hasattr(L, name):
+                continue  # an older diagnostic build (RT_HIP_LIB) may predate an entry point
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
