@@ -635,8 +635,8 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
 }
 
 // Shadow query through the light's direction grid (rt_lightgrid.h): each lane
-// tests the global list and the list of the cell its direction -d (from the
-// light towards the shaded point) falls in, with the same exact test and early
+// tests the list of the cell its direction (from the light towards the shaded
+// point) falls in and the global list, with the same exact test and early
 // exit as sweep_shadow.  A lane whose direction cannot be binned (degenerate or
 // non-finite) or whose line misses the light by more than max_off tests every
 // sphere.
@@ -648,8 +648,36 @@ struct LgArgs {
   double max_off;  // largest distance of a ray's line from its light the grid margins cover
 };
 
+// The cell list a shadow query of light l from point hp will test: the cell
+// of direction hp - L (within 1e-15 rad of the query line's -d, far inside
+// the grid's slack).  cb = -1: direction not binnable, test every sphere.
+// Issued one light ahead so the load overlaps the previous light's work.
+struct LgRange {
+  int cb, ce;
+};
+__device__ __forceinline__ LgRange lg_range(const LgArgs &lg, int l, D3 hp, D3 lp, bool act) {
+  LgRange r{0, 0};
+  if (act) {
+    const int N = lg.N, cells = 6 * N * N;
+    const int c = lg_cell((float)(hp.x - lp.x), (float)(hp.y - lp.y), (float)(hp.z - lp.z), N);
+    if (c < 0) {
+      r.cb = -1;
+    } else {
+      const int32_t *st = lg.start + (size_t)l * (size_t)(cells + 2);
+      r.cb = st[c];
+      r.ce = st[c + 1];
+    }
+  }
+  return r;
+}
+
+__device__ __forceinline__ int lg_first(const LgArgs &lg, LgRange r) {
+  return (r.cb >= 0 && r.ce > r.cb) ? lg.ids[r.cb] : 0;
+}
+
 __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d, D3 lp,
-                                             double dist, const LgArgs &lg, int l, Work &work) {
+                                             double dist, const LgArgs &lg, int l, LgRange cell, int id0,
+                                             Work &work) {
   if (__ballot(act) == 0) return false;
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
@@ -679,22 +707,22 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
     const D3 w = sub(lp, o);
     const double off = __builtin_fabs(w.y * d.z - w.z * d.y) + __builtin_fabs(w.z * d.x - w.x * d.z) +
                        __builtin_fabs(w.x * d.y - w.y * d.x);
-    const int c = (off <= lg.max_off) ? lg_cell((float)-d.x, (float)-d.y, (float)-d.z, N) : -1;
-    if (c < 0) {
+    if (!(off <= lg.max_off) || cell.cb < 0) {
       for (int i = 0; i < n && !occ; ++i) {
         work.exact += 1;
         test(i);
       }
     } else {
-      // global list, then the cell's list; the next id is loaded ahead
-      const int gb = st[cells], ge = st[cells + 1], cb = st[c], ce = st[c + 1];
-      const int len0 = ge - gb, len = len0 + (ce - cb);
+      // the cell's list (first id prefetched), then the global list
+      const int gb = st[cells], ge = st[cells + 1];
+      const int len1 = cell.ce - cell.cb, len = len1 + (ge - gb);
       int k = 0;
-      int nxt = len > 0 ? lg.ids[len0 > 0 ? gb : cb] : 0;
+      int nxt = id0;
+      if (len1 == 0 && len > 0) nxt = lg.ids[gb];
       while (k < len && !occ) {
         const int i = nxt;
         ++k;
-        if (k < len) nxt = lg.ids[k < len0 ? gb + k : cb + (k - len0)];
+        if (k < len) nxt = lg.ids[k < len1 ? cell.cb + k : gb + (k - len1)];
         work.exact += 1;
         test(i);
       }

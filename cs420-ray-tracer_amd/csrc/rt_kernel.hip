@@ -45,52 +45,37 @@ __device__ unsigned long long g_timeline[kTimelineWaves * kTl];
 
 constexpr int kMaxLdsStack = 4;  // levels of the LDS reflection stack (render_kernel)
 
-// trace_ray (src/main.cpp:16-58) for one camera ray per lane: the whole wave
-// walks the reflection levels together (uniform control flow around every
-// sweep, lanes masked by `alive`/`hit`).  `stk` is this wave's reflection
-// stack, [level][lane] (depth - 1 levels).  Returns the lane's colour.
+// One bounce of trace_ray (src/main.cpp:16-58) for the wave's `alive` lanes:
+// closest hit, sky on a miss, Phong shading with per-light shadow queries,
+// and the reflection decision (main.cpp:43-55).  Outcome per alive lane:
+// kEnded (colour = the level's final colour: sky, shade, or shade*(1-refl)
+// when no depth is left) or kSpawned (colour = shade*(1-refl), refl, and the
+// reflection ray no/nd leaving sphere nkey).  Wave-uniform control flow.
+enum { kEnded = 1, kSpawned = 2 };
 template <bool kCull>
-__device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const double *__restrict__ rad,
-                                         const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
-                                         int nl, D3 amb, int depth, const BvhArgs &bv, const LgArgs &lg, bool live,
-                                         D3 o, D3 d, StackEnt *stk, Work &work, unsigned &c_prim, unsigned &c_shadow,
-                                         unsigned &c_reflect) {
-  const int lane = threadIdx.x & 63;
-  int lev = 0;
-  int dleft = depth;
-  D3 res = mk(0.0, 0.0, 0.0);     // depth <= 0 -> black (main.cpp:17-18)
-  bool alive = live && depth >= 1;
-  int key = -1;  // sphere the current ray leaves (-1: camera), groups lanes in sweeps
-  c_prim += alive ? 1u : 0u;
-
-  while (__ballot(alive)) {
-    double bt;
-#ifdef RT_STAMPS
-    const unsigned long long it_before = work.it_closest;
-#endif
-    RT_T0(t_cl);
-    const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, key, bv, bt, work);
-    RT_ACC(work, 8, t_cl);
-#ifdef RT_STAMPS
-    if (dleft == depth) work.it_prim += work.it_closest - it_before;
-#endif
-    const bool hit = alive && bi >= 0;
-    if (alive && !hit) {  // sky, main.cpp:26-30
-      const double st = 0.5 * (d.y + 1.0);
-      res = add(scale(mk(1.0, 1.0, 1.0), 1.0 - st), scale(mk(0.5, 0.7, 1.0), st));
-      alive = false;
-    }
-    const int hi = hit ? bi : 0;
-    const D3 hp = add(o, scale(d, bt));                            // main.cpp:32
-    D3 col;
-    {
-      const SphMat m0 = mat[hi];
-      col = mul(amb, mk(m0.cr, m0.cg, m0.cb));                   // scene.h:91
-    }
-    // scene.h:94-120, split in two phases per block of 64 lights so that no
-    // shading state is live across the shadow sweeps: (A) occlusion bits for
-    // every light, (B) Phong terms in light order for the unoccluded ones.
-    // Phase B recomputes to_light / ldir with the same operations (same bits).
+__device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                       const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
+                                       int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg, bool alive, D3 o, D3 d,
+                                       int key, int dleft, Work &work, unsigned &c_shadow, int &outcome, D3 &color,
+                                       double &refl, D3 &no, D3 &nd, int &nkey) {
+  outcome = 0;
+  double bt;
+  RT_T0(t_cl);
+  const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, key, bv, bt, work);
+  RT_ACC(work, 8, t_cl);
+  const bool hit = alive && bi >= 0;
+  if (alive && !hit) {  // sky, main.cpp:26-30
+    const double st = 0.5 * (d.y + 1.0);
+    color = add(scale(mk(1.0, 1.0, 1.0), 1.0 - st), scale(mk(0.5, 0.7, 1.0), st));
+    outcome = kEnded;
+  }
+  const int hi = hit ? bi : 0;
+  const D3 hp = add(o, scale(d, bt));                            // main.cpp:32
+  D3 col;
+  {
+    const SphMat m0 = mat[hi];
+    col = mul(amb, mk(m0.cr, m0.cg, m0.cb));                   // scene.h:91
+  }
     // scene.h:94-120: per light in file order, the shadow query then (if lit)
     // the Phong terms with the same ldir
     {
@@ -99,8 +84,15 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
       const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
       const D3 view = normalized(sub(o, hp));                       // main.cpp:38
       const D3 mc = mk(m.cr, m.cg, m.cb);
+      LgRange next = lg.on && nl > 0 ? lg_range(lg, 0, hp, mk(slight[0].px, slight[0].py, slight[0].pz), hit)
+                                     : LgRange{0, 0};
       for (int l = 0; l < nl; ++l) {
         RT_T0(t_setup);
+        // this light's first list id, and the next light's cell range, are
+        // loaded now and consumed after the setup arithmetic below
+        const LgRange cell = next;
+        const int id0 = lg.on ? lg_first(lg, cell) : 0;
+        if (lg.on && l + 1 < nl) next = lg_range(lg, l + 1, hp, mk(slight[l + 1].px, slight[l + 1].py, slight[l + 1].pz), hit);
         const LightD L = slight[l];
         const D3 lp = mk(L.px, L.py, L.pz);
         const D3 to_light = sub(lp, hp);
@@ -109,7 +101,7 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
         const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
         RT_ACC(work, 3, t_setup);
         RT_T0(t_sh);
-        const bool occ = lg.on ? shadow_cells(g, n, hit, so, sd, lp, dist, lg, l, work)
+        const bool occ = lg.on ? shadow_cells(g, n, hit, so, sd, lp, dist, lg, l, cell, id0, work)
                                : sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, hi, dist, bv, work);
         RT_ACC(work, 9, t_sh);
         RT_T0(t_shade);
@@ -127,37 +119,160 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
         RT_ACC(work, 4, t_shade);
       }
     }
-    if (hit) {
-      c_shadow += (unsigned)nl;
-      const SphMat m = mat[hi];
-      if (m.refl > 0.0) {                                         // main.cpp:43-55
-        const double w = 1.0 - m.refl;
-        const D3 A = mk(col.x * w, col.y * w, col.z * w);
-        if (dleft - 1 >= 1) {  // the stack holds depth-1 levels, so lev < depth-1 here
-          stk[lev * 64 + lane] = StackEnt{A.x, A.y, A.z, m.refl};
-          ++lev;
-          const SphGeo sg = g[hi];
-          const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));
-          const D3 rd = sub(d, scale(scale(nrm, 2.0), dot(d, nrm)));
-          o = add(hp, scale(nrm, kEps));
-          d = normalized(rd);
-          key = hi;
-          --dleft;
-          ++c_reflect;
-        } else {
-          res = A;  // trace_ray(depth 0) is black: A + (0,0,0)*refl == A
-          alive = false;
-        }
+  if (hit) {
+    c_shadow += (unsigned)nl;
+    const SphMat m = mat[hi];
+    if (m.refl > 0.0) {                                         // main.cpp:43-55
+      const double w = 1.0 - m.refl;
+      const D3 A = mk(col.x * w, col.y * w, col.z * w);
+      color = A;  // with no depth left trace_ray(depth 0) is black: A + (0,0,0)*refl == A
+      outcome = kEnded;
+      if (dleft - 1 >= 1) {
+        const SphGeo sg = g[hi];
+        const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));
+        const D3 rd = sub(d, scale(scale(nrm, 2.0), dot(d, nrm)));
+        no = add(hp, scale(nrm, kEps));
+        nd = normalized(rd);
+        nkey = hi;
+        refl = m.refl;
+        outcome = kSpawned;
+      }
+    } else {
+      color = col;
+      outcome = kEnded;
+    }
+  }
+}
+
+// trace_ray for one camera ray per lane, the wave walking the levels together
+// (lanes masked by `alive`); the lane's reflection stack entries are
+// stk[level * sstride] (depth - 1 levels), unwound innermost first.
+template <bool kCull>
+__device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                         const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
+                                         int nl, D3 amb, int depth, const BvhArgs &bv, const LgArgs &lg, bool live,
+                                         D3 o, D3 d, StackEnt *stk, size_t sstride, Work &work, unsigned &c_prim,
+                                         unsigned &c_shadow, unsigned &c_reflect) {
+  int lev = 0;
+  int dleft = depth;
+  D3 res = mk(0.0, 0.0, 0.0);     // depth <= 0 -> black (main.cpp:17-18)
+  bool alive = live && depth >= 1;
+  int key = -1;  // sphere the current ray leaves (-1: camera), groups lanes in sweeps
+  c_prim += alive ? 1u : 0u;
+  while (__ballot(alive)) {
+    int outcome, nkey = 0;
+    D3 color = res, no = o, nd = d;
+    double refl = 0.0;
+    bounce<kCull>(g, rad, mat, slight, n, nl, amb, bv, lg, alive, o, d, key, dleft, work, c_shadow, outcome, color,
+                  refl, no, nd, nkey);
+    if (alive) {
+      if (outcome == kSpawned) {
+        stk[lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
+        ++lev;
+        o = no;
+        d = nd;
+        key = nkey;
+        --dleft;
+        ++c_reflect;
       } else {
-        res = col;
+        res = color;
         alive = false;
       }
     }
   }
   while (lev > 0) {  // unwind: shade*(1-refl) + reflected*refl, innermost first
     --lev;
-    const StackEnt e = stk[lev * 64 + lane];
+    const StackEnt e = stk[lev * sstride];
     res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
+  }
+  return res;
+}
+
+// Workgroup-compacted trace_ray.  Level 0 runs one lane per pixel (coherent
+// 8x8 tiles); the reflection rays it spawns, typically a few dozen of the
+// workgroup's 256 pixels, are appended to an LDS queue and the next level
+// runs them packed into the first waves, so the incoherent levels pay for
+// the rays they trace instead of a whole wave per tile.  Each pixel keeps
+// its (shade*(1-refl), refl) entries in `gstack` ([level][pixel], global
+// memory) and its final colour + level count in `term` (LDS); the unwind is
+// per pixel, innermost level first, exactly as trace_wave / main.cpp:54.
+struct QRay {  // 64 B
+  double ox, oy, oz, dx, dy, dz;
+  int orig, dleft, key, pix;
+};
+struct TermRec {  // 32 B
+  double r, g, b;
+  int nlev, pad;
+};
+template <bool kCull>
+__device__ __forceinline__ D3 trace_compact(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                            const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
+                                            int nl, D3 amb, int depth, const BvhArgs &bv, const LgArgs &lg,
+                                            bool live, D3 o, D3 d, int pix, StackEnt *__restrict__ gstack,
+                                            size_t npx, QRay *q, int *qcnt, TermRec *term, Work &work,
+                                            unsigned &c_prim, unsigned &c_shadow, unsigned &c_reflect) {
+  const int t = threadIdx.x, lane = t & 63;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  // appends this wave's spawned rays to the LDS queue
+  auto push = [&](bool spawn, const QRay &r) {
+    const unsigned long long m = __ballot(spawn);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(qcnt, (int)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (spawn) q[base + (int)__popcll(m & lt)] = r;
+  };
+  if (t == 0) *qcnt = 0;
+  __syncthreads();
+  {  // level 0: this lane's camera ray
+    const bool alive = live && depth >= 1;
+    c_prim += alive ? 1u : 0u;
+    int outcome = 0, nkey = 0;
+    D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;  // depth <= 0 -> black (main.cpp:17-18)
+    double refl = 0.0;
+    if (__ballot(alive))
+      bounce<kCull>(g, rad, mat, slight, n, nl, amb, bv, lg, alive, o, d, -1, depth, work, c_shadow, outcome, color,
+                    refl, no, nd, nkey);
+    const bool spawn = alive && outcome == kSpawned;
+    if (live) term[t] = TermRec{color.x, color.y, color.z, 0, 0};
+    if (spawn) {
+      gstack[pix] = StackEnt{color.x, color.y, color.z, refl};
+      ++c_reflect;
+    }
+    push(spawn, QRay{no.x, no.y, no.z, nd.x, nd.y, nd.z, t, depth - 1, nkey, pix});
+  }
+  __syncthreads();
+  for (int lev = 1; lev < depth; ++lev) {
+    const int nq = *qcnt;
+    if (nq == 0) break;  // workgroup-uniform
+    const bool act = t < nq;
+    QRay r = q[act ? t : 0];
+    __syncthreads();
+    if (t == 0) *qcnt = 0;
+    __syncthreads();
+    if (__ballot(act)) {
+      int outcome = 0, nkey = 0;
+      D3 color = mk(0.0, 0.0, 0.0), no = mk(r.ox, r.oy, r.oz), nd = mk(r.dx, r.dy, r.dz);
+      double refl = 0.0;
+      bounce<kCull>(g, rad, mat, slight, n, nl, amb, bv, lg, act, mk(r.ox, r.oy, r.oz), mk(r.dx, r.dy, r.dz), r.key,
+                    r.dleft, work, c_shadow, outcome, color, refl, no, nd, nkey);
+      const bool spawn = act && outcome == kSpawned;
+      if (act) term[r.orig] = TermRec{color.x, color.y, color.z, lev, 0};
+      if (spawn) {
+        gstack[(size_t)lev * npx + r.pix] = StackEnt{color.x, color.y, color.z, refl};
+        ++c_reflect;
+      }
+      push(spawn, QRay{no.x, no.y, no.z, nd.x, nd.y, nd.z, r.orig, r.dleft - 1, nkey, r.pix});
+    }
+    __syncthreads();
+  }
+  D3 res = mk(0.0, 0.0, 0.0);
+  if (live) {
+    const TermRec e0 = term[t];
+    res = mk(e0.r, e0.g, e0.b);
+    for (int lev = e0.nlev - 1; lev >= 0; --lev) {  // unwind, innermost first
+      const StackEnt e = gstack[(size_t)lev * npx + pix];
+      res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
+    }
   }
   return res;
 }
@@ -176,11 +291,24 @@ struct OutDesc {
 // path) or 4 (main_gpu.cu:249-333's antialias offsets, in fp64 serial
 // semantics: samples summed in order, then * 0.25).  Adds the tile's ray
 // counts to the wave sums.
-template <bool kCull, int kSamples>
+struct CompactArgs {
+  StackEnt *gstack;  // [depth-1][npx]
+  size_t npx;
+  QRay *q;           // LDS
+  int *qcnt;         // LDS
+  TermRec *term;     // LDS
+};
+
+// Reflection stack placement: kStackLds = [level][lane] per wave in LDS (4
+// levels), kStackGlobal = [level][pixel] in global memory (any depth),
+// kStackCompact = global, with the workgroup-compacted levels of trace_compact.
+enum { kStackLds = 0, kStackGlobal = 1, kStackCompact = 2 };
+template <bool kCull, int kSamples, int kStack>
 __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                            const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                            int nl, D3 amb, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                                           const BvhArgs &bv, const LgArgs &lg, const OutDesc &od, int x0, int k0, StackEnt *stk, Work &work,
+                                           const BvhArgs &bv, const LgArgs &lg, const OutDesc &od, int x0, int k0,
+                                           StackEnt *stk, const CompactArgs &ca, Work &work,
                                            unsigned long long (&sums)[4]) {
   const int lane = threadIdx.x & 63;
   const int x = x0 + (lane & 7);
@@ -203,8 +331,17 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
                        scale(mk(cam.ux, cam.uy, cam.uz), sv));
     const D3 d = normalized(normalized(dir));  // get_ray normalises, Ray() normalises again
     const D3 o = mk(cam.px, cam.py, cam.pz);
-    const D3 c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk, work, c_prim,
-                                   c_shadow, c_reflect);
+    D3 c;
+    const int pix = k * od.xw + (x - od.x0);
+    if (kStack == kStackCompact)
+      c = trace_compact<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, pix, ca.gstack, ca.npx,
+                               ca.q, ca.qcnt, ca.term, work, c_prim, c_shadow, c_reflect);
+    else if (kStack == kStackGlobal)
+      c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, ca.gstack + pix, ca.npx,
+                            work, c_prim, c_shadow, c_reflect);
+    else
+      c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk + lane, 64, work,
+                            c_prim, c_shadow, c_reflect);
     acc = kSamples == 1 ? c : add(acc, c);  // serial: the colour itself; AA: from 0 in sample order (main_gpu.cu:250, 327)
   }
   const D3 res = kSamples == 4 ? scale(acc, 0.25) : acc;  // main_gpu.cu:331, 1/4 is exact
@@ -299,12 +436,38 @@ __device__ __forceinline__ void record_timeline(unsigned wave_id, unsigned long 
 #endif
 // One wave per 8x8 tile (2x2 tiles per workgroup for kWaves = 4); the
 // reflection stack (depth <= 5) lives in LDS after the staged scene.
-constexpr int kWaves = 4;  // 2x2 tiles of 8x8 pixels per workgroup
-template <bool kLdsGeo, bool kCull, int kSamples>
-__global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kernel(
+constexpr int kWaves = 4;  // 2x2 tiles of 8x8 pixels per workgroup (persistent kernel, LDS sizes)
+// Waves per render_kernel workgroup: 4 (2x2 tiles) when the workgroup shares
+// LDS (a staged scene, the LDS stack or the compaction queue); 1 otherwise, so
+// no wave's slot waits for its slowest neighbour.
+template <bool kLdsGeo, int kStack>
+constexpr int wg_waves() {
+  return (kLdsGeo || kStack != 1) ? 4 : 1;
+}
+// LDS after the staged scene: the 4-level reflection stack per wave, or
+// (kCompact) the workgroup's ray queue, terminal colours and queue count.
+constexpr size_t kLdsStackBytes = (size_t)kWaves * 64 * kMaxLdsStack * sizeof(StackEnt);
+constexpr size_t kLdsCompactBytes = (size_t)kWaves * 64 * (sizeof(QRay) + sizeof(TermRec)) + 32;
+
+template <bool kLdsGeo, bool kCull, int kSamples, int kStack>
+__global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PER_EU) void render_kernel(
     const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
     const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
-    BvhArgs bv_in, LgArgs lg, OutDesc od, unsigned long long *__restrict__ counters) {
+    BvhArgs bv_in, LgArgs lg, OutDesc od, StackEnt *__restrict__ gstack, unsigned long long *__restrict__ counters,
+    int ntx, int ntiles, int xcd_per) {  // xcd_per: tiles per run
+  // 16x16-pixel workgroup tile.  Workgroups are dealt to the 8 XCDs round
+  // robin (b % 8).  With chunk > 0 the scanline-ordered tiles are cut into
+  // runs of `chunk` tiles and run r goes to XCD r % 8: each XCD's L2 serves
+  // a few compact image regions (locality for scene data read through L2)
+  // while every XCD still samples the whole image (balance).
+  const int b = blockIdx.x;
+  int tile = b;
+  if (xcd_per > 0) {
+    const int m = b >> 3;  // this workgroup's rank on its XCD
+    tile = ((m / xcd_per) * 8 + (b & 7)) * xcd_per + m % xcd_per;
+  }
+  if (tile >= ntiles) return;  // workgroup-uniform, before any barrier
+  const int tx = tile % ntx, ty = tile / ntx;
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
   const SphGeo *g;
   const double *rad;
@@ -312,21 +475,28 @@ __global__ __launch_bounds__(64 * kWaves, RT_MIN_WAVES_PER_EU) void render_kerne
   BvhArgs bv = bv_in;
   stage_scene<kLdsGeo>(smem, geo, radius, lights, n, nl, bv, g, rad, slight);
   const size_t stack_off = (lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31;
-  constexpr int kWx = kWaves == 4 ? 2 : 1;
+  constexpr int kWg = wg_waves<kLdsGeo, kStack>();
+  constexpr int kWx = kWg == 4 ? 2 : 1;
   const int wave = threadIdx.x >> 6;
   StackEnt *stk = reinterpret_cast<StackEnt *>(smem + stack_off) + (size_t)wave * kMaxLdsStack * 64;
+  CompactArgs ca;
+  ca.gstack = gstack;
+  ca.npx = (size_t)rows.count * od.xw;
+  ca.q = reinterpret_cast<QRay *>(smem + stack_off);
+  ca.term = reinterpret_cast<TermRec *>(smem + stack_off + (size_t)kWaves * 64 * sizeof(QRay));
+  ca.qcnt = reinterpret_cast<int *>(smem + stack_off + (size_t)kWaves * 64 * (sizeof(QRay) + sizeof(TermRec)));
   Work work;
   unsigned long long sums[4] = {0, 0, 0, 0};
   RT_T0(t_wave);
 #ifdef RT_STAMPS
   const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  trace_tile<kCull, kSamples>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
-                    od.x0 + blockIdx.x * (8 * kWx) + (wave % kWx) * 8,
-                    blockIdx.y * (8 * (kWaves / kWx)) + (wave / kWx) * 8, stk, work, sums);
+  trace_tile<kCull, kSamples, kStack>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
+                                        od.x0 + tx * (8 * kWx) + (wave % kWx) * 8,
+                                        ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, work, sums);
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
-  record_timeline((blockIdx.x + blockIdx.y * gridDim.x) * kWaves + wave, t_real0, work);
+  record_timeline(tile * kWg + wave, t_real0, work);
 #endif
   flush_counts(counters, sums, work);
 }
@@ -382,8 +552,8 @@ __global__ __launch_bounds__(64 * kWaves, RT_PERSIST_WAVES_PER_EU) void render_p
     }
     pending = fetch(shard);
     const int ty = (int)(tile / ntx), tx = (int)(tile % ntx);
-    trace_tile<kCull, kSamples>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
-                      od.x0 + tx * 8, ty * 8, stk, work, sums);
+    trace_tile<kCull, kSamples, kStackLds>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
+                                           od.x0 + tx * 8, ty * 8, stk, CompactArgs{}, work, sums);
   }
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
@@ -457,6 +627,12 @@ struct rt_ctx {
   unsigned char *stack_buf = nullptr;
   size_t stack_bytes = 0;
   int samples = 1;  // 4: the antialias mode (rt_set_antialias)
+  // RT_HIP_STACK: 0 LDS reflection stack (persistent kernel above depth 5),
+  // 1 global per-pixel stack, 2 global stack + workgroup-compacted levels
+  int stack_mode = 1;
+  int xcd_map = 0;  // RT_HIP_XCD_MAP: visits per XCD (runs of ntiles/(8*visits) tiles); 0 = launch order
+  unsigned char *cstack_buf = nullptr;
+  size_t cstack_bytes = 0;
   int persist = 0;  // RT_HIP_PERSIST=1: persistent megakernel for every depth (always used above depth 5)
   std::string err;
 };
@@ -534,17 +710,39 @@ LgArgs lg_args(const rt_ctx *c) {
   return g;
 }
 
-template <bool kLds, bool kCull, int kSamples>
-void launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                  const OutDesc &od) {
+template <bool kLds, bool kCull, int kSamples, int kStack>
+int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
+                 const OutDesc &od) {
   const BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
-  dim3 grid((od.xw + 15) / 16, (rows.count + 15) / 16);
+  constexpr int kWg = wg_waves<kLds, kStack>(), kWx = kWg == 4 ? 2 : 1, kWy = kWg / kWx;
+  const int ntx = (od.xw + 8 * kWx - 1) / (8 * kWx), nty = (rows.count + 8 * kWy - 1) / (8 * kWy);
+  const long long ntiles = (long long)ntx * nty;
+  if (ntiles > (1LL << 30)) return RT_ERR_INVALID_ARG;
+  // runs of tiles per XCD visit (see render_kernel); grid rounded up to whole rounds
+  const int xcd_per = c->xcd_map > 0 ? (int)std::max(1LL, ntiles / (8LL * c->xcd_map)) : 0;
+  const long long rounds = xcd_per ? (ntiles + 8LL * xcd_per - 1) / (8LL * xcd_per) : 0;
+  const dim3 grid(xcd_per ? (unsigned)(rounds * 8 * xcd_per) : (unsigned)ntiles);
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
-  lds = ((lds + 31) & ~(size_t)31) + (size_t)kWaves * 64 * kMaxLdsStack * sizeof(StackEnt);
-  hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples>), grid, dim3(64 * kWaves), lds, c->stream, c->d_geo,
-                     c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv, lg, od,
-                     c->d_counters);
+  lds = ((lds + 31) & ~(size_t)31) +
+        (kStack == kStackCompact ? kLdsCompactBytes : kStack == kStackLds ? kLdsStackBytes : 0);
+  StackEnt *gstack = nullptr;
+  if (kStack != kStackLds && depth > 1) {
+    const size_t need = (size_t)(depth - 1) * rows.count * od.xw * sizeof(StackEnt);
+    if (c->cstack_bytes < need) {
+      RT_TRY(c, hipStreamSynchronize(c->stream));
+      if (c->cstack_buf) (void)hipFree(c->cstack_buf);
+      c->cstack_buf = nullptr;
+      c->cstack_bytes = 0;
+      RT_TRY(c, hipMalloc(&c->cstack_buf, need));
+      c->cstack_bytes = need;
+    }
+    gstack = reinterpret_cast<StackEnt *>(c->cstack_buf);
+  }
+  hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream,
+                     c->d_geo, c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv,
+                     lg, od, gstack, c->d_counters, ntx, (int)ntiles, xcd_per);
+  return RT_OK;
 }
 
 template <bool kLds, bool kCull, int kSamples>
@@ -585,10 +783,13 @@ int launch_persist3(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dep
 template <bool kLds, bool kCull, int kSamples>
 int launch_render4(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
                    const OutDesc &od) {
+  if (c->stack_mode == kStackCompact)
+    return launch_tiles<kLds, kCull, kSamples, kStackCompact>(c, lds, cam, W, H, depth, rows, od);
+  if (c->stack_mode == kStackGlobal)
+    return launch_tiles<kLds, kCull, kSamples, kStackGlobal>(c, lds, cam, W, H, depth, rows, od);
   if (c->persist || depth - 1 > kMaxLdsStack) return launch_persist3<kLds, kCull, kSamples>(c, lds, cam, W, H, depth,
                                                                                            rows, od);
-  launch_tiles<kLds, kCull, kSamples>(c, lds, cam, W, H, depth, rows, od);
-  return RT_OK;
+  return launch_tiles<kLds, kCull, kSamples, kStackLds>(c, lds, cam, W, H, depth, rows, od);
 }
 
 int launch_render(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
@@ -778,6 +979,8 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH_GROUPS")) c->bvh_groups = std::max(1, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID")) c->lg_on = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_PERSIST")) c->persist = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_STACK")) c->stack_mode = std::max(0, std::min(2, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_XCD_MAP")) c->xcd_map = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n = std::max(1, std::min(256, std::atoi(e)));
   auto bail = [&](int rc) {
@@ -813,6 +1016,7 @@ void rt_destroy(rt_ctx *c) {
   if (c->d_tmp) (void)hipFree(c->d_tmp);
   if (c->wf_buf) (void)hipFree(c->wf_buf);
   if (c->stack_buf) (void)hipFree(c->stack_buf);
+  if (c->cstack_buf) (void)hipFree(c->cstack_buf);
   for (int i = 0; i < rt_ctx::kRing; i++) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);

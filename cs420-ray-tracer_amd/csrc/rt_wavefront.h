@@ -213,7 +213,8 @@ __global__ __launch_bounds__(64) void wf_level0(WfArgs a) {
       const double dist = length(to_light);
       const D3 ldir = normalized(to_light);
       const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
-      const bool occ = a.lg.on ? shadow_cells(g, a.n, hit, so, sd, lp, dist, a.lg, l, work)
+      const LgRange cr = a.lg.on ? lg_range(a.lg, l, hp, lp, hit) : LgRange{0, 0};
+      const bool occ = a.lg.on ? shadow_cells(g, a.n, hit, so, sd, lp, dist, a.lg, l, cr, lg_first(a.lg, cr), work)
                                : sweep_shadow<kCull>(g, rad, a.n, hit, so, sd, lp, hi, dist, bv, work);
       if (occ) occm |= 1ull << (l - l0);
     }
@@ -312,7 +313,8 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs a, int level) {
       const double dist = length(to_light);
       const D3 ldir = normalized(to_light);
       const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
-      const bool occ = a.lg.on ? shadow_cells(g, a.n, hit, so, sd, lp, dist, a.lg, l, work)
+      const LgRange cr = a.lg.on ? lg_range(a.lg, l, hp, lp, hit) : LgRange{0, 0};
+      const bool occ = a.lg.on ? shadow_cells(g, a.n, hit, so, sd, lp, dist, a.lg, l, cr, lg_first(a.lg, cr), work)
                                : sweep_shadow<kCull>(g, rad, a.n, hit, so, sd, lp, h.sph, dist, bv, work);
       if (hit && !occ) {
         const double ndl = max0(dot(nrm, ldir));

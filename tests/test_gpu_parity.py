@@ -395,3 +395,49 @@ def test_pipelines_random_scenes(pipeline_renderer, seed):
     ref, _, _ = orc.OracleScene(text=text).render(W, H, D, threads=4)
     rgb, _ = pipeline_renderer.render(sc.camera(), W, H, D)
     assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
+
+
+@pytest.fixture(params=[{"RT_HIP_STACK": "0"}, {"RT_HIP_STACK": "2"}, {"RT_HIP_XCD_MAP": "0"}],
+                ids=["lds-stack", "compact", "no-xcd-map"])
+def stack_renderer(request, monkeypatch):
+    """Non-default kernel layouts (RT_HIP_STACK=0: LDS reflection stack, the
+    persistent kernel above depth 5; 2: workgroup-compacted reflection levels;
+    RT_HIP_XCD_MAP=0: workgroup tiles in launch order)."""
+    import rt_hip
+
+    for k, v in request.param.items():
+        monkeypatch.setenv(k, v)
+    r = rt_hip.Renderer(0)
+    yield r
+    r.close()
+
+
+@pytest.mark.parametrize("name", ["complex_97x61_d4", "medium_1280x720_d10", "synth200_1920x1080_d4",
+                                  "synth10k_384x216_d6", "simple_2x2_d10"])
+def test_stack_modes_golden(stack_renderer, name):
+    rgb, st, m = _render(stack_renderer, name)
+    assert rgb == golden_rgb(name), diff_summary(rgb, golden_rgb(name))
+    assert {"primary": st.rays_primary, "shadow": st.rays_shadow, "reflect": st.rays_reflect} == m["rays"]
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2, 7, 64])
+def test_stack_modes_depth_edges(stack_renderer, depth):
+    import orc
+    import rt_hip
+
+    W, H = 67, 45
+    sc = rt_hip.Scene.load(scene_path("medium"))
+    stack_renderer.upload(sc)
+    rgb, st = stack_renderer.render(sc.camera(), W, H, depth)
+    ref, counts, _ = orc.OracleScene(scene_path("medium")).render(W, H, depth, threads=4)
+    assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
+    assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
+                                                                   counts["reflect"])
+    rows = rt_hip.rows_for_shard(H, 8, 1, 3)
+    rgb2, _ = stack_renderer.render(sc.camera(), W, H, depth, rows=rows)
+    got = np.frombuffer(bytes(rgb2), np.uint8).reshape(-1, W, 3)
+    want = np.frombuffer(ref, np.uint8).reshape(H, W, 3)
+    for k in range(rows.count):
+        y = (k // 8) * 8 * 3 + 8 + k % 8
+        if y < H:
+            assert np.array_equal(got[k], want[y])
