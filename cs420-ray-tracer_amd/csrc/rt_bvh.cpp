@@ -153,4 +153,38 @@ void build_bvh(const double *cx, const double *cy, const double *cz, const doubl
   b.build(0, n);
 }
 
+int32_t build_bvh2(const std::vector<BvhNode> &nodes, std::vector<BvhNode2> &out, int &depth) {
+  out.clear();
+  depth = 0;
+  if (nodes.empty()) return -1;
+  // preorder index of each internal node -> its BvhNode2 index
+  std::vector<int32_t> map(nodes.size(), -1);
+  for (size_t i = 0; i < nodes.size(); i++)
+    if (nodes[i].leaf < 0) {
+      map[i] = (int32_t)out.size();
+      out.push_back(BvhNode2{});
+    }
+  auto ref = [&](int i) { return nodes[i].leaf >= 0 ? -(nodes[i].leaf + 1) : map[i]; };
+  std::vector<std::pair<int, int>> todo{{0, 0}};  // (preorder index, depth)
+  while (!todo.empty()) {
+    const auto [i, dep] = todo.back();
+    todo.pop_back();
+    depth = std::max(depth, dep);
+    if (nodes[i].leaf >= 0) continue;
+    const int l = i + 1, r = nodes[l].skip;
+    BvhNode2 &b = out[map[i]];
+    for (int k = 0; k < 3; k++) {
+      b.lo0[k] = nodes[l].lo[k];
+      b.hi0[k] = nodes[l].hi[k];
+      b.lo1[k] = nodes[r].lo[k];
+      b.hi1[k] = nodes[r].hi[k];
+    }
+    b.c0 = ref(l);
+    b.c1 = ref(r);
+    todo.push_back({l, dep + 1});
+    todo.push_back({r, dep + 1});
+  }
+  return ref(0);
+}
+
 }  // namespace rtk

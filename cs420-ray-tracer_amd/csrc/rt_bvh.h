@@ -19,6 +19,20 @@ struct BvhNode {  // 32 B
   int32_t leaf;   // leaf: (first << 4) | count (count 1..15); internal: -1
 };
 
+// Two-child node for ordered (near-first) traversal: both children's boxes
+// in one 64-B record.  Child reference c >= 0: internal node c of this array;
+// c < 0: leaf -(c + 1) = (first << 4) | count, as BvhNode::leaf.
+struct BvhNode2 {  // 64 B
+  float lo0[3], hi0[3], lo1[3], hi1[3];
+  int32_t c0, c1;
+  int32_t pad[2];
+};
+
+// Derives the two-child layout from the preorder one; returns the root's
+// reference (a leaf reference when the whole tree is one leaf) and the tree
+// depth (the most far-children an ordered walk can have pending).
+int32_t build_bvh2(const std::vector<BvhNode> &nodes, std::vector<BvhNode2> &out, int &depth);
+
 // Builds the BVH over spheres (centres cx,cy,cz, radii r).  `prims` receives
 // the sphere indices in leaf order.  Leaves hold at most `max_leaf` (<= 15)
 // spheres; depth is unlimited (the traversal is stackless).

@@ -290,7 +290,15 @@ struct BvhArgs {
   int min_cands;        // switch a group to the BVH above this many cull candidates
   int always;           // 1: skip the cull and traverse for every group
   int max_groups;       // lanes of groups beyond this many go straight to the BVH
+  // ordered (near-first) traversal: two-child nodes, the root's reference, and
+  // this lane's LDS stack ([entry][lane], kOrderedStack entries); ostk ==
+  // nullptr selects the stackless preorder walk
+  const BvhNode2 *n2;
+  int root_ref;
+  int ordered;  // the host allows the ordered walk (tree depth <= kOrderedStack)
+  int2 *ostk;
 };
+constexpr int kOrderedStack = 24;  // pending far children; the host requires depth <= this
 
 // Visits every leaf whose (grown) box the line meets and whose entry does not
 // exceed tmax_fn() (re-read per node: closest-hit tightens it); calls
@@ -338,6 +346,76 @@ __device__ __forceinline__ void bvh_walk(const BvhArgs &bv, D3 o, D3 d, T &&tmax
     } else {
       i = in ? i + 1 : nd.skip;
     }
+  }
+}
+
+// Ordered closest-hit walk: at an internal node both child boxes are tested
+// (same grown fp32 slab test, both directions of the line, as bvh_walk), the
+// nearer child is entered and the farther pushed with its entry t; pops skip
+// entries whose entry exceeds tmax_fn().  A box is pruned only against the
+// current best (with bvh_walk's margin), so every leaf that can still hold a
+// closer root is visited and the lexicographic (t, index) minimum is the one
+// bvh_walk finds, in fewer steps.
+template <typename T, typename F>
+__device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, T &&tmax_fn, Work &work,
+                                                 F &&leaf_fn) {
+  const float ox = (float)(o.x - bv.c0x), oy = (float)(o.y - bv.c0y), oz = (float)(o.z - bv.c0z);
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+  const float dd = (dx * dx + dy * dy + dz * dz) * (1.0f + 1e-5f);
+  const float m = bv.margin;
+  auto slab = [&](const float *lo, const float *hi, float &tn) {
+    const float ax = (lo[0] - m - ox) * ix, bx = (hi[0] + m - ox) * ix;
+    const float ay = (lo[1] - m - oy) * iy, by = (hi[1] + m - oy) * iy;
+    const float az = (lo[2] - m - oz) * iz, bz = (hi[2] + m - oz) * iz;
+    tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    return tn <= tf && !((double)tn > tmax_fn());
+  };
+  int2 *st = bv.ostk + (threadIdx.x & 63);
+  int sp = 0;
+  float tn;
+  if (!slab(bv.nodes[0].lo, bv.nodes[0].hi, tn)) return;
+  int ref = bv.root_ref;
+  for (;;) {
+    work.cull += 1;
+    if (ref >= 0) {
+      const BvhNode2 nd = bv.n2[ref];
+      float t0, t1;
+      const bool h0 = slab(nd.lo0, nd.hi0, t0), h1 = slab(nd.lo1, nd.hi1, t1);
+      if (h0 && h1) {
+        const bool first0 = t0 <= t1;
+        st[sp * 64] = make_int2(first0 ? nd.c1 : nd.c0, __float_as_int(first0 ? t1 : t0));
+        ++sp;
+        ref = first0 ? nd.c0 : nd.c1;
+        continue;
+      }
+      if (h0 || h1) {
+        ref = h0 ? nd.c0 : nd.c1;
+        continue;
+      }
+    } else {
+      const int leaf = -(ref + 1), first = leaf >> 4, cnt = leaf & 15;
+      for (int k = 0; k < cnt; ++k) {
+        const float4 q = bv.pf[first + k];  // fp32 prefilter, as bvh_walk
+        const float wx = q.x - ox, wy = q.y - oy, wz = q.z - oz;
+        const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
+        const float R = q.w + bv.pmargin;
+        if (cx * cx + cy * cy + cz * cz > R * R * dd) continue;
+        if (!leaf_fn((int)bv.prims[first + k])) return;
+      }
+    }
+    bool more = false;
+    while (sp > 0) {
+      --sp;
+      const int2 e = st[sp * 64];
+      if (!((double)__int_as_float(e.y) > tmax_fn())) {
+        ref = e.x;
+        more = true;
+        break;
+      }
+    }
+    if (!more) return;
   }
 }
 
@@ -521,11 +599,14 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
   if (have_bvh && need) {
     // a box whose entry is beyond the best t (by the margin) holds no closer root;
     // spheres a group pass already tested are harmless to test again
-    bvh_walk(bv, o, d, [&] { return bt + 2e-6 * (bv.diam + __builtin_fabs(bt)); }, work, [&](int i) {
+    auto tmax = [&] { return bt + 2e-6 * (bv.diam + __builtin_fabs(bt)); };
+    auto leaf = [&](int i) {
       work.exact += 1;
       test(i);
       return true;
-    });
+    };
+    if (bv.ostk) bvh_walk_ordered(bv, o, d, tmax, work, leaf);
+    else bvh_walk(bv, o, d, tmax, work, leaf);
   }
 #ifdef RT_STAMPS
   if (any_need) RT_ACC(work, 6, tv);

@@ -475,6 +475,9 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   BvhArgs bv = bv_in;
   stage_scene<kLdsGeo>(smem, geo, radius, lights, n, nl, bv, g, rad, slight);
   const size_t stack_off = (lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31;
+  // the ordered BVH walk's per-lane stack (one-wave workgroups without a staged scene)
+  if (!kLdsGeo && kStack == kStackGlobal && bv.ordered)
+    bv.ostk = reinterpret_cast<int2 *>(smem + stack_off) + (size_t)(threadIdx.x >> 6) * kOrderedStack * 64;
   constexpr int kWg = wg_waves<kLdsGeo, kStack>();
   constexpr int kWx = kWg == 4 ? 2 : 1;
   const int wave = threadIdx.x >> 6;
@@ -593,6 +596,8 @@ struct rt_ctx {
   BvhNode *d_bvh = nullptr;
   int32_t *d_prims = nullptr;
   float4 *d_pf = nullptr;
+  BvhNode2 *d_bvh2 = nullptr;
+  int bvh2_root = -1, bvh_depth = 0, bvh_ordered = 1;  // RT_HIP_BVH_ORDERED
   int bvh_nodes = 0;
   // per-light direction grids for shadow rays (rt_lightgrid.h), built at upload
   int32_t *d_lg_start = nullptr, *d_lg_ids = nullptr;
@@ -659,6 +664,8 @@ void free_scene(rt_ctx *c) {
   if (c->d_prims) (void)hipFree(c->d_prims);
   if (c->d_pf) (void)hipFree(c->d_pf);
   c->d_pf = nullptr;
+  if (c->d_bvh2) (void)hipFree(c->d_bvh2);
+  c->d_bvh2 = nullptr;
   if (c->d_lg_start) (void)hipFree(c->d_lg_start);
   if (c->d_lg_ids) (void)hipFree(c->d_lg_ids);
   c->d_lg_start = c->d_lg_ids = nullptr;
@@ -679,6 +686,10 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   b.nodes = c->d_bvh;
   b.prims = c->d_prims;
   b.pf = c->d_pf;
+  b.n2 = c->d_bvh2;
+  b.root_ref = c->bvh2_root;
+  b.ordered = (c->bvh_ordered && c->d_bvh2 && c->bvh_depth <= kOrderedStack) ? 1 : 0;
+  b.ostk = nullptr;  // set in the kernel (LDS)
   b.nnodes = (c->bvh_on && c->cull) ? c->bvh_nodes : 0;
   b.c0x = c->c0[0];
   b.c0y = c->c0[1];
@@ -726,6 +737,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   lds = ((lds + 31) & ~(size_t)31) +
         (kStack == kStackCompact ? kLdsCompactBytes : kStack == kStackLds ? kLdsStackBytes : 0);
+  if (!kLds && kStack == kStackGlobal && bvh_args(c, cam).ordered)
+    lds += (size_t)kWg * kOrderedStack * 64 * sizeof(int2);
   StackEnt *gstack = nullptr;
   if (kStack != kStackLds && depth > 1) {
     const size_t need = (size_t)(depth - 1) * rows.count * od.xw * sizeof(StackEnt);
@@ -981,6 +994,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_PERSIST")) c->persist = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_STACK")) c->stack_mode = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_XCD_MAP")) c->xcd_map = std::max(0, std::atoi(e));
+  if (const char *e = std::getenv("RT_HIP_BVH_ORDERED")) c->bvh_ordered = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n = std::max(1, std::min(256, std::atoi(e)));
   auto bail = [&](int rc) {
@@ -1095,9 +1109,15 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     if ((double)rr < std::fabs(br[id])) rr = std::nextafter(rr, INFINITY);
     pf[k] = make_float4((float)bx[id], (float)by[id], (float)bz[id], rr);
   }
+  std::vector<BvhNode2> nodes2;
+  int depth2 = 0;
+  const int32_t root2 = build_bvh2(nodes, nodes2, depth2);
   int rc = RT_OK;
   hipError_t e = hipSuccess;
-  if ((e = hipMalloc(&c->d_pf, sizeof(float4) * (pf.size() + 1))) != hipSuccess ||
+  if ((e = hipMalloc(&c->d_bvh2, sizeof(BvhNode2) * (nodes2.size() + 1))) != hipSuccess ||
+      (!nodes2.empty() && (e = hipMemcpy(c->d_bvh2, nodes2.data(), sizeof(BvhNode2) * nodes2.size(),
+                                         hipMemcpyHostToDevice)) != hipSuccess) ||
+      (e = hipMalloc(&c->d_pf, sizeof(float4) * (pf.size() + 1))) != hipSuccess ||
       (!pf.empty() && (e = hipMemcpy(c->d_pf, pf.data(), sizeof(float4) * pf.size(), hipMemcpyHostToDevice)) !=
                           hipSuccess) ||
       (e = hipMalloc(&c->d_bvh, sizeof(BvhNode) * (nodes.size() + 1))) != hipSuccess ||
@@ -1115,6 +1135,8 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     return rc;
   }
   c->bvh_nodes = (int)nodes.size();
+  c->bvh2_root = root2;
+  c->bvh_depth = depth2;
   {
     double d2 = 0.0;
     for (int k = 0; k < 3; k++) d2 += (hi[k] - lo[k]) * (hi[k] - lo[k]);

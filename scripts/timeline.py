@@ -46,7 +46,7 @@ sys.path.insert(0, os.path.join(REPO, "cs420-ray-tracer_amd"))
 import rt_hip  # noqa: E402
 
 scene = sys.argv[1] if len(sys.argv) > 1 else "synth200"
-W, H, D = 1920, 1080, 4
+W, H, D = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080, 4)
 sc = rt_hip.Scene.load(os.path.join(REPO, "cs420-ray-tracer_amd", "scenes", scene + ".txt"))
 r = rt_hip.Renderer(0)
 r.upload(sc)

@@ -441,3 +441,28 @@ def test_stack_modes_depth_edges(stack_renderer, depth):
         y = (k // 8) * 8 * 3 + 8 + k % 8
         if y < H:
             assert np.array_equal(got[k], want[y])
+
+
+@pytest.mark.parametrize("ordered", ["1", "0"])
+@pytest.mark.parametrize("seed,count", [(101, 700), (102, 1100), (103, 1600)])
+def test_large_scenes_global_memory_paths(monkeypatch, ordered, seed, count):
+    """Scenes too large for LDS (geometry and BVH read through L2, one-wave
+    workgroups): the ordered BVH walk (RT_HIP_BVH_ORDERED=1, default) and the
+    stackless one against the oracle."""
+    import orc
+    import rt_hip
+
+    monkeypatch.setenv("RT_HIP_BVH_ORDERED", ordered)
+    r = rt_hip.Renderer(0)
+    try:
+        text = _random_scene(seed, count)
+        W, H, D = 96, 64, 5
+        sc = rt_hip.Scene.parse(text)
+        r.upload(sc)
+        ref, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=8)
+        rgb, st = r.render(sc.camera(), W, H, D)
+        assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
+        assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
+                                                                       counts["reflect"])
+    finally:
+        r.close()
