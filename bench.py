@@ -103,29 +103,35 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     r.set_stream(stream.cuda_stream)  # the kernel runs on torch's stream: events and RCCL order with it
     rows = rt_hip.rows_for_shard(H, BAND, rank, world) if world > 1 else rt_hip.rt_rows(1, 0, 1, H)
     R = rows.count
-    shard = torch.empty((R, W, 3), dtype=torch.uint8, device=f"cuda:{device}")
+    # two shard / gather buffers: frame i renders while frame i-1 is gathered (rt_frames)
+    shards = [torch.empty((R, W, 3), dtype=torch.uint8, device=f"cuda:{device}") for _ in range(2)]
     gathered = image = None
     if world > 1 and rank == 0:
-        gathered = torch.empty((world, R, W, 3), dtype=torch.uint8, device=f"cuda:{device}")
+        gathered = [list(torch.empty((world, R, W, 3), dtype=torch.uint8, device=f"cuda:{device}").unbind(0))
+                    for _ in range(2)]
         image = torch.empty((H, W, 3), dtype=torch.uint8, device=f"cuda:{device}")
 
-    def step():
+    def render(shard):
         r.render_async(cam, W, H, D, rows, shard.data_ptr())
-        if world > 1:
-            dist.gather(shard, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                r.unpermute(gathered.data_ptr(), image.data_ptr(), W, H, BAND, world, R)
 
-    for _ in range(warmup):
-        step()
+    def unpermute(g):
+        r.unpermute(g[0].data_ptr(), image.data_ptr(), W, H, BAND, world, R)  # g: views of one buffer
+
+    def frames(n):
+        if world > 1:
+            rt_frames.run_frames(dist, n, rank, render, shards, gathered, unpermute if rank == 0 else None)
+        else:
+            for i in range(n):
+                render(shards[i & 1])
+
+    frames(warmup)
     st = r.stats()  # syncs; ray counts of this rank's shard (identical every step)
     r.kernel_times()  # drop warmup launches from the history
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    frames(steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -167,6 +173,7 @@ def main():
     world, rank, local = dist_env()
     import torch  # loads torch's HIP runtime first; librt_hip.so binds to it
     import torch.distributed as dist
+    import rt_frames
     import rt_hip
 
     torch.cuda.set_device(local)

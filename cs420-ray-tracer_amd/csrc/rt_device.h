@@ -296,6 +296,7 @@ struct BvhArgs {
   const BvhNode2 *n2;
   int root_ref;
   int ordered;  // the host allows the ordered walk (tree depth <= kOrderedStack)
+  int odepth;   // stack entries per lane (the tree depth)
   int2 *ostk;
 };
 constexpr int kOrderedStack = 24;  // pending far children; the host requires depth <= this

@@ -345,31 +345,47 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
     acc = kSamples == 1 ? c : add(acc, c);  // serial: the colour itself; AA: from 0 in sample order (main_gpu.cu:250, 327)
   }
   const D3 res = kSamples == 4 ? scale(acc, 0.25) : acc;  // main_gpu.cu:331, 1/4 is exact
-  if (in_tile) {
-    if (od.fmt == RT_FB_RGB8) {
-      uint8_t *px = static_cast<uint8_t *>(od.ptr) + ((size_t)(od.full ? y : k) * W + x) * 3;
-      if (in_img) {
-        const int q0 = quantize(res.x), q1 = quantize(res.y), q2 = quantize(res.z);
-        c_neg = (q0 < 0) + (q1 < 0) + (q2 < 0);
-        px[0] = (uint8_t)(q0 < 0 ? 0 : q0);
-        px[1] = (uint8_t)(q1 < 0 ? 0 : q1);
-        px[2] = (uint8_t)(q2 < 0 ? 0 : q2);
-      } else if (!od.full) {
-        px[0] = px[1] = px[2] = 0;
+  if (od.fmt == RT_FB_RGB8) {
+    // RGB8: a tile row of 8 pixels is 24 contiguous bytes.  When the whole row
+    // is written and dword aligned, lanes 0-5 of the row store it as 6 dwords
+    // assembled with two shuffles; otherwise every lane stores its 3 bytes.
+    unsigned v = 0;  // r | g << 8 | b << 16
+    if (in_img) {
+      const int q0 = quantize(res.x), q1 = quantize(res.y), q2 = quantize(res.z);
+      c_neg = (q0 < 0) + (q1 < 0) + (q2 < 0);
+      v = (unsigned)(q0 < 0 ? 0 : q0) | (unsigned)(q1 < 0 ? 0 : q1) << 8 | (unsigned)(q2 < 0 ? 0 : q2) << 16;
+    }
+    const bool put = in_tile && (in_img || !od.full);  // padding rows of a shard are zero-filled
+    const int c = lane & 7, rb = lane & ~7;
+    const unsigned long long rowmask = 0xFFull << rb;
+    const bool whole = (__ballot(put) & rowmask) == rowmask;
+    uint8_t *row = static_cast<uint8_t *>(od.ptr) + ((size_t)(od.full ? y : k) * W + (x - c)) * 3;
+    const bool packed = whole && ((reinterpret_cast<uintptr_t>(row) & 3u) == 0);
+    const int p0 = (4 * c) / 3;  // dword c holds bytes 4c..4c+3: pixels p0, p0+1
+    const unsigned v0 = __shfl(v, rb + (p0 < 7 ? p0 : 7), 64), v1 = __shfl(v, rb + (p0 + 1 < 7 ? p0 + 1 : 7), 64);
+    if (packed) {
+      if (c < 6) {
+        const unsigned long long both = (unsigned long long)v0 | (unsigned long long)v1 << 24;
+        reinterpret_cast<unsigned *>(row)[c] = (unsigned)(both >> (8 * (4 * c - 3 * p0)));
       }
-    } else if (in_img) {
-      const size_t i = ((size_t)j * W + x) * 3;
-      if (od.fmt == RT_FB_F64X3) {
-        double *f = static_cast<double *>(od.ptr) + i;
-        f[0] = res.x;
-        f[1] = res.y;
-        f[2] = res.z;
-      } else {
-        float *f = static_cast<float *>(od.ptr) + i;
-        f[0] = (float)res.x;
-        f[1] = (float)res.y;
-        f[2] = (float)res.z;
-      }
+    } else if (put) {
+      uint8_t *px = row + c * 3;
+      px[0] = (uint8_t)v;
+      px[1] = (uint8_t)(v >> 8);
+      px[2] = (uint8_t)(v >> 16);
+    }
+  } else if (in_tile && in_img) {
+    const size_t i = ((size_t)j * W + x) * 3;
+    if (od.fmt == RT_FB_F64X3) {
+      double *f = static_cast<double *>(od.ptr) + i;
+      f[0] = res.x;
+      f[1] = res.y;
+      f[2] = res.z;
+    } else {
+      float *f = static_cast<float *>(od.ptr) + i;
+      f[0] = (float)res.x;
+      f[1] = (float)res.y;
+      f[2] = (float)res.z;
     }
   }
   sums[0] += wave_sum(c_prim);
@@ -475,9 +491,9 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   BvhArgs bv = bv_in;
   stage_scene<kLdsGeo>(smem, geo, radius, lights, n, nl, bv, g, rad, slight);
   const size_t stack_off = (lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31;
-  // the ordered BVH walk's per-lane stack (one-wave workgroups without a staged scene)
-  if (!kLdsGeo && kStack == kStackGlobal && bv.ordered)
-    bv.ostk = reinterpret_cast<int2 *>(smem + stack_off) + (size_t)(threadIdx.x >> 6) * kOrderedStack * 64;
+  // the ordered BVH walk's per-lane stacks, [wave][entry][lane], after the scene
+  if (kStack == kStackGlobal && bv.ordered)
+    bv.ostk = reinterpret_cast<int2 *>(smem + stack_off) + (size_t)(threadIdx.x >> 6) * bv.odepth * 64;
   constexpr int kWg = wg_waves<kLdsGeo, kStack>();
   constexpr int kWx = kWg == 4 ? 2 : 1;
   const int wave = threadIdx.x >> 6;
@@ -682,15 +698,16 @@ void free_scene(rt_ctx *c) {
 // BVH arguments for one render: the scene extent includes the camera (the
 // origin of primary rays); margin = 1e-6 * (diameter + largest radius).
 BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
-  BvhArgs b;
+  BvhArgs b{};
   b.nodes = c->d_bvh;
   b.prims = c->d_prims;
   b.pf = c->d_pf;
   b.n2 = c->d_bvh2;
   b.root_ref = c->bvh2_root;
-  b.ordered = (c->bvh_ordered && c->d_bvh2 && c->bvh_depth <= kOrderedStack) ? 1 : 0;
-  b.ostk = nullptr;  // set in the kernel (LDS)
   b.nnodes = (c->bvh_on && c->cull) ? c->bvh_nodes : 0;
+  b.ordered = (c->bvh_ordered && c->d_bvh2 && c->bvh_depth <= kOrderedStack && b.nnodes > 0) ? 1 : 0;
+  b.odepth = std::max(1, c->bvh_depth);
+  b.ostk = nullptr;  // set in the kernel (LDS)
   b.c0x = c->c0[0];
   b.c0y = c->c0[1];
   b.c0z = c->c0[2];
@@ -712,7 +729,7 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
 }
 
 LgArgs lg_args(const rt_ctx *c) {
-  LgArgs g;
+  LgArgs g{};
   g.start = c->d_lg_start;
   g.ids = c->d_lg_ids;
   g.N = c->lg_n;
@@ -737,8 +754,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   lds = ((lds + 31) & ~(size_t)31) +
         (kStack == kStackCompact ? kLdsCompactBytes : kStack == kStackLds ? kLdsStackBytes : 0);
-  if (!kLds && kStack == kStackGlobal && bvh_args(c, cam).ordered)
-    lds += (size_t)kWg * kOrderedStack * 64 * sizeof(int2);
+  // the kernel places the ordered walk's stacks from these same arguments
+  if (kStack == kStackGlobal && bv.ordered) lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
   StackEnt *gstack = nullptr;
   if (kStack != kStackLds && depth > 1) {
     const size_t need = (size_t)(depth - 1) * rows.count * od.xw * sizeof(StackEnt);
@@ -890,7 +907,7 @@ int launch_wavefront2(rt_ctx *c, WfArgs &a, size_t lds) {
 
 int launch_wavefront(rt_ctx *c, const Cam &cam, int W, int H, int depth, const Rows &r, uint8_t *dst, bool lds_geo,
                      size_t lds) {
-  WfArgs a;
+  WfArgs a{};
   a.geo = c->d_geo;
   a.rad = c->d_rad;
   a.mat = c->d_mat;

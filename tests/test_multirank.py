@@ -73,3 +73,62 @@ def test_gloo_gather_reassembles_golden(world, name):
         assert p.exitcode == 0
     assert img == golden_rgb(name)
     assert rays == sum(manifest()[name]["rays"].values())
+
+
+def _pipelined_worker(rank, world, port, q):
+    """bench.py's pipelined frame loop (rt_frames.run_frames) under gloo: frame f
+    of rank r fills its shard with (f, r, row); every reassembled frame must be
+    exact and arrive in order."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import rt_frames
+
+    W, H, band, steps = 5, 37, 8, 7
+    import rt_hip
+
+    rows = rt_hip.rows_for_shard(H, band, rank, world)
+    R = rows.count
+    shards = [torch.zeros((R, W, 3), dtype=torch.uint8) for _ in range(2)]
+    gathered = ([list(torch.zeros((world, R, W, 3), dtype=torch.uint8).unbind(0)) for _ in range(2)]
+                if rank == 0 else None)
+    frame = [0]
+    seen = []
+
+    def render(shard):
+        f = frame[0]
+        for k in range(R):
+            shard[k] = (f * 16 + rank * 4 + k % 4) % 256
+        frame[0] += 1
+
+    def unpermute(g):
+        img = unpermute_host(torch.stack(g).numpy(), H, band)
+        seen.append(img[:, 0, 0].tolist())
+
+    rt_frames.run_frames(dist, steps, rank, render, shards, gathered, unpermute if rank == 0 else None)
+    if rank == 0:
+        q.put(seen)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_pipelined_frames(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    seen = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    H, band = 37, 8
+    assert len(seen) == 7
+    for f, col in enumerate(seen):
+        want = []
+        for y in range(H):
+            b = y // band
+            r, k = b % world, (b // world) * band + y % band
+            want.append((f * 16 + r * 4 + k % 4) % 256)
+        assert col == want, f
