@@ -977,9 +977,7 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
   }
   RT_TRY(c, hipEventRecord(c->ev1[slot], c->stream));
   c->launches++;
-  RT_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, kShards * kShardStride * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                           c->stream));
-  return RT_OK;
+  return RT_OK;  // the counters are read back by rt_render_stats, after the stream drains
 }
 
 }  // namespace
@@ -1233,6 +1231,8 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
     const int slot = (int)((c->launches - 1) % rt_ctx::kRing);
     RT_TRY(c, hipEventElapsedTime(&ms, c->ev0[slot], c->ev1[slot]));
   }
+  RT_TRY(c, hipMemcpy(c->h_counters, c->d_counters, kShards * kShardStride * sizeof(unsigned long long),
+                      hipMemcpyDeviceToHost));
   unsigned long long sum[kCounters] = {};
   for (int sh = 0; sh < kShards; sh++)
     for (int q = 0; q < kCounters; q++) sum[q] += c->h_counters[sh * kShardStride + q];
