@@ -298,18 +298,28 @@ struct CompactArgs {
   int *qcnt;         // LDS
   TermRec *term;     // LDS
 };
+// kStackSplit: level 0 here, the reflection levels through the ray queues of
+// rt_wavefront.h (wf_bounce), the unwind in wf_resolve.
+struct SplitArgs {
+  RayRec *rayq;       // [kShards][seg_cap]
+  unsigned *ray_cnt;  // [depth+1][kShards]
+  int seg_cap;
+  Term *term;         // [npx]
+  uint8_t *nlev;      // [npx]
+};
 
 // Reflection stack placement: kStackLds = [level][lane] per wave in LDS (4
 // levels), kStackGlobal = [level][pixel] in global memory (any depth),
 // kStackCompact = global, with the workgroup-compacted levels of trace_compact.
-enum { kStackLds = 0, kStackGlobal = 1, kStackCompact = 2 };
+// kStackSplit = level 0 only, the rest queued (SplitArgs).
+enum { kStackLds = 0, kStackGlobal = 1, kStackCompact = 2, kStackSplit = 3 };
 template <bool kCull, int kSamples, int kStack>
 __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                            const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                            int nl, D3 amb, const Cam &cam, int W, int H, int depth, const Rows &rows,
                                            const BvhArgs &bv, const LgArgs &lg, const OutDesc &od, int x0, int k0,
-                                           StackEnt *stk, const CompactArgs &ca, Work &work,
-                                           unsigned long long (&sums)[4]) {
+                                           StackEnt *stk, const CompactArgs &ca, const SplitArgs &sa,
+                                           Work &work, unsigned long long (&sums)[4]) {
   const int lane = threadIdx.x & 63;
   const int x = x0 + (lane & 7);
   const int k = k0 + (lane >> 3);
@@ -333,7 +343,30 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
     const D3 o = mk(cam.px, cam.py, cam.pz);
     D3 c;
     const int pix = k * od.xw + (x - od.x0);
-    if (kStack == kStackCompact)
+    if (kStack == kStackSplit) {  // level 0; spawned rays go to the level-1 queue
+      const bool alive = in_img && depth >= 1;
+      c_prim += alive ? 1u : 0u;
+      int outcome = 0, nkey = 0;
+      D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;  // depth <= 0 -> black (main.cpp:17-18)
+      double refl = 0.0;
+      if (__ballot(alive))
+        bounce<kCull>(g, rad, mat, slight, n, nl, amb, bv, lg, alive, o, d, -1, depth, work, c_shadow, outcome,
+                      color, refl, no, nd, nkey);
+      const bool spawn = alive && outcome == kSpawned;
+      if (in_img && !spawn) {
+        sa.term[pix] = Term{color.x, color.y, color.z};
+        sa.nlev[pix] = 0;
+      }
+      if (spawn) {
+        ca.gstack[pix] = StackEnt{color.x, color.y, color.z, refl};
+        ++c_reflect;
+      }
+      const unsigned shard = blockIdx.x % kShards;
+      const unsigned slot = wave_append(spawn, &sa.ray_cnt[1 * kShards + shard]);
+      if (spawn)
+        sa.rayq[(size_t)shard * sa.seg_cap + slot] = RayRec{no.x, no.y, no.z, nd.x, nd.y, nd.z, pix, depth - 1, nkey, 0};
+      c = color;
+    } else if (kStack == kStackCompact)
       c = trace_compact<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, pix, ca.gstack, ca.npx,
                                ca.q, ca.qcnt, ca.term, work, c_prim, c_shadow, c_reflect);
     else if (kStack == kStackGlobal)
@@ -345,7 +378,9 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
     acc = kSamples == 1 ? c : add(acc, c);  // serial: the colour itself; AA: from 0 in sample order (main_gpu.cu:250, 327)
   }
   const D3 res = kSamples == 4 ? scale(acc, 0.25) : acc;  // main_gpu.cu:331, 1/4 is exact
-  if (od.fmt == RT_FB_RGB8) {
+  if (kStack == kStackSplit) {
+    // the colour is written by wf_resolve once the queued levels are done
+  } else if (od.fmt == RT_FB_RGB8) {
     // RGB8: a tile row of 8 pixels is 24 contiguous bytes.  When the whole row
     // is written and dword aligned, lanes 0-5 of the row store it as 6 dwords
     // assembled with two shuffles; otherwise every lane stores its 3 bytes.
@@ -458,7 +493,7 @@ constexpr int kWaves = 4;  // 2x2 tiles of 8x8 pixels per workgroup (persistent 
 // no wave's slot waits for its slowest neighbour.
 template <bool kLdsGeo, int kStack>
 constexpr int wg_waves() {
-  return (kLdsGeo || kStack != 1) ? 4 : 1;
+  return (kLdsGeo || (kStack != 1 && kStack != 3)) ? 4 : 1;
 }
 // LDS after the staged scene: the 4-level reflection stack per wave, or
 // (kCompact) the workgroup's ray queue, terminal colours and queue count.
@@ -470,7 +505,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
     const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
     const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
     BvhArgs bv_in, LgArgs lg, OutDesc od, StackEnt *__restrict__ gstack, unsigned long long *__restrict__ counters,
-    int ntx, int ntiles, int xcd_per) {  // xcd_per: tiles per run
+    int ntx, int ntiles, int xcd_per, SplitArgs sa) {  // xcd_per: tiles per run
   // 16x16-pixel workgroup tile.  Workgroups are dealt to the 8 XCDs round
   // robin (b % 8).  With chunk > 0 the scanline-ordered tiles are cut into
   // runs of `chunk` tiles and run r goes to XCD r % 8: each XCD's L2 serves
@@ -492,7 +527,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   stage_scene<kLdsGeo>(smem, geo, radius, lights, n, nl, bv, g, rad, slight);
   const size_t stack_off = (lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31;
   // the ordered BVH walk's per-lane stacks, [wave][entry][lane], after the scene
-  if (kStack == kStackGlobal && bv.ordered)
+  if ((kStack == kStackGlobal || kStack == kStackSplit) && bv.ordered)
     bv.ostk = reinterpret_cast<int2 *>(smem + stack_off) + (size_t)(threadIdx.x >> 6) * bv.odepth * 64;
   constexpr int kWg = wg_waves<kLdsGeo, kStack>();
   constexpr int kWx = kWg == 4 ? 2 : 1;
@@ -512,12 +547,69 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
 #endif
   trace_tile<kCull, kSamples, kStack>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
                                         od.x0 + tx * (8 * kWx) + (wave % kWx) * 8,
-                                        ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, work, sums);
+                                        ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, sa, work, sums);
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
   record_timeline(tile * kWg + wave, t_real0, work);
 #endif
   flush_counts(counters, sums, work);
+}
+
+// Reflection level `level` of the split pipeline (RT_HIP_PIPELINE=3): one
+// lane per queued ray, a persistent grid-stride loop over the level's queue
+// segment (workgroup b serves segment b % kShards), the megakernel's bounce()
+// with its ordered BVH walk.  Level L reads ray buffer L & 1 and appends the
+// rays it spawns to buffer (L + 1) & 1; a chain that ends writes its colour
+// and level count for wf_resolve.
+template <bool kLdsGeo, bool kCull>
+__global__ __launch_bounds__(256) void wf_bounce(WfArgs a, int level) {
+  const unsigned shard = blockIdx.x % kShards, j = blockIdx.x / kShards, nj = gridDim.x / kShards;
+  const unsigned cnt = a.ray_cnt[level * kShards + shard];
+  if (j * 256u >= cnt) return;  // workgroup-uniform, before any barrier
+  RayRec *const bufs[2] = {a.rayq, reinterpret_cast<RayRec *>(a.hitq)};
+  const RayRec *__restrict__ rq = bufs[level & 1] + (size_t)shard * a.seg_cap;
+  RayRec *__restrict__ wq = bufs[(level + 1) & 1] + (size_t)shard * a.seg_cap;
+  extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
+  const SphGeo *g;
+  const double *rad;
+  const LightD *lights;
+  BvhArgs bv;
+  stage<kLdsGeo>(a, smem, g, rad, lights, bv);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (bv.ordered)
+    bv.ostk = reinterpret_cast<int2 *>(smem + ((lds_layout(kLdsGeo, a.n, a.nl, a.bv.nnodes).end + 31) & ~(size_t)31)) +
+              (size_t)wave * bv.odepth * 64;
+  Work work;
+  unsigned c_shadow = 0, c_reflect = 0;
+  const unsigned stride = nj * 256u;
+  for (unsigned base = j * 256u + wave * 64u; base < cnt; base += stride) {
+    const unsigned idx = base + lane;
+    const bool act = idx < cnt;
+    const RayRec r = rq[act ? idx : base];
+    int outcome = 0, nkey = 0;
+    D3 color = mk(0.0, 0.0, 0.0), no = mk(r.ox, r.oy, r.oz), nd = mk(r.dx, r.dy, r.dz);
+    double refl = 0.0;
+    bounce<kCull>(g, rad, a.mat, lights, a.n, a.nl, a.amb, bv, a.lg, act, mk(r.ox, r.oy, r.oz),
+                  mk(r.dx, r.dy, r.dz), r.key, r.dleft, work, c_shadow, outcome, color, refl, no, nd, nkey);
+    const bool spawn = act && outcome == kSpawned;
+    if (act && !spawn) {
+      a.term[r.pix] = Term{color.x, color.y, color.z};
+      a.nlev[r.pix] = (uint8_t)level;
+    }
+    if (spawn) {
+      a.stack[(size_t)level * a.npx + r.pix] = StackEnt{color.x, color.y, color.z, refl};
+      ++c_reflect;
+    }
+    const unsigned slot = wave_append(spawn, &a.ray_cnt[(level + 1) * kShards + shard]);
+    if (spawn) wq[slot] = RayRec{no.x, no.y, no.z, nd.x, nd.y, nd.z, r.pix, r.dleft - 1, nkey, 0};
+  }
+  const unsigned long long ss = wave_sum(c_shadow), sr = wave_sum(c_reflect);
+  if (lane == 0) {
+    unsigned long long *sc = counter_shard(a.counters);
+    if (ss) atomicAdd(&sc[1], ss);
+    if (sr) atomicAdd(&sc[2], sr);
+  }
+  flush_work(work, a.counters);
 }
 
 // Persistent variant: a resident grid whose waves take 8x8 tiles from 64
@@ -572,7 +664,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_PERSIST_WAVES_PER_EU) void render_p
     pending = fetch(shard);
     const int ty = (int)(tile / ntx), tx = (int)(tile % ntx);
     trace_tile<kCull, kSamples, kStackLds>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
-                                           od.x0 + tx * 8, ty * 8, stk, CompactArgs{}, work, sums);
+                                           od.x0 + tx * 8, ty * 8, stk, CompactArgs{}, SplitArgs{}, work, sums);
   }
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
@@ -740,7 +832,7 @@ LgArgs lg_args(const rt_ctx *c) {
 
 template <bool kLds, bool kCull, int kSamples, int kStack>
 int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                 const OutDesc &od) {
+                 const OutDesc &od, const SplitArgs &sa = SplitArgs{}, StackEnt *split_stack = nullptr) {
   const BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
   constexpr int kWg = wg_waves<kLds, kStack>(), kWx = kWg == 4 ? 2 : 1, kWy = kWg / kWx;
@@ -755,9 +847,10 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   lds = ((lds + 31) & ~(size_t)31) +
         (kStack == kStackCompact ? kLdsCompactBytes : kStack == kStackLds ? kLdsStackBytes : 0);
   // the kernel places the ordered walk's stacks from these same arguments
-  if (kStack == kStackGlobal && bv.ordered) lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
-  StackEnt *gstack = nullptr;
-  if (kStack != kStackLds && depth > 1) {
+  if ((kStack == kStackGlobal || kStack == kStackSplit) && bv.ordered)
+    lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
+  StackEnt *gstack = split_stack;
+  if (kStack != kStackLds && kStack != kStackSplit && depth > 1) {
     const size_t need = (size_t)(depth - 1) * rows.count * od.xw * sizeof(StackEnt);
     if (c->cstack_bytes < need) {
       RT_TRY(c, hipStreamSynchronize(c->stream));
@@ -771,7 +864,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   }
   hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream,
                      c->d_geo, c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv,
-                     lg, od, gstack, c->d_counters, ntx, (int)ntiles, xcd_per);
+                     lg, od, gstack, c->d_counters, ntx, (int)ntiles, xcd_per, sa);
   return RT_OK;
 }
 
@@ -905,6 +998,37 @@ int launch_wavefront2(rt_ctx *c, WfArgs &a, size_t lds) {
   return RT_OK;
 }
 
+// RT_HIP_PIPELINE=3: level 0 in the megakernel (coherent tiles), reflection
+// levels through the ray queues with wf_bounce, the unwind in wf_resolve.
+template <bool kLds, bool kCull>
+int launch_split(rt_ctx *c, WfArgs &a, const Cam &cam, size_t lds) {
+  SplitArgs sa;
+  sa.rayq = reinterpret_cast<RayRec *>(a.hitq);  // level 1 reads buffer 1
+  sa.ray_cnt = a.ray_cnt;
+  sa.seg_cap = a.seg_cap;
+  sa.term = a.term;
+  sa.nlev = a.nlev;
+  int rc = launch_tiles<kLds, kCull, 1, kStackSplit>(c, lds, cam, a.W, a.H, a.depth, a.rows,
+                                                     OutDesc{a.out, RT_FB_RGB8, 0, 0, a.W}, sa, a.stack);
+  if (rc != RT_OK) return rc;
+  static int blocks_per_cu = 0;
+  size_t blds = ((lds + 31) & ~(size_t)31);
+  if (a.bv.ordered) blds += (size_t)4 * a.bv.odepth * 64 * sizeof(int2);
+  if (blocks_per_cu == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, wf_bounce<kLds, kCull>, 256, blds) != hipSuccess || nb < 1)
+      nb = 2;
+    blocks_per_cu = nb;
+  }
+  const size_t want = ((size_t)a.npx + 255) / 256, resident = (size_t)c->n_cu * blocks_per_cu;
+  const size_t per_shard = std::max<size_t>(1, (std::min(want, resident) + kShards - 1) / kShards);
+  for (int level = 1; level < a.depth; ++level)
+    hipLaunchKernelGGL((wf_bounce<kLds, kCull>), dim3((unsigned)(per_shard * kShards)), dim3(256), blds, c->stream, a,
+                       level);
+  hipLaunchKernelGGL(wf_resolve, dim3((a.W + 63) / 64, (a.rows.count + 3) / 4), dim3(256), 0, c->stream, a);
+  return RT_OK;
+}
+
 int launch_wavefront(rt_ctx *c, const Cam &cam, int W, int H, int depth, const Rows &r, uint8_t *dst, bool lds_geo,
                      size_t lds) {
   WfArgs a{};
@@ -932,6 +1056,10 @@ int launch_wavefront(rt_ctx *c, const Cam &cam, int W, int H, int depth, const R
   const size_t seg_cap = std::max((wgs16 + kShards - 1) / kShards * 256, (wgs8 + kShards - 1) / kShards * 64);
   int rc = ensure_wf(c, (size_t)a.npx, depth, seg_cap, a);
   if (rc != RT_OK) return rc;
+  if (c->pipeline == 3) {
+    if (lds_geo) return c->cull ? launch_split<true, true>(c, a, cam, lds) : launch_split<true, false>(c, a, cam, lds);
+    return c->cull ? launch_split<false, true>(c, a, cam, lds) : launch_split<false, false>(c, a, cam, lds);
+  }
   if (lds_geo) return c->cull ? launch_wavefront2<true, true>(c, a, lds) : launch_wavefront2<true, false>(c, a, lds);
   return c->cull ? launch_wavefront2<false, true>(c, a, lds) : launch_wavefront2<false, false>(c, a, lds);
 }
@@ -1000,7 +1128,7 @@ int rt_create(int device, rt_ctx **out) {
   if (device < 0 || device >= n) return RT_ERR_INVALID_ARG;
   rt_ctx *c = new rt_ctx();
   c->device = device;
-  if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::max(0, std::min(2, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::max(0, std::min(3, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_BVH")) c->bvh_on = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_MIN")) c->bvh_min = std::atoi(e);
   if (const char *e = std::getenv("RT_HIP_BVH_ALWAYS")) c->bvh_always = std::atoi(e) != 0;

@@ -326,10 +326,11 @@ def test_bvh_far_from_origin(bvh_renderer):
     assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
 
 
-@pytest.fixture(params=["1", "2"], ids=["queues", "hybrid"])
+@pytest.fixture(params=["1", "2", "3"], ids=["queues", "hybrid", "split"])
 def pipeline_renderer(request, monkeypatch):
     """The queue-based pipelines (RT_HIP_PIPELINE=1: every level through the
-    ray/hit queues; 2: fused coherent level 0, queues from level 1 on)."""
+    ray/hit queues; 2: fused coherent level 0, queues from level 1 on; 3: the
+    megakernel's level 0, then wf_bounce per level over the ray queues)."""
     import rt_hip
 
     monkeypatch.setenv("RT_HIP_PIPELINE", request.param)
