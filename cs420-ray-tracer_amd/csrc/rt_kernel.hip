@@ -146,12 +146,14 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
 
 // trace_ray for one camera ray per lane, the wave walking the levels together
 // (lanes masked by `alive`); the lane's reflection stack entries are
-// stk[level * sstride] (depth - 1 levels), unwound innermost first.
+// sbase[sidx + level * sstride] (depth - 1 levels), unwound innermost first.
+// The wave-uniform base and a 32-bit lane index (not a per-lane 64-bit
+// pointer) keep the stack address out of the registers that spill.
 template <bool kCull>
 __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                          const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                          int nl, D3 amb, int depth, const BvhArgs &bv, const LgArgs &lg, bool live,
-                                         D3 o, D3 d, StackEnt *stk, size_t sstride, Work &work, unsigned &c_prim,
+                                         D3 o, D3 d, StackEnt *sbase, unsigned sidx, unsigned sstride, Work &work, unsigned &c_prim,
                                          unsigned &c_shadow, unsigned &c_reflect) {
   int lev = 0;
   int dleft = depth;
@@ -167,7 +169,7 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
                   refl, no, nd, nkey);
     if (alive) {
       if (outcome == kSpawned) {
-        stk[lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
+        sbase[sidx + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
         ++lev;
         o = no;
         d = nd;
@@ -182,7 +184,7 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
   }
   while (lev > 0) {  // unwind: shade*(1-refl) + reflected*refl, innermost first
     --lev;
-    const StackEnt e = stk[lev * sstride];
+    const StackEnt e = sbase[sidx + (unsigned)lev * sstride];
     res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
   }
   return res;
@@ -370,14 +372,25 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
       c = trace_compact<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, pix, ca.gstack, ca.npx,
                                ca.q, ca.qcnt, ca.term, work, c_prim, c_shadow, c_reflect);
     else if (kStack == kStackGlobal)
-      c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, ca.gstack + pix, ca.npx,
+      c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, ca.gstack, (unsigned)pix, (unsigned)ca.npx,
                             work, c_prim, c_shadow, c_reflect);
     else
-      c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk + lane, 64, work,
+      c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk, (unsigned)lane, 64u, work,
                             c_prim, c_shadow, c_reflect);
     acc = kSamples == 1 ? c : add(acc, c);  // serial: the colour itself; AA: from 0 in sample order (main_gpu.cu:250, 327)
   }
   const D3 res = kSamples == 4 ? scale(acc, 0.25) : acc;  // main_gpu.cu:331, 1/4 is exact
+  // The pixel's coordinates are recomputed from the lane id (mbcnt) rather
+  // than kept live across the trace, which would spill them to scratch.
+  {
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const int x = x0 + (lane & 7);
+    const int k = k0 + (lane >> 3);
+    const bool in_tile = x < W && x < od.x0 + od.xw && k < rows.count;
+    const long long y = (long long)(k / rows.band) * rows.band * rows.stride + (long long)rows.first * rows.band +
+                        (k % rows.band);
+    const bool in_img = in_tile && y < H;
+    const int j = H - 1 - (int)(in_img ? y : 0);
   if (kStack == kStackSplit) {
     // the colour is written by wf_resolve once the queued levels are done
   } else if (od.fmt == RT_FB_RGB8) {
@@ -422,6 +435,7 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
       f[1] = (float)res.y;
       f[2] = (float)res.z;
     }
+  }
   }
   sums[0] += wave_sum(c_prim);
   sums[1] += wave_sum(c_shadow);
@@ -531,7 +545,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
     bv.ostk = reinterpret_cast<int2 *>(smem + stack_off) + (size_t)(threadIdx.x >> 6) * bv.odepth * 64;
   constexpr int kWg = wg_waves<kLdsGeo, kStack>();
   constexpr int kWx = kWg == 4 ? 2 : 1;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: keeps tile coordinates in SGPRs
   StackEnt *stk = reinterpret_cast<StackEnt *>(smem + stack_off) + (size_t)wave * kMaxLdsStack * 64;
   CompactArgs ca;
   ca.gstack = gstack;
@@ -851,6 +865,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
   StackEnt *gstack = split_stack;
   if (kStack != kStackLds && kStack != kStackSplit && depth > 1) {
+    // the kernel indexes the stack with 32 bits: entry + level * npx < 2^32
+    if ((unsigned long long)(depth - 1) * rows.count * od.xw >= (1ull << 32)) return RT_ERR_INVALID_ARG;
     const size_t need = (size_t)(depth - 1) * rows.count * od.xw * sizeof(StackEnt);
     if (c->cstack_bytes < need) {
       RT_TRY(c, hipStreamSynchronize(c->stream));
