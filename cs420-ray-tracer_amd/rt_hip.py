@@ -22,6 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(HERE, "librt_hip.so")
 
 RT_MAX_DEPTH = 64
+ABI_VERSION = 2  # RT_HIP_ABI_VERSION in include/rt_hip.h
 
 
 class RtError(RuntimeError):
