@@ -50,9 +50,48 @@ __device__ __forceinline__ D3 mul(D3 a, D3 b) { return mk(a.x * b.x, a.y * b.y, 
 __device__ __forceinline__ D3 scale(D3 a, double t) { return mk(a.x * t, a.y * t, a.z * t); }
 __device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ double length(D3 a) { return __builtin_sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+
+// (a.x / b, a.y / b, a.z / b), bit-identical to three IEEE divisions.  The
+// compiler lowers one fp64 division to v_div_scale (x2), v_rcp_f64, two
+// Newton steps on the reciprocal, q = x*r, e = fma(-b, q, x), v_div_fmas
+// (= fma(e, r, q) when no scaling was applied) and v_div_fixup (only the sign
+// and special values).  The reciprocal and its refinement depend on b alone,
+// so for three numerators they are computed once.  v_div_scale leaves both
+// operands unscaled (and VCC clear) exactly when b is a normal number whose
+// reciprocal is normal, x is 0 or neither tiny (exponent <= 53) nor 2^768
+// larger than b, and x/b is not subnormal; the guard below is a subset of
+// that (b in [2^-300, 2^300], x == 0 or |x| in [2^-600, 2^400]), and for it
+// v_div_fixup returns the fma result with the sign of x ^ b = the sign of x
+// (so 0/b keeps the sign of the zero).  Anything else -- zero, NaN, infinite
+// or extreme operands -- takes the ordinary divisions.
+#ifndef RT_FASTDIV
+#define RT_FASTDIV 0
+#endif
+__device__ __forceinline__ bool div_num_ok(double x) {
+  const double m = __builtin_fabs(x);
+  return x == 0.0 || (m >= 0x1p-600 && m <= 0x1p400);
+}
+__device__ __forceinline__ D3 div3(D3 a, double b) {
+#if RT_FASTDIV
+  if (__builtin_expect(b >= 0x1p-300 && b <= 0x1p300 && div_num_ok(a.x) && div_num_ok(a.y) && div_num_ok(a.z), 1)) {
+    double r = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    auto one = [&](double x) {
+      const double q = x * r;
+      const double res = __builtin_fma(-b, q, x);
+      return __builtin_copysign(__builtin_fma(res, r, q), x);
+    };
+    return mk(one(a.x), one(a.y), one(a.z));
+  }
+#endif
+  return mk(a.x / b, a.y / b, a.z / b);
+}
 __device__ __forceinline__ D3 normalized(D3 a) {
   double len = length(a);
-  return mk(a.x / len, a.y / len, a.z / len);
+  return div3(a, len);  // vec3.h:26-29: x/len, y/len, z/len
 }
 // ocml's fp64 pow needs ~50 VGPRs when inlined into the render loop; called
 // out of line it only adds its own frame where little of the caller is live.
@@ -423,8 +462,11 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
 // LDS layout of a staged scene: sphere geometry, radii, lights and, when the
 // scene is staged (lds_geo) and has a BVH, its nodes and leaf sphere indices.
 // The host sizes the dynamic LDS with the same function.
+#ifndef RT_MAT_LDS
+#define RT_MAT_LDS 0
+#endif
 struct LdsLayout {
-  size_t rad, light, nodes, pf, prims, end;
+  size_t rad, light, nodes, pf, prims, mat, end;
 };
 __host__ __device__ inline LdsLayout lds_layout(bool lds_geo, int n, int nl, int nnodes) {
   LdsLayout L;
@@ -438,16 +480,20 @@ __host__ __device__ inline LdsLayout lds_layout(bool lds_geo, int n, int nl, int
   if (bvh) e += (size_t)n * sizeof(float4);
   L.prims = e;
   if (bvh) e += (size_t)n * sizeof(int32_t);
+  // materials (read once per hit) after the BVH, when staged
+  L.mat = (e + 15) & ~(size_t)15;
+  if (lds_geo && RT_MAT_LDS) e = L.mat + (size_t)n * sizeof(SphMat);
   L.end = e;
   return L;
 }
 
-// Copies the scene (and, with kLdsGeo, its BVH) into LDS; g/rad/lights and
+// Copies the scene (and, with kLdsGeo, its BVH and materials) into LDS; g/rad/sm/lights and
 // bv.nodes/bv.prims then point at the LDS copies.  Ends with a barrier.
 template <bool kLdsGeo>
 __device__ __forceinline__ void stage_scene(unsigned char *smem, const SphGeo *geo, const double *radius,
-                                            const LightD *lights, int n, int nl, BvhArgs &bv, const SphGeo *&g,
-                                            const double *&rad, const LightD *&sl) {
+                                            const SphMat *mat, const LightD *lights, int n, int nl, BvhArgs &bv,
+                                            const SphGeo *&g, const double *&rad, const SphMat *&sm,
+                                            const LightD *&sl) {
   const LdsLayout L = lds_layout(kLdsGeo, n, nl, bv.nnodes);
   SphGeo *sgeo = reinterpret_cast<SphGeo *>(smem);
   double *srad = reinterpret_cast<double *>(smem + L.rad);
@@ -455,11 +501,13 @@ __device__ __forceinline__ void stage_scene(unsigned char *smem, const SphGeo *g
   BvhNode *snodes = reinterpret_cast<BvhNode *>(smem + L.nodes);
   int32_t *sprims = reinterpret_cast<int32_t *>(smem + L.prims);
   float4 *spf = reinterpret_cast<float4 *>(smem + L.pf);
+  SphMat *smat = reinterpret_cast<SphMat *>(smem + L.mat);
   const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
   if (kLdsGeo) {
     for (int i = tid; i < n; i += nt) {
       sgeo[i] = geo[i];
       srad[i] = radius[i];
+      if (RT_MAT_LDS) smat[i] = mat[i];
     }
     if (bv.nnodes > 0) {
       for (int i = tid; i < bv.nnodes; i += nt) snodes[i] = bv.nodes[i];
@@ -473,6 +521,7 @@ __device__ __forceinline__ void stage_scene(unsigned char *smem, const SphGeo *g
   __syncthreads();
   g = kLdsGeo ? sgeo : geo;
   rad = kLdsGeo ? srad : radius;
+  sm = (kLdsGeo && RT_MAT_LDS) ? smat : mat;
   sl = slight;
   if (kLdsGeo) {
     bv.nodes = snodes;

@@ -537,8 +537,9 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   const SphGeo *g;
   const double *rad;
   const LightD *slight;
+  const SphMat *sm;
   BvhArgs bv = bv_in;
-  stage_scene<kLdsGeo>(smem, geo, radius, lights, n, nl, bv, g, rad, slight);
+  stage_scene<kLdsGeo>(smem, geo, radius, mat, lights, n, nl, bv, g, rad, sm, slight);
   const size_t stack_off = (lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31;
   // the ordered BVH walk's per-lane stacks, [wave][entry][lane], after the scene
   if ((kStack == kStackGlobal || kStack == kStackSplit) && bv.ordered)
@@ -559,7 +560,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
 #ifdef RT_STAMPS
   const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  trace_tile<kCull, kSamples, kStack>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
+  trace_tile<kCull, kSamples, kStack>(g, rad, sm, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
                                         od.x0 + tx * (8 * kWx) + (wave % kWx) * 8,
                                         ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, sa, work, sums);
   RT_ACC(work, 5, t_wave);
@@ -645,8 +646,13 @@ __global__ __launch_bounds__(64 * kWaves, RT_PERSIST_WAVES_PER_EU) void render_p
   const SphGeo *g;
   const double *rad;
   const LightD *slight;
+  const SphMat *sm;
   BvhArgs bv = bv_in;
-  stage_scene<kLdsGeo>(smem, geo, radius, lights, n, nl, bv, g, rad, slight);
+  stage_scene<kLdsGeo>(smem, geo, radius, mat, lights, n, nl, bv, g, rad, sm, slight);
+  // the ordered BVH walk's per-lane stacks, [wave][entry][lane], after the scene
+  if (bv.ordered)
+    bv.ostk = reinterpret_cast<int2 *>(smem + ((lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31)) +
+              (size_t)(threadIdx.x >> 6) * bv.odepth * 64;
   const unsigned wave_id = blockIdx.x * kWaves + (threadIdx.x >> 6);
   const int levels = depth > 1 ? depth - 1 : 1;
   StackEnt *stk = gstack + (size_t)wave_id * levels * 64;
@@ -677,7 +683,7 @@ __global__ __launch_bounds__(64 * kWaves, RT_PERSIST_WAVES_PER_EU) void render_p
     }
     pending = fetch(shard);
     const int ty = (int)(tile / ntx), tx = (int)(tile % ntx);
-    trace_tile<kCull, kSamples, kStackLds>(g, rad, mat, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
+    trace_tile<kCull, kSamples, kStackLds>(g, rad, sm, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
                                            od.x0 + tx * 8, ty * 8, stk, CompactArgs{}, SplitArgs{}, work, sums);
   }
   RT_ACC(work, 5, t_wave);
@@ -760,6 +766,11 @@ struct rt_ctx {
   int xcd_map = 0;  // RT_HIP_XCD_MAP: visits per XCD (runs of ntiles/(8*visits) tiles); 0 = launch order
   unsigned char *cstack_buf = nullptr;
   size_t cstack_bytes = 0;
+  // RT_HIP_LDS_SCENE=1: stage scenes that fit (<= kLdsBudget) in LDS, 4-wave
+  // workgroups.  Off by default: one-wave workgroups reading the scene through
+  // L2 free each wave's slot as soon as its own tile is done (synth200:
+  // 0.473 -> 0.428 ms), which beats the LDS latency advantage.
+  int lds_scene = 0;
   int persist = 0;  // RT_HIP_PERSIST=1: persistent megakernel for every depth (always used above depth 5)
   std::string err;
 };
@@ -890,6 +901,8 @@ int launch_persist3(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dep
   const BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
+  lds = (lds + 31) & ~(size_t)31;
+  if (bv.ordered) lds += (size_t)kWaves * bv.odepth * 64 * sizeof(int2);  // the kernel places them from bv
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_persist<kLds, kCull, kSamples>, 64 * kWaves, lds) !=
           hipSuccess ||
@@ -1102,7 +1115,7 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
             cm->scale};
     // the scene and its BVH are staged in LDS when they fit (lds_layout)
     const int nn = (c->bvh_on && c->cull) ? c->bvh_nodes : 0;
-    const bool lds_geo = lds_layout(true, c->nsph, c->nlight, nn).end <= kLdsBudget;
+    const bool lds_geo = c->lds_scene && lds_layout(true, c->nsph, c->nlight, nn).end <= kLdsBudget;
     const size_t lds = lds_layout(lds_geo, c->nsph, c->nlight, nn).end;
     if (lds > kLdsBudget) {
       c->err = "light list does not fit in LDS";
@@ -1151,6 +1164,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH_GROUPS")) c->bvh_groups = std::max(1, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID")) c->lg_on = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_PERSIST")) c->persist = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_LDS_SCENE")) c->lds_scene = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_STACK")) c->stack_mode = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_XCD_MAP")) c->xcd_map = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_BVH_ORDERED")) c->bvh_ordered = std::atoi(e) != 0;

@@ -90,7 +90,8 @@ template <bool kLdsGeo>
 __device__ __forceinline__ void stage(const WfArgs &a, unsigned char *smem, const SphGeo *&g, const double *&rad,
                                       const LightD *&lights, BvhArgs &bv) {
   bv = a.bv;
-  stage_scene<kLdsGeo>(smem, a.geo, a.rad, a.lights, a.n, a.nl, bv, g, rad, lights);
+  const SphMat *sm;  // the queue kernels read materials from a.mat
+  stage_scene<kLdsGeo>(smem, a.geo, a.rad, a.mat, a.lights, a.n, a.nl, bv, g, rad, sm, lights);
 }
 
 __device__ __forceinline__ void flush_work(const Work &w, unsigned long long *counters) {
