@@ -334,6 +334,7 @@ struct BvhArgs {
   // nullptr selects the stackless preorder walk
   const BvhNode2 *n2;
   int root_ref;
+  int lane_sweep;  // scenes of at most this many spheres: loose lanes sweep every leaf slot instead (lane_sweep())
   int ordered;  // the host allows the ordered walk (tree depth <= kOrderedStack)
   int odepth;   // stack entries per lane (the tree depth)
   int2 *ostk;
@@ -456,6 +457,35 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
       }
     }
     if (!more) return;
+  }
+}
+
+// The loose-group fallback without the tree: every lane runs the leaf loop of
+// bvh_walk over all n leaf slots (the same fp32 line prefilter, then
+// leaf_fn(sphere) for survivors).  The slot index is wave-uniform, so the
+// prefilter records are scalar broadcasts and the lanes never diverge on the
+// traversal itself -- for small scenes this beats divergent per-lane walks of
+// incoherent (reflection) rays.  A slot whose sphere lies wholly beyond
+// tmax_fn() along the line is skipped: any root of it has t >= (w.d)/|d|^2 - R
+// (R the grown fp32 radius, |d| = 1 +- 2^-50), and tmax_fn() carries the
+// 2e-6 * (diameter + |t|) margin, far above the fp32 error of w.d
+// (~3 * 2^-24 * diameter).
+template <typename T, typename F>
+__device__ __forceinline__ void lane_sweep(const BvhArgs &bv, int n, D3 o, D3 d, T &&tmax_fn, Work &work,
+                                           F &&leaf_fn) {
+  const float ox = (float)(o.x - bv.c0x), oy = (float)(o.y - bv.c0y), oz = (float)(o.z - bv.c0z);
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float dd = (dx * dx + dy * dy + dz * dz) * (1.0f + 1e-5f);
+  work.cull += (unsigned)n;
+  for (int k = 0; k < n; ++k) {
+    const float4 q = bv.pf[k];
+    const float wx = q.x - ox, wy = q.y - oy, wz = q.z - oz;
+    const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
+    const float R = q.w + bv.pmargin;
+    if (cx * cx + cy * cy + cz * cz > R * R * dd) continue;
+    const float ta = wx * dx + wy * dy + wz * dz;
+    if ((double)(ta - R) > tmax_fn()) continue;
+    if (!leaf_fn((int)bv.prims[k])) return;
   }
 }
 
@@ -655,7 +685,8 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       test(i);
       return true;
     };
-    if (bv.ostk) bvh_walk_ordered(bv, o, d, tmax, work, leaf);
+    if (n <= bv.lane_sweep) lane_sweep(bv, n, o, d, tmax, work, leaf);
+    else if (bv.ostk) bvh_walk_ordered(bv, o, d, tmax, work, leaf);
     else bvh_walk(bv, o, d, tmax, work, leaf);
   }
 #ifdef RT_STAMPS

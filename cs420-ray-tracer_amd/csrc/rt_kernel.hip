@@ -29,6 +29,7 @@
 
 #include "rt_device.h"
 #include "rt_wavefront.h"
+#include "rt_sched.h"
 
 #include <cmath>
 #include <vector>
@@ -519,7 +520,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
     const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
     const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
     BvhArgs bv_in, LgArgs lg, OutDesc od, StackEnt *__restrict__ gstack, unsigned long long *__restrict__ counters,
-    int ntx, int ntiles, int xcd_per, SplitArgs sa) {  // xcd_per: tiles per run
+    int ntx, int ntiles, int xcd_per, SplitArgs sa, const int *__restrict__ perm) {  // xcd_per: tiles per run
   // 16x16-pixel workgroup tile.  Workgroups are dealt to the 8 XCDs round
   // robin (b % 8).  With chunk > 0 the scanline-ordered tiles are cut into
   // runs of `chunk` tiles and run r goes to XCD r % 8: each XCD's L2 serves
@@ -527,7 +528,10 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   // while every XCD still samples the whole image (balance).
   const int b = blockIdx.x;
   int tile = b;
-  if (xcd_per > 0) {
+  if (perm) {
+    if (b >= ntiles) return;
+    tile = perm[b];  // launch order (rt_sched.h): heaviest predicted tiles first
+  } else if (xcd_per > 0) {
     const int m = b >> 3;  // this workgroup's rank on its XCD
     tile = ((m / xcd_per) * 8 + (b & 7)) * xcd_per + m % xcd_per;
   }
@@ -735,6 +739,7 @@ struct rt_ctx {
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
   double rmax = 0;
   int bvh_min = 24, bvh_on = 1, bvh_groups = 2, bvh_leaf = 4;
+  int lane_sweep = 0;  // RT_HIP_LANE_SWEEP: loose groups sweep all leaf slots per lane up to this many spheres
   // -1 (auto): every group walks the BVH when the scene has more than
   // kBvhAlwaysAbove spheres (a linear cull sweep is O(n) per group)
   int bvh_always = -1;
@@ -771,6 +776,15 @@ struct rt_ctx {
   // L2 free each wave's slot as soon as its own tile is done (synth200:
   // 0.473 -> 0.428 ms), which beats the LDS latency advantage.
   int lds_scene = 0;
+  // Launch order of the tiles (rt_sched.h), rebuilt when the view or the
+  // scene changes; RT_HIP_SCHED=0 dispatches in scanline order.
+  int sched = 1;
+  std::vector<SchedSphere> h_refl;  // reflective spheres of the scene
+  unsigned long long scene_gen = 0;
+  SchedView perm_view{};
+  unsigned long long perm_gen = ~0ull;
+  int *d_perm = nullptr, *h_perm = nullptr;  // h_perm pinned
+  size_t perm_cap = 0;
   int persist = 0;  // RT_HIP_PERSIST=1: persistent megakernel for every depth (always used above depth 5)
   std::string err;
 };
@@ -840,6 +854,7 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   b.pmargin = 4.0f * b.margin;
   if (!std::isfinite(b.diam)) b.diam = INFINITY;
   b.min_cands = c->bvh_min;
+  b.lane_sweep = c->lane_sweep;
   b.always = c->bvh_always >= 0 ? c->bvh_always : (c->nsph > kBvhAlwaysAbove ? 1 : 0);
   b.max_groups = c->bvh_groups;
   return b;
@@ -853,6 +868,43 @@ LgArgs lg_args(const rt_ctx *c) {
   g.on = (c->lg_on && c->cull && c->d_lg_start) ? 1 : 0;
   g.max_off = c->lg_max_off;
   return g;
+}
+
+// The tile launch order for this view (rt_sched.h), on the device; rebuilt
+// only when the camera, the image/shard geometry, the tile size or the scene
+// changed since the last build.
+int tile_perm(rt_ctx *c, const Cam &cam, int W, int H, const Rows &rows, const OutDesc &od, int tw, int th,
+              long long ntiles, const int *&out) {
+  SchedView v{};
+  v.px = cam.px, v.py = cam.py, v.pz = cam.pz, v.fx = cam.fx, v.fy = cam.fy, v.fz = cam.fz;
+  v.rx = cam.rx, v.ry = cam.ry, v.rz = cam.rz, v.ux = cam.ux, v.uy = cam.uy, v.uz = cam.uz, v.scale = cam.scale;
+  v.W = W, v.H = H, v.band = rows.band, v.first = rows.first, v.stride = rows.stride, v.count = rows.count;
+  v.x0 = od.x0, v.xw = od.xw, v.tw = tw, v.th = th;
+  if (c->perm_gen == c->scene_gen && std::memcmp(&v, &c->perm_view, sizeof v) == 0 && c->d_perm) {
+    out = c->d_perm;
+    return RT_OK;
+  }
+  std::vector<int> perm;
+  tile_order(v, c->h_refl, perm);
+  if ((long long)perm.size() != ntiles) return RT_ERR_INVALID_ARG;
+  const size_t bytes = perm.size() * sizeof(int);
+  RT_TRY(c, hipStreamSynchronize(c->stream));  // the previous order may still be in flight from h_perm
+  if (c->perm_cap < bytes) {
+    if (c->d_perm) (void)hipFree(c->d_perm);
+    if (c->h_perm) (void)hipHostFree(c->h_perm);
+    c->d_perm = c->h_perm = nullptr;
+    c->perm_cap = 0;
+    c->perm_gen = ~0ull;
+    RT_TRY(c, hipMalloc(&c->d_perm, bytes));
+    RT_TRY(c, hipHostMalloc(&c->h_perm, bytes, hipHostMallocDefault));
+    c->perm_cap = bytes;
+  }
+  std::memcpy(c->h_perm, perm.data(), bytes);
+  RT_TRY(c, hipMemcpyAsync(c->d_perm, c->h_perm, bytes, hipMemcpyHostToDevice, c->stream));
+  c->perm_view = v;
+  c->perm_gen = c->scene_gen;
+  out = c->d_perm;
+  return RT_OK;
 }
 
 template <bool kLds, bool kCull, int kSamples, int kStack>
@@ -889,9 +941,14 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     }
     gstack = reinterpret_cast<StackEnt *>(c->cstack_buf);
   }
+  const int *perm = nullptr;
+  if (c->sched && xcd_per == 0 && kStack != kStackSplit) {
+    int rc = tile_perm(c, cam, W, H, rows, od, 8 * kWx, 8 * kWy, ntiles, perm);
+    if (rc != RT_OK) return rc;
+  }
   hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream,
                      c->d_geo, c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv,
-                     lg, od, gstack, c->d_counters, ntx, (int)ntiles, xcd_per, sa);
+                     lg, od, gstack, c->d_counters, ntx, (int)ntiles, xcd_per, sa, perm);
   return RT_OK;
 }
 
@@ -1160,11 +1217,13 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::max(0, std::min(3, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_BVH")) c->bvh_on = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_MIN")) c->bvh_min = std::atoi(e);
+  if (const char *e = std::getenv("RT_HIP_LANE_SWEEP")) c->lane_sweep = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_BVH_ALWAYS")) c->bvh_always = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_GROUPS")) c->bvh_groups = std::max(1, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID")) c->lg_on = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_PERSIST")) c->persist = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_LDS_SCENE")) c->lds_scene = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_SCHED")) c->sched = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_STACK")) c->stack_mode = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_XCD_MAP")) c->xcd_map = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_BVH_ORDERED")) c->bvh_ordered = std::atoi(e) != 0;
@@ -1204,6 +1263,8 @@ void rt_destroy(rt_ctx *c) {
   if (c->wf_buf) (void)hipFree(c->wf_buf);
   if (c->stack_buf) (void)hipFree(c->stack_buf);
   if (c->cstack_buf) (void)hipFree(c->cstack_buf);
+  if (c->d_perm) (void)hipFree(c->d_perm);
+  if (c->h_perm) (void)hipHostFree(c->h_perm);
   for (int i = 0; i < rt_ctx::kRing; i++) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
@@ -1363,6 +1424,12 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
   } else {
     c->nsph = n;
     c->nlight = nl;
+    c->h_refl.clear();
+    for (int i = 0; i < n; i++)
+      if (s->spheres[i].reflectivity > 0.0)  // main.cpp:43
+        c->h_refl.push_back(SchedSphere{s->spheres[i].center[0], s->spheres[i].center[1], s->spheres[i].center[2],
+                                        s->spheres[i].radius});
+    c->scene_gen++;
     for (int q = 0; q < 3; q++) c->amb[q] = s->ambient[q];
     c->has_scene = true;
   }

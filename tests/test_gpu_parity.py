@@ -400,14 +400,16 @@ def test_pipelines_random_scenes(pipeline_renderer, seed):
 
 @pytest.fixture(params=[{"RT_HIP_STACK": "0"}, {"RT_HIP_STACK": "2"}, {"RT_HIP_XCD_MAP": "0"},
                         {"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_LDS_SCENE": "1", "RT_HIP_STACK": "0"},
-                        {"RT_HIP_PERSIST": "1", "RT_HIP_STACK": "0"}],
-                ids=["lds-stack", "compact", "no-xcd-map", "lds-scene", "lds-scene-lds-stack", "persist"])
+                        {"RT_HIP_PERSIST": "1", "RT_HIP_STACK": "0"}, {"RT_HIP_SCHED": "0"}],
+                ids=["lds-stack", "compact", "no-xcd-map", "lds-scene", "lds-scene-lds-stack", "persist",
+                     "scanline-order"])
 def stack_renderer(request, monkeypatch):
     """Non-default kernel layouts (RT_HIP_STACK=0: LDS reflection stack, the
     persistent kernel above depth 5; 2: workgroup-compacted reflection levels;
     RT_HIP_XCD_MAP=0: workgroup tiles in launch order; RT_HIP_LDS_SCENE=1:
     scenes that fit staged in LDS with 4-wave workgroups; RT_HIP_PERSIST=1:
-    the persistent tile-queue kernel at every depth)."""
+    the persistent tile-queue kernel at every depth; RT_HIP_SCHED=0: tiles
+    launched in scanline order instead of heaviest-predicted first)."""
     import rt_hip
 
     for k, v in request.param.items():
