@@ -7,8 +7,10 @@ A step renders ONE frame of the workload: each rank traces its cyclic 8-row
 bands through librt_hip.so (rt_render_async on torch's current stream, output
 resident in HBM), then the shards are gathered to rank 0 with RCCL
 (torch.distributed "nccl" = RCCL over xGMI) and unpermuted into the final
-PPM-ordered framebuffer on device.  Total work per step is fixed as N grows
-("scaling": "strong").  value = rays of the frame x K / max-over-ranks wall
+PPM-ordered framebuffer on device.  For N > 1 the frames are pipelined in
+batches (--frames-per-gather, default 4): a batch renders while the previous
+batch's shards travel to rank 0 in one gather.  Total work per step is fixed
+as N grows ("scaling": "strong").  value = rays of the frame x K / max-over-ranks wall
 time of the K timed steps.
 
 Also reported:
@@ -91,7 +93,7 @@ def cpu_baseline(scene_file: str, W: int, H: int, D: int, rays_per_frame: int, t
             "sample": f"{what}; {W}x{H} d{D}, {rays} rays in {secs:.3f} s on {threads} thread(s) of {cpu_model()}"}
 
 
-def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, cull=True):
+def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, cull=True, batch=4):
     scene_name, W, H, D = WORKLOADS[workload]
     scene_file = os.path.join(PKG, "scenes", scene_name + ".txt")
     scene = rt_hip.Scene.load(scene_file)
@@ -103,26 +105,30 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     r.set_stream(stream.cuda_stream)  # the kernel runs on torch's stream: events and RCCL order with it
     rows = rt_hip.rows_for_shard(H, BAND, rank, world) if world > 1 else rt_hip.rt_rows(1, 0, 1, H)
     R = rows.count
-    # two shard / gather buffers: frame i renders while frame i-1 is gathered (rt_frames)
-    shards = [torch.empty((R, W, 3), dtype=torch.uint8, device=f"cuda:{device}") for _ in range(2)]
+    # two shard / gather buffers of `batch` frames each: a batch renders while
+    # the previous one is gathered to rank 0 by one RCCL gather (rt_frames)
+    F = batch if world > 1 else 1
+    shards = [torch.empty((F, R, W, 3), dtype=torch.uint8, device=f"cuda:{device}") for _ in range(2)]
     gathered = image = None
     if world > 1 and rank == 0:
-        gathered = [list(torch.empty((world, R, W, 3), dtype=torch.uint8, device=f"cuda:{device}").unbind(0))
+        gathered = [list(torch.empty((world, F, R, W, 3), dtype=torch.uint8, device=f"cuda:{device}").unbind(0))
                     for _ in range(2)]
         image = torch.empty((H, W, 3), dtype=torch.uint8, device=f"cuda:{device}")
 
     def render(shard):
         r.render_async(cam, W, H, D, rows, shard.data_ptr())
 
-    def unpermute(g):
-        r.unpermute(g[0].data_ptr(), image.data_ptr(), W, H, BAND, world, R)  # g: views of one buffer
+    def unpermute(g, j):
+        # g: per-rank views of one [world, F, R, W, 3] buffer; frame j of rank r
+        # starts (r * F + j) * R rows in, i.e. rank-major with F * R rows per rank
+        r.unpermute(g[0].data_ptr() + j * R * W * 3, image.data_ptr(), W, H, BAND, world, F * R)
 
     def frames(n):
         if world > 1:
-            rt_frames.run_frames(dist, n, rank, render, shards, gathered, unpermute if rank == 0 else None)
+            rt_frames.run_frames(dist, n, rank, render, shards, gathered, unpermute if rank == 0 else None, F)
         else:
             for i in range(n):
-                render(shards[i & 1])
+                render(shards[i & 1][0])
 
     frames(warmup)
     st = r.stats()  # syncs; ray counts of this rank's shard (identical every step)
@@ -166,6 +172,8 @@ def main():
     ap.add_argument("--workload", default="synth200_1920x1080_d4", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-also", action="store_true", help="skip the complex.txt north-star line item")
+    ap.add_argument("--frames-per-gather", type=int, default=4,
+                    help="N > 1: frames rendered per RCCL gather to rank 0 (one collective per batch)")
     ap.add_argument("--brute-force", action="store_true",
                     help="disable the exact per-wave sphere culling: every ray tests every sphere")
     args = ap.parse_args()
@@ -181,11 +189,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
     cull = not args.brute_force
-    m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local, cull)
+    batch = max(1, args.frames_per_gather)
+    m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local, cull, batch)
     also = {}
     if not args.no_also and args.workload != "complex_1920x1080_d4":
         a = measure(rt_hip, torch, dist, "complex_1920x1080_d4", max(args.steps // 2, 5), 2, world, rank, local,
-                    cull)
+                    cull, batch)
         also["complex_1920x1080_d4"] = {
             "mrays_per_s": round(a["frame_rays"] * max(args.steps // 2, 5) / a["elapsed"] / 1e6, 2),
             "ms_per_frame": round(a["elapsed"] / max(args.steps // 2, 5) * 1e3, 4),
@@ -224,7 +233,7 @@ def main():
                        "depth": m["D"], "spheres": m["spheres"], "lights": m["lights"],
                        "rays_per_frame": m["frame_rays"],
                        "parallelism": f"rows cyclic {BAND}-row bands x {world} GPU" +
-                                      (" + RCCL gather to rank 0" if world > 1 else "")},
+                                      (f" + RCCL gather to rank 0 every {batch} frames" if world > 1 else "")},
             # achieved = SURVEY 8(d)'s algorithmic FLOPs (25 per ray-sphere pair, every
             # ray against every sphere) over the measured kernel time.  The kernel
             # prunes pairs exactly (cull bounds, BVH, shadow grids), so this

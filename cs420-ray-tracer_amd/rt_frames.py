@@ -1,14 +1,17 @@
 """Pipelined multi-rank frame loop: each rank renders its cyclic
-row bands of frame i while frame i-1's shards travel to rank 0.
+row bands of a batch of frames while the previous batch's shards travel to
+rank 0.
 
-Two shard buffers per rank and two gather buffers on rank 0 alternate by frame
-parity.  Frame i's gather is issued asynchronously (RCCL runs it on the
-process group's stream after the render that produced the shard); before
-frame i+2 renders into the same buffer the rank's stream waits for that
-gather (Work.wait() orders streams, it does not block the host under NCCL),
-and rank 0 reassembles frame i then.  So on every rank the render of frame i
-overlaps the gather of frame i-1, and the image of frame i is complete once
-the loop has drained.
+Frames are rendered into one of two shard buffers per rank ([batch, R, W, 3]
+each) and the buffer's frames are gathered to rank 0 with ONE collective, so
+the per-collective host cost is paid once per batch instead of once per frame.
+The two buffers alternate by batch parity: a batch's gather is issued
+asynchronously (RCCL runs it on the process group's stream after the renders
+that produced it); before the buffer is rendered into again the rank's stream
+waits for that gather (Work.wait() orders streams, it does not block the host
+under NCCL) and rank 0 reassembles the batch's frames then.  So on every rank
+the rendering of batch i overlaps the gather of batch i-1, and every frame's
+image is complete once the loop has drained.
 """
 from __future__ import annotations
 
@@ -16,25 +19,37 @@ from typing import Callable, Sequence
 
 
 def run_frames(dist, steps: int, rank: int, render: Callable[[object], None], shards: Sequence,
-               gathered: Sequence | None, unpermute: Callable[[object], None] | None) -> None:
-    """render(shard) enqueues frame rendering into `shard`; on rank 0,
-    gathered[k] is the list of per-rank receive tensors for buffer k and
-    unpermute(gathered_k) enqueues the reassembly of that buffer."""
+               gathered: Sequence | None, unpermute: Callable[[Sequence, int], None] | None,
+               batch: int = 1) -> None:
+    """render(view) enqueues one frame into `view` (a [R, W, 3] slice of a
+    shard buffer); shards[k] is buffer k ([batch, R, W, 3]); on rank 0,
+    gathered[k] is the list of per-rank receive tensors ([batch, R, W, 3]) for
+    buffer k and unpermute(gathered[k], j) enqueues the reassembly of frame j
+    of that buffer.  `steps` frames are rendered in batches of `batch`."""
     works = [None, None]
+    counts = [0, 0]
 
     def retire(k):
         works[k].wait()
         works[k] = None
         if rank == 0 and unpermute is not None:
-            unpermute(gathered[k])
+            for j in range(counts[k]):
+                unpermute(gathered[k], j)
 
-    for i in range(steps):
-        k = i & 1
+    done, b = 0, 0
+    while done < steps:
+        k = b & 1
         if works[k] is not None:
-            retire(k)  # frame i-2: its shard buffer is free, rank 0 reassembles it
-        render(shards[k])
-        works[k] = dist.gather(shards[k], gathered[k] if rank == 0 else None, dst=0, async_op=True)
-    for i in range(max(0, steps - 2), steps):  # drain in frame order
+            retire(k)  # batch b-2: its shard buffer is free, rank 0 reassembles it
+        n = min(batch, steps - done)
+        for j in range(n):
+            render(shards[k][j])
+        recv = [g[:n] for g in gathered[k]] if rank == 0 else None
+        works[k] = dist.gather(shards[k][:n], recv, dst=0, async_op=True)
+        counts[k] = n
+        done += n
+        b += 1
+    for i in range(max(0, b - 2), b):  # drain in batch order
         k = i & 1
         if works[k] is not None:
             retire(k)

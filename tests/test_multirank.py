@@ -75,10 +75,11 @@ def test_gloo_gather_reassembles_golden(world, name):
     assert rays == sum(manifest()[name]["rays"].values())
 
 
-def _pipelined_worker(rank, world, port, q):
+def _pipelined_worker(rank, world, port, batch, q):
     """bench.py's pipelined frame loop (rt_frames.run_frames) under gloo: frame f
     of rank r fills its shard with (f, r, row); every reassembled frame must be
-    exact and arrive in order."""
+    exact and arrive in order, with `batch` frames per gather (steps not a
+    multiple of it: the last batch is partial)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import rt_frames
@@ -88,8 +89,8 @@ def _pipelined_worker(rank, world, port, q):
 
     rows = rt_hip.rows_for_shard(H, band, rank, world)
     R = rows.count
-    shards = [torch.zeros((R, W, 3), dtype=torch.uint8) for _ in range(2)]
-    gathered = ([list(torch.zeros((world, R, W, 3), dtype=torch.uint8).unbind(0)) for _ in range(2)]
+    shards = [torch.zeros((batch, R, W, 3), dtype=torch.uint8) for _ in range(2)]
+    gathered = ([list(torch.zeros((world, batch, R, W, 3), dtype=torch.uint8).unbind(0)) for _ in range(2)]
                 if rank == 0 else None)
     frame = [0]
     seen = []
@@ -100,23 +101,26 @@ def _pipelined_worker(rank, world, port, q):
             shard[k] = (f * 16 + rank * 4 + k % 4) % 256
         frame[0] += 1
 
-    def unpermute(g):
-        img = unpermute_host(torch.stack(g).numpy(), H, band)
+    def unpermute(g, j):
+        # the device unpermute's addressing: frame j of rank r at rows (r * batch + j) * R
+        flat = torch.stack(g).reshape(world * batch * R, W, 3)[j * R:]
+        img = unpermute_host(np.stack([flat[r * batch * R:r * batch * R + R].numpy() for r in range(world)]), H,
+                             band)
         seen.append(img[:, 0, 0].tolist())
 
-    rt_frames.run_frames(dist, steps, rank, render, shards, gathered, unpermute if rank == 0 else None)
+    rt_frames.run_frames(dist, steps, rank, render, shards, gathered, unpermute if rank == 0 else None, batch)
     if rank == 0:
         q.put(seen)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_pipelined_frames(world):
+@pytest.mark.parametrize("world,batch", [(2, 1), (3, 1), (2, 4), (3, 3)])
+def test_gloo_pipelined_frames(world, batch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, batch, q)) for r in range(world)]
     for p in procs:
         p.start()
     seen = q.get(timeout=120)
