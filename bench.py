@@ -93,7 +93,11 @@ def cpu_baseline(scene_file: str, W: int, H: int, D: int, rays_per_frame: int, t
             "sample": f"{what}; {W}x{H} d{D}, {rays} rays in {secs:.3f} s on {threads} thread(s) of {cpu_model()}"}
 
 
-def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, cull=True, batch=4):
+def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, cull=True, batch=4, dist_on=None):
+    import rt_frames
+
+    if dist_on is None:
+        dist_on = world > 1
     scene_name, W, H, D = WORKLOADS[workload]
     scene_file = os.path.join(PKG, "scenes", scene_name + ".txt")
     scene = rt_hip.Scene.load(scene_file)
@@ -103,14 +107,14 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     r.upload(scene)
     stream = torch.cuda.current_stream()
     r.set_stream(stream.cuda_stream)  # the kernel runs on torch's stream: events and RCCL order with it
-    rows = rt_hip.rows_for_shard(H, BAND, rank, world) if world > 1 else rt_hip.rt_rows(1, 0, 1, H)
+    rows = rt_hip.rows_for_shard(H, BAND, rank, world) if dist_on else rt_hip.rt_rows(1, 0, 1, H)
     R = rows.count
     # two shard / gather buffers of `batch` frames each: a batch renders while
     # the previous one is gathered to rank 0 by one RCCL gather (rt_frames)
-    F = batch if world > 1 else 1
+    F = batch if dist_on else 1
     shards = [torch.empty((F, R, W, 3), dtype=torch.uint8, device=f"cuda:{device}") for _ in range(2)]
     gathered = image = None
-    if world > 1 and rank == 0:
+    if dist_on and rank == 0:
         gathered = [list(torch.empty((world, F, R, W, 3), dtype=torch.uint8, device=f"cuda:{device}").unbind(0))
                     for _ in range(2)]
         image = torch.empty((H, W, 3), dtype=torch.uint8, device=f"cuda:{device}")
@@ -124,7 +128,7 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
         r.unpermute(g[0].data_ptr() + j * R * W * 3, image.data_ptr(), W, H, BAND, world, F * R)
 
     def frames(n):
-        if world > 1:
+        if dist_on:
             rt_frames.run_frames(dist, n, rank, render, shards, gathered, unpermute if rank == 0 else None, F)
         else:
             for i in range(n):
@@ -133,20 +137,20 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     frames(warmup)
     st = r.stats()  # syncs; ray counts of this rank's shard (identical every step)
     r.kernel_times()  # drop warmup launches from the history
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     frames(steps)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ktimes = r.kernel_times(max(steps, 1))
     kmean = sum(ktimes) / len(ktimes)
     my_rays = st.rays
     tests_exact, tests_cull = st.tests_exact, st.tests_cull
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed, kmean], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kmax = t.tolist()
@@ -156,8 +160,16 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     else:
         kmax = kmean
         frame_rays = my_rays
+    assembled_ok = None
+    if dist_on and rank == 0 and steps > 0:
+        # untimed: the last frame reassembled from the gathered shards must equal
+        # one full-frame render on this device, byte for byte
+        full = torch.empty((H, W, 3), dtype=torch.uint8, device=f"cuda:{device}")
+        r.render_async(cam, W, H, D, rt_hip.rt_rows(1, 0, 1, H), full.data_ptr())
+        torch.cuda.synchronize()
+        assembled_ok = bool(torch.equal(full, image))
     r.close()
-    return {"scene": scene_name, "scene_file": scene_file, "W": W, "H": H, "D": D, "spheres": scene.num_spheres,
+    return {"assembled_ok": assembled_ok, "scene": scene_name, "scene_file": scene_file, "W": W, "H": H, "D": D, "spheres": scene.num_spheres,
             "lights": scene.num_lights, "frame_rays": frame_rays, "rank_rays": my_rays, "elapsed": elapsed,
             "kernel_ms_mean": kmean, "kernel_ms_max_rank": kmax, "kernel_ms_min": min(ktimes),
             "launches_timed": len(ktimes), "rows_per_rank": R, "tests_exact": tests_exact,
@@ -174,6 +186,8 @@ def main():
     ap.add_argument("--no-also", action="store_true", help="skip the complex.txt north-star line item")
     ap.add_argument("--frames-per-gather", type=int, default=4,
                     help="N > 1: frames rendered per RCCL gather to rank 0 (one collective per batch)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="rehearsal: run the N > 1 data path (RCCL process group, shard gather, unpermute) at N = 1")
     ap.add_argument("--brute-force", action="store_true",
                     help="disable the exact per-wave sphere culling: every ray tests every sphere")
     args = ap.parse_args()
@@ -181,20 +195,22 @@ def main():
     world, rank, local = dist_env()
     import torch  # loads torch's HIP runtime first; librt_hip.so binds to it
     import torch.distributed as dist
-    import rt_frames
     import rt_hip
 
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world)
 
     cull = not args.brute_force
     batch = max(1, args.frames_per_gather)
-    m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local, cull, batch)
+    m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local, cull, batch, dist_on)
     also = {}
     if not args.no_also and args.workload != "complex_1920x1080_d4":
         a = measure(rt_hip, torch, dist, "complex_1920x1080_d4", max(args.steps // 2, 5), 2, world, rank, local,
-                    cull, batch)
+                    cull, batch, dist_on)
         also["complex_1920x1080_d4"] = {
             "mrays_per_s": round(a["frame_rays"] * max(args.steps // 2, 5) / a["elapsed"] / 1e6, 2),
             "ms_per_frame": round(a["elapsed"] / max(args.steps // 2, 5) * 1e3, 4),
@@ -232,8 +248,9 @@ def main():
             "config": {"workload": args.workload, "scene": m["scene"], "width": m["W"], "height": m["H"],
                        "depth": m["D"], "spheres": m["spheres"], "lights": m["lights"],
                        "rays_per_frame": m["frame_rays"],
+                       **({"assembled_frame_equals_single_gpu_render": m["assembled_ok"]} if dist_on else {}),
                        "parallelism": f"rows cyclic {BAND}-row bands x {world} GPU" +
-                                      (f" + RCCL gather to rank 0 every {batch} frames" if world > 1 else "")},
+                                      (f" + RCCL gather to rank 0 every {batch} frames" if dist_on else "")},
             # achieved = SURVEY 8(d)'s algorithmic FLOPs (25 per ray-sphere pair, every
             # ray against every sphere) over the measured kernel time.  The kernel
             # prunes pairs exactly (cull bounds, BVH, shadow grids), so this
@@ -269,7 +286,7 @@ def main():
             line["cpu_baseline_all_cores"] = cpu_baseline(m["scene_file"], m["W"], m["H"], m["D"],
                                                           m["frame_rays"], threads=min(16, os.cpu_count() or 1))
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 
