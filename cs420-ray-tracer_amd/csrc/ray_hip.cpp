@@ -39,6 +39,7 @@ struct Opts {
   int gpus = 1, device = 0, repeat = 1;
   std::string out;
   bool p6 = false, json = false;
+  bool force_gather = false;  // --force-gather: the G-device gather path even for G = 1 (rehearsal)
   int samples = 1;
 };
 
@@ -178,7 +179,7 @@ int render_multi(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::v
 int render_pass(const Opts &o, const rt_scene &sc, const rt_camera &cam, const char *label, const char *file) {
   std::vector<uint8_t> img((size_t)o.width * o.height * 3);
   Result res;
-  int rc = o.gpus > 1 ? render_multi(o, sc, cam, img, res) : render_single(o, sc, cam, img, res);
+  int rc = (o.gpus > 1 || o.force_gather) ? render_multi(o, sc, cam, img, res) : render_single(o, sc, cam, img, res);
   if (rc) return rc;
   if (o.mode == "hip")
     std::printf("GPU rendering time: %g seconds\n", res.wall_s);  // main_gpu.cu:519
@@ -231,6 +232,7 @@ int main(int argc, char **argv) {
     else if (a == "--repeat") { if (!next(o.repeat)) return usage(argv[0]); }
     else if (a == "--out") { if (i + 1 >= argc) return usage(argv[0]); o.out = argv[++i]; }
     else if (a == "--p6") o.p6 = true;
+    else if (a == "--force-gather") o.force_gather = true;
     else if (a == "-a") o.samples = 4;
     else if (a == "--json") o.json = true;
     else if (a == "-h" || a == "--help") return usage(argv[0]);

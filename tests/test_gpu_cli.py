@@ -74,6 +74,15 @@ def test_ray_hip_missing_scene_fails_like_the_reference(tmp_path):
     assert r.returncode != 0 and "Could not open scene file" in r.stderr
 
 
+def test_ray_hip_gather_path_one_gpu(tmp_path):
+    """The --gpus G code path (ncclCommInitAll, ncclGather to device 0,
+    unpermute) rehearsed with G = 1."""
+    run(tmp_path, "ray_hip", "--gpus", "1", "--force-gather", "--width", "1920", "--height", "1080", "--depth", "4",
+        "--p6", scene_path("complex"))
+    data = open(tmp_path / "output_gpu.ppm", "rb").read()
+    assert data.endswith(golden_rgb("complex_1920x1080_d4"))
+
+
 def test_ray_hip_multi_gpu_gather(tmp_path):
     import torch
 
