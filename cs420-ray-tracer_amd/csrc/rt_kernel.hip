@@ -733,12 +733,16 @@ struct rt_ctx {
   int bvh_nodes = 0;
   // per-light direction grids for shadow rays (rt_lightgrid.h), built at upload
   int32_t *d_lg_start = nullptr, *d_lg_ids = nullptr;
-  int lg_n = 128, lg_on = 1;
+  int lg_n = 128, lg_on = 1;  // lg_n: the grid of the uploaded scene
+  int lg_n_opt = 0;            // RT_HIP_SHADOW_GRID_N; 0 = 128, or 256 above kBvhAlwaysAbove spheres
   double lg_max_off = 0.0;
   double c0[3] = {0, 0, 0};
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
   double rmax = 0;
   int bvh_min = 24, bvh_on = 1, bvh_groups = 2, bvh_leaf = 4;
+  // RT_HIP_BVH_LEAF; 0 = 4, or 2 above kBvhAlwaysAbove spheres (synth10k: with
+  // the 256 grid 6.95 -> 6.46 ms; neither helps synth200)
+  int bvh_leaf_opt = 0;
   int lane_sweep = 0;  // RT_HIP_LANE_SWEEP: loose groups sweep all leaf slots per lane up to this many spheres
   // -1 (auto): every group walks the BVH when the scene has more than
   // kBvhAlwaysAbove spheres (a linear cull sweep is O(n) per group)
@@ -1227,8 +1231,8 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_STACK")) c->stack_mode = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_XCD_MAP")) c->xcd_map = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_BVH_ORDERED")) c->bvh_ordered = std::atoi(e) != 0;
-  if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf = std::max(1, std::min(15, std::atoi(e)));
-  if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n = std::max(1, std::min(256, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(256, std::atoi(e)));
   auto bail = [&](int rc) {
     rt_destroy(c);
     return rc;
@@ -1332,6 +1336,9 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     bz[i] = s->spheres[i].center[2] - c0[2];
     br[i] = s->spheres[i].radius;
   }
+  const bool big = n > kBvhAlwaysAbove;
+  c->bvh_leaf = c->bvh_leaf_opt ? c->bvh_leaf_opt : (big ? 2 : 4);
+  c->lg_n = c->lg_n_opt ? c->lg_n_opt : (big ? 256 : 128);
   std::vector<BvhNode> nodes;
   std::vector<int32_t> prims;
   build_bvh(bx.data(), by.data(), bz.data(), br.data(), n, c->bvh_leaf, nodes, prims);
