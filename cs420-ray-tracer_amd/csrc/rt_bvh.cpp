@@ -187,4 +187,63 @@ int32_t build_bvh2(const std::vector<BvhNode> &nodes, std::vector<BvhNode2> &out
   return ref(0);
 }
 
+int32_t build_bvh4(const std::vector<BvhNode> &nodes, std::vector<BvhNode4> &out, int &stack) {
+  out.clear();
+  stack = 0;
+  if (nodes.empty()) return -1;
+  if (nodes[0].leaf >= 0) return -(nodes[0].leaf + 1);
+  // the 4-wide nodes are the binary root and every internal grandchild reached
+  // from one; `kids` lists the up-to-4 preorder children of binary node i
+  auto kids = [&](int i, int *c) {
+    int n = 0;
+    const int l = i + 1, r = nodes[l].skip;
+    for (int x : {l, r}) {
+      if (nodes[x].leaf >= 0) {
+        c[n++] = x;
+      } else {
+        c[n++] = x + 1;
+        c[n++] = nodes[x + 1].skip;
+      }
+    }
+    return n;
+  };
+  std::vector<int32_t> map(nodes.size(), -1);
+  std::vector<int> order{0};  // breadth of 4-wide nodes, in creation order
+  map[0] = 0;
+  for (size_t q = 0; q < order.size(); q++) {
+    int c[4];
+    const int n = kids(order[q], c);
+    for (int k = 0; k < n; k++)
+      if (nodes[c[k]].leaf < 0 && map[c[k]] < 0) {
+        map[c[k]] = (int32_t)order.size();
+        order.push_back(c[k]);
+      }
+  }
+  out.resize(order.size());
+  const float qnan = __builtin_nanf("");
+  std::vector<int> need(order.size(), 0);  // worst pending entries below each node
+  for (size_t q = order.size(); q-- > 0;) {
+    int c[4];
+    const int n = kids(order[q], c);
+    BvhNode4 &b = out[q];
+    int worst = 0;
+    for (int k = 0; k < 4; k++) {
+      const bool on = k < n;
+      b.lox[k] = on ? nodes[c[k]].lo[0] : qnan;
+      b.loy[k] = on ? nodes[c[k]].lo[1] : qnan;
+      b.loz[k] = on ? nodes[c[k]].lo[2] : qnan;
+      b.hix[k] = on ? nodes[c[k]].hi[0] : qnan;
+      b.hiy[k] = on ? nodes[c[k]].hi[1] : qnan;
+      b.hiz[k] = on ? nodes[c[k]].hi[2] : qnan;
+      b.c[k] = !on ? 0 : nodes[c[k]].leaf >= 0 ? -(nodes[c[k]].leaf + 1) : map[c[k]];
+      if (on && nodes[c[k]].leaf < 0) worst = std::max(worst, need[map[c[k]]]);
+      b.pad[k] = 0;
+    }
+    // entering the nearest child leaves at most n - 1 pending here
+    need[q] = n - 1 + worst;
+  }
+  stack = need[0];
+  return 0;
+}
+
 }  // namespace rtk

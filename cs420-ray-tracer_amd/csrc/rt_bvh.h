@@ -28,10 +28,26 @@ struct BvhNode2 {  // 64 B
   int32_t pad[2];
 };
 
+// Four-child node for the ordered 4-wide walk: the grandchildren of a binary
+// node (a leaf child stands for itself), boxes in SoA order so child k's slab
+// test reads lox[k] .. hiz[k].  Unused slots have NaN boxes (every slab
+// comparison with them is false, so they are never entered).  Child
+// references as BvhNode2 (>= 0: internal node of this array, < 0: leaf).
+struct BvhNode4 {  // 128 B
+  float lox[4], loy[4], loz[4], hix[4], hiy[4], hiz[4];
+  int32_t c[4];
+  int32_t pad[4];
+};
+
 // Derives the two-child layout from the preorder one; returns the root's
 // reference (a leaf reference when the whole tree is one leaf) and the tree
 // depth (the most far-children an ordered walk can have pending).
 int32_t build_bvh2(const std::vector<BvhNode> &nodes, std::vector<BvhNode2> &out, int &depth);
+
+// Derives the four-child layout; returns the root's reference and, in
+// `stack`, the most entries an ordered 4-wide walk can have pending (the
+// largest sum over a root-to-leaf path of (children - 1) per node).
+int32_t build_bvh4(const std::vector<BvhNode> &nodes, std::vector<BvhNode4> &out, int &stack);
 
 // Builds the BVH over spheres (centres cx,cy,cz, radii r).  `prims` receives
 // the sphere indices in leaf order.  Leaves hold at most `max_leaf` (<= 15)

@@ -334,6 +334,11 @@ struct BvhArgs {
   // nullptr selects the stackless preorder walk
   const BvhNode2 *n2;
   int root_ref;
+  // 4-wide ordered walk (wide = 1): grandchild nodes, root reference; odepth is
+  // then the 4-wide walk's worst-case pending entries (build_bvh4)
+  const BvhNode4 *n4;
+  int root4;
+  int wide;
   int lane_sweep;  // scenes of at most this many spheres: loose lanes sweep every leaf slot instead (lane_sweep())
   int ordered;  // the host allows the ordered walk (tree depth <= kOrderedStack)
   int odepth;   // stack entries per lane (the tree depth)
@@ -433,6 +438,97 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
       }
       if (h0 || h1) {
         ref = h0 ? nd.c0 : nd.c1;
+        continue;
+      }
+    } else {
+      const int leaf = -(ref + 1), first = leaf >> 4, cnt = leaf & 15;
+      for (int k = 0; k < cnt; ++k) {
+        const float4 q = bv.pf[first + k];  // fp32 prefilter, as bvh_walk
+        const float wx = q.x - ox, wy = q.y - oy, wz = q.z - oz;
+        const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
+        const float R = q.w + bv.pmargin;
+        if (cx * cx + cy * cy + cz * cz > R * R * dd) continue;
+        if (!leaf_fn((int)bv.prims[first + k])) return;
+      }
+    }
+    bool more = false;
+    while (sp > 0) {
+      --sp;
+      const int2 e = st[sp * 64];
+      if (!((double)__int_as_float(e.y) > tmax_fn())) {
+        ref = e.x;
+        more = true;
+        break;
+      }
+    }
+    if (!more) return;
+  }
+}
+
+// Ordered closest-hit walk over the 4-wide nodes (rt_bvh.h BvhNode4): the
+// same grown fp32 slab test as bvh_walk_ordered on up to four child boxes,
+// the nearest entered, the other hits pushed farthest first (so the nearest
+// pending one is popped next), pops pruned against the current best.  Half
+// the iterations of the two-child walk (scripts/bvh_sim.cpp: 29 -> 15 wave
+// node-steps per primary query, 89 -> 46 per secondary, synth10k), each one
+// with four independent box tests.  Every leaf that can hold a closer root is
+// still visited, so the lexicographic (t, index) minimum is unchanged.
+template <typename T, typename F>
+__device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d, T &&tmax_fn, Work &work,
+                                                  F &&leaf_fn) {
+  const float ox = (float)(o.x - bv.c0x), oy = (float)(o.y - bv.c0y), oz = (float)(o.z - bv.c0z);
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+  const float dd = (dx * dx + dy * dy + dz * dz) * (1.0f + 1e-5f);
+  const float m = bv.margin;
+  {
+    const BvhNode &r0 = bv.nodes[0];
+    const float ax = (r0.lo[0] - m - ox) * ix, bx = (r0.hi[0] + m - ox) * ix;
+    const float ay = (r0.lo[1] - m - oy) * iy, by = (r0.hi[1] + m - oy) * iy;
+    const float az = (r0.lo[2] - m - oz) * iz, bz = (r0.hi[2] + m - oz) * iz;
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    if (!(tn <= tf && !((double)tn > tmax_fn()))) return;
+  }
+  int2 *st = bv.ostk + (threadIdx.x & 63);
+  int sp = 0;
+  int ref = bv.root4;
+  for (;;) {
+    work.cull += 1;
+    if (ref >= 0) {
+      const BvhNode4 *nd = bv.n4 + ref;
+      float t[4];
+      int r[4];
+      int hits = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float ax = (nd->lox[k] - m - ox) * ix, bx = (nd->hix[k] + m - ox) * ix;
+        const float ay = (nd->loy[k] - m - oy) * iy, by = (nd->hiy[k] + m - oy) * iy;
+        const float az = (nd->loz[k] - m - oz) * iz, bz = (nd->hiz[k] + m - oz) * iz;
+        const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+        const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+        const bool h = tn <= tf && !((double)tn > tmax_fn());  // NaN (unused slot) -> false
+        hits += h ? 1 : 0;
+        // sort key: a hit sorts below every miss (fminf keeps it finite-or-below-inf)
+        t[k] = h ? fminf(tn, 3.0e38f) : __builtin_inff();
+        r[k] = nd->c[k];
+      }
+      auto ce = [&](int a, int b) {  // compare-exchange, ascending
+        const bool sw = t[b] < t[a];
+        const float ta = sw ? t[b] : t[a], tb = sw ? t[a] : t[b];
+        const int ra = sw ? r[b] : r[a], rb = sw ? r[a] : r[b];
+        t[a] = ta, t[b] = tb, r[a] = ra, r[b] = rb;
+      };
+      ce(0, 1);
+      ce(2, 3);
+      ce(0, 2);
+      ce(1, 3);
+      ce(1, 2);
+      if (hits > 0) {
+        if (hits > 3) st[(sp++) * 64] = make_int2(r[3], __float_as_int(t[3]));
+        if (hits > 2) st[(sp++) * 64] = make_int2(r[2], __float_as_int(t[2]));
+        if (hits > 1) st[(sp++) * 64] = make_int2(r[1], __float_as_int(t[1]));
+        ref = r[0];
         continue;
       }
     } else {
@@ -686,6 +782,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       return true;
     };
     if (n <= bv.lane_sweep) lane_sweep(bv, n, o, d, tmax, work, leaf);
+    else if (bv.ostk && bv.wide) bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
     else if (bv.ostk) bvh_walk_ordered(bv, o, d, tmax, work, leaf);
     else bvh_walk(bv, o, d, tmax, work, leaf);
   }

@@ -730,6 +730,8 @@ struct rt_ctx {
   float4 *d_pf = nullptr;
   BvhNode2 *d_bvh2 = nullptr;
   int bvh2_root = -1, bvh_depth = 0, bvh_ordered = 1;  // RT_HIP_BVH_ORDERED
+  BvhNode4 *d_bvh4 = nullptr;  // 4-wide nodes for the ordered walk (RT_HIP_BVH4=0: two-child walk)
+  int bvh4_root = -1, bvh4_stack = 0, bvh_wide = 1;
   int bvh_nodes = 0;
   // per-light direction grids for shadow rays (rt_lightgrid.h), built at upload
   int32_t *d_lg_start = nullptr, *d_lg_ids = nullptr;
@@ -817,6 +819,8 @@ void free_scene(rt_ctx *c) {
   c->d_pf = nullptr;
   if (c->d_bvh2) (void)hipFree(c->d_bvh2);
   c->d_bvh2 = nullptr;
+  if (c->d_bvh4) (void)hipFree(c->d_bvh4);
+  c->d_bvh4 = nullptr;
   if (c->d_lg_start) (void)hipFree(c->d_lg_start);
   if (c->d_lg_ids) (void)hipFree(c->d_lg_ids);
   c->d_lg_start = c->d_lg_ids = nullptr;
@@ -840,8 +844,12 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   b.n2 = c->d_bvh2;
   b.root_ref = c->bvh2_root;
   b.nnodes = (c->bvh_on && c->cull) ? c->bvh_nodes : 0;
-  b.ordered = (c->bvh_ordered && c->d_bvh2 && c->bvh_depth <= kOrderedStack && b.nnodes > 0) ? 1 : 0;
-  b.odepth = std::max(1, c->bvh_depth);
+  b.n4 = c->d_bvh4;
+  b.root4 = c->bvh4_root;
+  b.wide = (c->bvh_wide && c->d_bvh4 && c->bvh4_stack <= kOrderedStack) ? 1 : 0;
+  b.ordered = (c->bvh_ordered && b.nnodes > 0 && (b.wide || (c->d_bvh2 && c->bvh_depth <= kOrderedStack))) ? 1 : 0;
+  if (!b.ordered) b.wide = 0;
+  b.odepth = std::max(1, b.wide ? c->bvh4_stack : c->bvh_depth);
   b.ostk = nullptr;  // set in the kernel (LDS)
   b.c0x = c->c0[0];
   b.c0y = c->c0[1];
@@ -1231,6 +1239,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_STACK")) c->stack_mode = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_XCD_MAP")) c->xcd_map = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_BVH_ORDERED")) c->bvh_ordered = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_BVH4")) c->bvh_wide = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(256, std::atoi(e)));
   auto bail = [&](int rc) {
@@ -1353,9 +1362,15 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
   std::vector<BvhNode2> nodes2;
   int depth2 = 0;
   const int32_t root2 = build_bvh2(nodes, nodes2, depth2);
+  std::vector<BvhNode4> nodes4;
+  int stack4 = 0;
+  const int32_t root4 = build_bvh4(nodes, nodes4, stack4);
   int rc = RT_OK;
   hipError_t e = hipSuccess;
   if ((e = hipMalloc(&c->d_bvh2, sizeof(BvhNode2) * (nodes2.size() + 1))) != hipSuccess ||
+      (e = hipMalloc(&c->d_bvh4, sizeof(BvhNode4) * (nodes4.size() + 1))) != hipSuccess ||
+      (!nodes4.empty() && (e = hipMemcpy(c->d_bvh4, nodes4.data(), sizeof(BvhNode4) * nodes4.size(),
+                                         hipMemcpyHostToDevice)) != hipSuccess) ||
       (!nodes2.empty() && (e = hipMemcpy(c->d_bvh2, nodes2.data(), sizeof(BvhNode2) * nodes2.size(),
                                          hipMemcpyHostToDevice)) != hipSuccess) ||
       (e = hipMalloc(&c->d_pf, sizeof(float4) * (pf.size() + 1))) != hipSuccess ||
@@ -1378,6 +1393,8 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
   c->bvh_nodes = (int)nodes.size();
   c->bvh2_root = root2;
   c->bvh_depth = depth2;
+  c->bvh4_root = root4;
+  c->bvh4_stack = stack4;
   {
     double d2 = 0.0;
     for (int k = 0; k < 3; k++) d2 += (hi[k] - lo[k]) * (hi[k] - lo[k]);

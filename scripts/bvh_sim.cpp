@@ -64,6 +64,7 @@ struct Bvh4 {
   std::vector<Node> n;
 };
 
+static long g_maxstk[3] = {0, 0, 0};
 static const std::vector<BvhNode> *g_nodes;
 static const std::vector<int32_t> *g_prims;
 
@@ -128,6 +129,28 @@ static void walk2(const Scene &s, const Strategy &st, V o, V d, bool shadow, dou
       continue;
     }
     int l = i + 1, r = N[i + 1].skip;
+    if (st.kind == 2) {  // 4-wide: the grandchildren of i (a leaf child stands for itself)
+      int cand[4], nc = 0;
+      for (int c : {l, r}) {
+        if (N[c].leaf >= 0) cand[nc++] = c;
+        else {
+          cand[nc++] = c + 1;
+          cand[nc++] = N[c + 1].skip;
+        }
+      }
+      nodes++;
+      std::pair<double, int> hits[4];
+      int nh = 0;
+      for (int k = 0; k < nc; k++) {
+        double a, b;
+        if (box(N[cand[k]].lo, N[cand[k]].hi, o, inv, a, b) && !(a > lim()) && (!st.forward || b >= 0))
+          hits[nh++] = {a, cand[k]};
+      }
+      std::sort(hits, hits + nh, [](auto &x, auto &y) { return x.first > y.first; });  // far first
+      for (int k = 0; k < nh; k++) stk.push_back({hits[k].second, hits[k].first});
+      g_maxstk[2] = std::max(g_maxstk[2], (long)stk.size());
+      continue;
+    }
     double tnl, tfl, tnr, tfr;
     nodes++;  // one visit tests both children (child boxes stored in the parent)
     bool hl = box(N[l].lo, N[l].hi, o, inv, tnl, tfl) && !(tnl > lim()) && (!st.forward || tfl >= 0);
@@ -140,6 +163,7 @@ static void walk2(const Scene &s, const Strategy &st, V o, V d, bool shadow, dou
         stk.push_back({l, tnl});
         stk.push_back({r, tnr});
       }
+      if (st.kind == 1) g_maxstk[1] = std::max(g_maxstk[1], (long)stk.size());
     } else if (hl)
       stk.push_back({l, tnl});
     else if (hr)
@@ -178,9 +202,8 @@ int main(int argc, char **argv) {
   g_nodes = &nodes;
   g_prims = &prims;
   std::printf("spheres %zu nodes %zu\n", s.r.size(), nodes.size());
-  const Strategy strats[] = {{"preorder-line", 0, false}, {"preorder-fwd", 0, true}, {"ordered-line", 1, false},
-                             {"ordered-fwd", 1, true}};
-  const int NS = 4;
+  const Strategy strats[] = {{"preorder-line", 0, false}, {"ordered-line", 1, false}, {"ordered4-line", 2, false}};
+  const int NS = 3;
   // stats[strategy][class]: class 0 primary closest, 1 primary shadow, 2 secondary closest, 3 secondary shadow
   Stats stats[NS][4];
   V P{cam.position[0], cam.position[1], cam.position[2]};
@@ -287,5 +310,6 @@ int main(int argc, char **argv) {
                   q.wave_tests / q.wq, q.wave_nodes, q.wave_tests);
     }
   }
+  std::printf("max stack: ordered %ld ordered4 %ld\n", g_maxstk[1], g_maxstk[2]);
   return 0;
 }
