@@ -450,16 +450,19 @@ def test_stack_modes_depth_edges(stack_renderer, depth):
             assert np.array_equal(got[k], want[y])
 
 
-@pytest.mark.parametrize("ordered", ["1", "0"])
+@pytest.mark.parametrize("walk", [{}, {"RT_HIP_BVH4": "0"}, {"RT_HIP_BVH_ORDERED": "0"}],
+                         ids=["ordered4", "ordered2", "stackless"])
 @pytest.mark.parametrize("seed,count", [(101, 700), (102, 1100), (103, 1600)])
-def test_large_scenes_global_memory_paths(monkeypatch, ordered, seed, count):
-    """Scenes too large for LDS (geometry and BVH read through L2, one-wave
-    workgroups): the ordered BVH walk (RT_HIP_BVH_ORDERED=1, default) and the
-    stackless one against the oracle."""
+def test_large_scenes_global_memory_paths(monkeypatch, walk, seed, count):
+    """Scenes read through L2 with the BVH fallback: the ordered 4-wide walk
+    (default), the ordered two-child walk (RT_HIP_BVH4=0) and the stackless
+    preorder walk (RT_HIP_BVH_ORDERED=0) against the oracle; above 1024 spheres
+    every group walks the tree (256-cell shadow grids, 2-sphere leaves)."""
     import orc
     import rt_hip
 
-    monkeypatch.setenv("RT_HIP_BVH_ORDERED", ordered)
+    for k, v in walk.items():
+        monkeypatch.setenv(k, v)
     r = rt_hip.Renderer(0)
     try:
         text = _random_scene(seed, count)
