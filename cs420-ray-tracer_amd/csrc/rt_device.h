@@ -343,8 +343,22 @@ struct BvhArgs {
   int ordered;  // the host allows the ordered walk (tree depth <= kOrderedStack)
   int odepth;   // stack entries per lane (the tree depth)
   int2 *ostk;
+  int ostk_off;  // ostk == nullptr: the stacks sit at this byte offset of dynamic LDS ([wave][entry][lane]); -1 none
 };
 constexpr int kOrderedStack = 24;  // pending far children; the host requires depth <= this
+
+// Dynamic LDS (every extern __shared__ array starts at its base).
+extern __shared__ __attribute__((aligned(32))) unsigned char rt_dyn_lds[];
+
+// This lane's entry 0 of the ordered walk's stack.
+__device__ __forceinline__ int2 *ordered_stack(const BvhArgs &bv) {
+  int2 *base = bv.ostk ? bv.ostk
+                       : reinterpret_cast<int2 *>(rt_dyn_lds + bv.ostk_off) +
+                             (size_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * bv.odepth * 64;
+  return base + (threadIdx.x & 63);
+}
+__device__ __forceinline__ bool has_ordered_stack(const BvhArgs &bv) { return bv.ostk || bv.ostk_off >= 0; }
+
 
 // Visits every leaf whose (grown) box the line meets and whose entry does not
 // exceed tmax_fn() (re-read per node: closest-hit tightens it); calls
@@ -418,7 +432,7 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
     return tn <= tf && !((double)tn > tmax_fn());
   };
-  int2 *st = bv.ostk + (threadIdx.x & 63);
+  int2 *st = ordered_stack(bv);
   int sp = 0;
   float tn;
   if (!slab(bv.nodes[0].lo, bv.nodes[0].hi, tn)) return;
@@ -490,7 +504,7 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
     if (!(tn <= tf && !((double)tn > tmax_fn()))) return;
   }
-  int2 *st = bv.ostk + (threadIdx.x & 63);
+  int2 *st = ordered_stack(bv);
   int sp = 0;
   int ref = bv.root4;
   for (;;) {
@@ -782,8 +796,8 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       return true;
     };
     if (n <= bv.lane_sweep) lane_sweep(bv, n, o, d, tmax, work, leaf);
-    else if (bv.ostk && bv.wide) bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
-    else if (bv.ostk) bvh_walk_ordered(bv, o, d, tmax, work, leaf);
+    else if (has_ordered_stack(bv) && bv.wide) bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
+    else if (has_ordered_stack(bv)) bvh_walk_ordered(bv, o, d, tmax, work, leaf);
     else bvh_walk(bv, o, d, tmax, work, leaf);
   }
 #ifdef RT_STAMPS

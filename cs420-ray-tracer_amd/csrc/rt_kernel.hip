@@ -46,6 +46,68 @@ __device__ unsigned long long g_timeline[kTimelineWaves * kTl];
 
 constexpr int kMaxLdsStack = 4;  // levels of the LDS reflection stack (render_kernel)
 
+// Output of a launch.  RT_FB_RGB8 with full = 0: rows.count x W RGB8 (the
+// rows of `rows`, rt_render); RT_FB_RGB8 with full = 1: a W x H RGB8 image in
+// PPM row order; RT_FB_F32X3 / RT_FB_F64X3: the reference's framebuffer,
+// index j*W + x with j = 0 the bottom row (src/main.cpp:156, kernel.cu:112),
+// unquantised.  Pixels x0 <= x < x0 + xw are written.
+struct OutDesc {
+  void *ptr;
+  int fmt, full, x0, xw;
+};
+
+// kStackSplit: level 0 here, the reflection levels through the ray queues of
+// rt_wavefront.h (wf_bounce), the unwind in wf_resolve.
+struct SplitArgs {
+  RayRec *rayq;       // [kShards][seg_cap]
+  unsigned *ray_cnt;  // [depth+1][kShards]
+  int seg_cap;
+  Term *term;         // [npx]
+  uint8_t *nlev;      // [npx]
+};
+
+// All arguments of render_kernel in one struct: its only kernel parameter, so
+// it sits at offset 0 of the kernarg segment and a member can be re-read from
+// there by offsetof (kernarg_late).
+struct RenderArgs {
+  const SphGeo *geo;
+  const double *radius;
+  const SphMat *mat;
+  const LightD *lights;
+  int n, nl;
+  D3 amb;
+  Cam cam;
+  int W, H, depth;
+  Rows rows;
+  BvhArgs bv;
+  LgArgs lg;
+  OutDesc od;
+  StackEnt *gstack;
+  unsigned long long *counters;
+  int ntx, ntiles, xcd_per;
+  SplitArgs sa;
+  const int *perm;
+};
+
+// Member `x` (at offset kOff of RenderArgs) re-read from the kernarg segment
+// here.  Kernel arguments are otherwise loaded into SGPRs at entry and live
+// for the whole kernel; the big loop-invariant ones (BVH and light-grid
+// descriptors) then spill to VGPR lanes, paid for with v_readlane /
+// v_writelane in the level and light loops.  The empty asm makes the kernarg
+// pointer opaque, so the scalar loads happen at this point and their
+// registers are free again afterwards.  kLate = false returns x itself.
+template <bool kLate, size_t kOff, class T>
+__device__ __forceinline__ const T &kernarg_late(const T &x) {
+  if constexpr (!kLate) {
+    return x;
+  } else {
+    typedef const __attribute__((address_space(4))) unsigned char KB;
+    KB *p = (KB *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const T *)(p + kOff);
+  }
+}
+
 // One bounce of trace_ray (src/main.cpp:16-58) for the wave's `alive` lanes:
 // closest hit, sky on a miss, Phong shading with per-light shadow queries,
 // and the reflection decision (main.cpp:43-55).  Outcome per alive lane:
@@ -53,16 +115,19 @@ constexpr int kMaxLdsStack = 4;  // levels of the LDS reflection stack (render_k
 // when no depth is left) or kSpawned (colour = shade*(1-refl), refl, and the
 // reflection ray no/nd leaving sphere nkey).  Wave-uniform control flow.
 enum { kEnded = 1, kSpawned = 2 };
-template <bool kCull>
+// kArgMem: bv and lg are the kernel's own arguments (kernarg segment), so they
+// are re-read where needed (kernarg_late) instead of held in SGPRs throughout.
+template <bool kCull, bool kArgMem = false>
 __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                        const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
-                                       int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg, bool alive, D3 o, D3 d,
+                                       int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o, D3 d,
                                        int key, int dleft, Work &work, unsigned &c_shadow, int &outcome, D3 &color,
                                        double &refl, D3 &no, D3 &nd, int &nkey) {
   outcome = 0;
   double bt;
   RT_T0(t_cl);
-  const int bi = sweep_closest<kCull>(g, rad, n, alive, o, d, key, bv, bt, work);
+  const int bi =
+      sweep_closest<kCull>(g, rad, n, alive, o, d, key, kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt, work);
   RT_ACC(work, 8, t_cl);
   const bool hit = alive && bi >= 0;
   if (alive && !hit) {  // sky, main.cpp:26-30
@@ -85,9 +150,13 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
       const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
       const D3 view = normalized(sub(o, hp));                       // main.cpp:38
       const D3 mc = mk(m.cr, m.cg, m.cb);
-      LgRange next = lg.on && nl > 0 ? lg_range(lg, 0, hp, mk(slight[0].px, slight[0].py, slight[0].pz), hit)
-                                     : LgRange{0, 0};
+      LgRange next{0, 0};
+      {
+        const LgArgs &lg0 = kernarg_late<kArgMem, offsetof(RenderArgs, lg)>(lg_arg);
+        if (lg0.on && nl > 0) next = lg_range(lg0, 0, hp, mk(slight[0].px, slight[0].py, slight[0].pz), hit);
+      }
       for (int l = 0; l < nl; ++l) {
+        const LgArgs &lg = kernarg_late<kArgMem, offsetof(RenderArgs, lg)>(lg_arg);
         RT_T0(t_setup);
         // this light's first list id, and the next light's cell range, are
         // loaded now and consumed after the setup arithmetic below
@@ -103,7 +172,8 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
         RT_ACC(work, 3, t_setup);
         RT_T0(t_sh);
         const bool occ = lg.on ? shadow_cells(g, n, hit, so, sd, lp, dist, lg, l, cell, id0, work)
-                               : sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, hi, dist, bv, work);
+                               : sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, hi, dist,
+                                                     kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), work);
         RT_ACC(work, 9, t_sh);
         RT_T0(t_shade);
         if (hit && !occ) {
@@ -150,7 +220,7 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
 // sbase[sidx + level * sstride] (depth - 1 levels), unwound innermost first.
 // The wave-uniform base and a 32-bit lane index (not a per-lane 64-bit
 // pointer) keep the stack address out of the registers that spill.
-template <bool kCull>
+template <bool kCull, bool kArgMem = false>
 __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                          const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                          int nl, D3 amb, int depth, const BvhArgs &bv, const LgArgs &lg, bool live,
@@ -166,8 +236,8 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
     int outcome, nkey = 0;
     D3 color = res, no = o, nd = d;
     double refl = 0.0;
-    bounce<kCull>(g, rad, mat, slight, n, nl, amb, bv, lg, alive, o, d, key, dleft, work, c_shadow, outcome, color,
-                  refl, no, nd, nkey);
+    bounce<kCull, kArgMem>(g, rad, mat, slight, n, nl, amb, bv, lg, alive, o, d, key, dleft, work, c_shadow, outcome,
+                           color, refl, no, nd, nkey);
     if (alive) {
       if (outcome == kSpawned) {
         sbase[sidx + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
@@ -280,15 +350,6 @@ __device__ __forceinline__ D3 trace_compact(const SphGeo *__restrict__ g, const 
   return res;
 }
 
-// Output of a launch.  RT_FB_RGB8 with full = 0: rows.count x W RGB8 (the
-// rows of `rows`, rt_render); RT_FB_RGB8 with full = 1: a W x H RGB8 image in
-// PPM row order; RT_FB_F32X3 / RT_FB_F64X3: the reference's framebuffer,
-// index j*W + x with j = 0 the bottom row (src/main.cpp:156, kernel.cu:112),
-// unquantised.  Pixels x0 <= x < x0 + xw are written.
-struct OutDesc {
-  void *ptr;
-  int fmt, full, x0, xw;
-};
 
 // One 8x8 tile of pixels, one lane per pixel; `samples` = 1 (the serial
 // path) or 4 (main_gpu.cu:249-333's antialias offsets, in fp64 serial
@@ -301,22 +362,13 @@ struct CompactArgs {
   int *qcnt;         // LDS
   TermRec *term;     // LDS
 };
-// kStackSplit: level 0 here, the reflection levels through the ray queues of
-// rt_wavefront.h (wf_bounce), the unwind in wf_resolve.
-struct SplitArgs {
-  RayRec *rayq;       // [kShards][seg_cap]
-  unsigned *ray_cnt;  // [depth+1][kShards]
-  int seg_cap;
-  Term *term;         // [npx]
-  uint8_t *nlev;      // [npx]
-};
 
 // Reflection stack placement: kStackLds = [level][lane] per wave in LDS (4
 // levels), kStackGlobal = [level][pixel] in global memory (any depth),
 // kStackCompact = global, with the workgroup-compacted levels of trace_compact.
 // kStackSplit = level 0 only, the rest queued (SplitArgs).
 enum { kStackLds = 0, kStackGlobal = 1, kStackCompact = 2, kStackSplit = 3 };
-template <bool kCull, int kSamples, int kStack>
+template <bool kCull, int kSamples, int kStack, bool kArgMem = false>
 __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                            const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                            int nl, D3 amb, const Cam &cam, int W, int H, int depth, const Rows &rows,
@@ -353,8 +405,8 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
       D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;  // depth <= 0 -> black (main.cpp:17-18)
       double refl = 0.0;
       if (__ballot(alive))
-        bounce<kCull>(g, rad, mat, slight, n, nl, amb, bv, lg, alive, o, d, -1, depth, work, c_shadow, outcome,
-                      color, refl, no, nd, nkey);
+        bounce<kCull, kArgMem>(g, rad, mat, slight, n, nl, amb, bv, lg, alive, o, d, -1, depth, work, c_shadow,
+                               outcome, color, refl, no, nd, nkey);
       const bool spawn = alive && outcome == kSpawned;
       if (in_img && !spawn) {
         sa.term[pix] = Term{color.x, color.y, color.z};
@@ -373,10 +425,10 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
       c = trace_compact<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, pix, ca.gstack, ca.npx,
                                ca.q, ca.qcnt, ca.term, work, c_prim, c_shadow, c_reflect);
     else if (kStack == kStackGlobal)
-      c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, ca.gstack, (unsigned)pix, (unsigned)ca.npx,
+      c = trace_wave<kCull, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, ca.gstack, (unsigned)pix, (unsigned)ca.npx,
                             work, c_prim, c_shadow, c_reflect);
     else
-      c = trace_wave<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk, (unsigned)lane, 64u, work,
+      c = trace_wave<kCull, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk, (unsigned)lane, 64u, work,
                             c_prim, c_shadow, c_reflect);
     acc = kSamples == 1 ? c : add(acc, c);  // serial: the colour itself; AA: from 0 in sample order (main_gpu.cu:250, 327)
   }
@@ -517,44 +569,46 @@ constexpr size_t kLdsCompactBytes = (size_t)kWaves * 64 * (sizeof(QRay) + sizeof
 
 template <bool kLdsGeo, bool kCull, int kSamples, int kStack>
 __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PER_EU) void render_kernel(
-    const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
-    const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
-    BvhArgs bv_in, LgArgs lg, OutDesc od, StackEnt *__restrict__ gstack, unsigned long long *__restrict__ counters,
-    int ntx, int ntiles, int xcd_per, SplitArgs sa, const int *__restrict__ perm) {  // xcd_per: tiles per run
-  // 16x16-pixel workgroup tile.  Workgroups are dealt to the 8 XCDs round
-  // robin (b % 8).  With chunk > 0 the scanline-ordered tiles are cut into
-  // runs of `chunk` tiles and run r goes to XCD r % 8: each XCD's L2 serves
-  // a few compact image regions (locality for scene data read through L2)
-  // while every XCD still samples the whole image (balance).
+    const RenderArgs a) {
+  // Workgroups are dealt to the 8 XCDs round robin (b % 8).  perm: the host's
+  // launch order (rt_sched.h).  Otherwise, with xcd_per > 0 the
+  // scanline-ordered tiles are cut into runs of `xcd_per` tiles and run r goes
+  // to XCD r % 8: each XCD's L2 serves a few compact image regions while every
+  // XCD still samples the whole image.
   const int b = blockIdx.x;
   int tile = b;
-  if (perm) {
-    if (b >= ntiles) return;
-    tile = perm[b];  // launch order (rt_sched.h): heaviest predicted tiles first
-  } else if (xcd_per > 0) {
+  if (a.perm) {
+    if (b >= a.ntiles) return;
+    tile = a.perm[b];  // heaviest predicted tiles first
+  } else if (a.xcd_per > 0) {
     const int m = b >> 3;  // this workgroup's rank on its XCD
-    tile = ((m / xcd_per) * 8 + (b & 7)) * xcd_per + m % xcd_per;
+    tile = ((m / a.xcd_per) * 8 + (b & 7)) * a.xcd_per + m % a.xcd_per;
   }
-  if (tile >= ntiles) return;  // workgroup-uniform, before any barrier
-  const int tx = tile % ntx, ty = tile / ntx;
+  if (tile >= a.ntiles) return;  // workgroup-uniform, before any barrier
+  const int tx = tile % a.ntx, ty = tile / a.ntx;
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
   const SphGeo *g;
   const double *rad;
   const LightD *slight;
   const SphMat *sm;
-  BvhArgs bv = bv_in;
-  stage_scene<kLdsGeo>(smem, geo, radius, mat, lights, n, nl, bv, g, rad, sm, slight);
-  const size_t stack_off = (lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31;
+  // With the scene staged in LDS the BVH arguments are a modified local copy;
+  // otherwise the kernel argument itself is used (re-read from the kernarg
+  // segment where needed: kernarg_late) and the ordered walk finds its LDS
+  // stacks at bv.ostk_off (set by the host).
+  BvhArgs bv_local = a.bv;
+  stage_scene<kLdsGeo>(smem, a.geo, a.radius, a.mat, a.lights, a.n, a.nl, bv_local, g, rad, sm, slight);
+  const size_t stack_off = (lds_layout(kLdsGeo, a.n, a.nl, a.bv.nnodes).end + 31) & ~(size_t)31;
   // the ordered BVH walk's per-lane stacks, [wave][entry][lane], after the scene
-  if ((kStack == kStackGlobal || kStack == kStackSplit) && bv.ordered)
-    bv.ostk = reinterpret_cast<int2 *>(smem + stack_off) + (size_t)(threadIdx.x >> 6) * bv.odepth * 64;
+  if (kLdsGeo && (kStack == kStackGlobal || kStack == kStackSplit) && bv_local.ordered)
+    bv_local.ostk = reinterpret_cast<int2 *>(smem + stack_off) + (size_t)(threadIdx.x >> 6) * bv_local.odepth * 64;
+  const BvhArgs &bv = kLdsGeo ? bv_local : a.bv;
   constexpr int kWg = wg_waves<kLdsGeo, kStack>();
   constexpr int kWx = kWg == 4 ? 2 : 1;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: keeps tile coordinates in SGPRs
   StackEnt *stk = reinterpret_cast<StackEnt *>(smem + stack_off) + (size_t)wave * kMaxLdsStack * 64;
   CompactArgs ca;
-  ca.gstack = gstack;
-  ca.npx = (size_t)rows.count * od.xw;
+  ca.gstack = a.gstack;
+  ca.npx = (size_t)a.rows.count * a.od.xw;
   ca.q = reinterpret_cast<QRay *>(smem + stack_off);
   ca.term = reinterpret_cast<TermRec *>(smem + stack_off + (size_t)kWaves * 64 * sizeof(QRay));
   ca.qcnt = reinterpret_cast<int *>(smem + stack_off + (size_t)kWaves * 64 * (sizeof(QRay) + sizeof(TermRec)));
@@ -564,14 +618,14 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
 #ifdef RT_STAMPS
   const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  trace_tile<kCull, kSamples, kStack>(g, rad, sm, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
-                                        od.x0 + tx * (8 * kWx) + (wave % kWx) * 8,
-                                        ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, sa, work, sums);
+  trace_tile<kCull, kSamples, kStack, !kLdsGeo>(g, rad, sm, slight, a.n, a.nl, a.amb, a.cam, a.W, a.H, a.depth, a.rows,
+                                                bv, a.lg, a.od, a.od.x0 + tx * (8 * kWx) + (wave % kWx) * 8,
+                                                ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, a.sa, work, sums);
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
   record_timeline(tile * kWg + wave, t_real0, work);
 #endif
-  flush_counts(counters, sums, work);
+  flush_counts(a.counters, sums, work);
 }
 
 // Reflection level `level` of the split pipeline (RT_HIP_PIPELINE=3): one
@@ -850,7 +904,8 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   b.ordered = (c->bvh_ordered && b.nnodes > 0 && (b.wide || (c->d_bvh2 && c->bvh_depth <= kOrderedStack))) ? 1 : 0;
   if (!b.ordered) b.wide = 0;
   b.odepth = std::max(1, b.wide ? c->bvh4_stack : c->bvh_depth);
-  b.ostk = nullptr;  // set in the kernel (LDS)
+  b.ostk = nullptr;  // set in the kernel (LDS), or found at ostk_off
+  b.ostk_off = -1;
   b.c0x = c->c0[0];
   b.c0y = c->c0[1];
   b.c0z = c->c0[2];
@@ -922,9 +977,12 @@ int tile_perm(rt_ctx *c, const Cam &cam, int W, int H, const Rows &rows, const O
 template <bool kLds, bool kCull, int kSamples, int kStack>
 int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
                  const OutDesc &od, const SplitArgs &sa = SplitArgs{}, StackEnt *split_stack = nullptr) {
-  const BvhArgs bv = bvh_args(c, cam);
+  BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
   constexpr int kWg = wg_waves<kLds, kStack>(), kWx = kWg == 4 ? 2 : 1, kWy = kWg / kWx;
+  // the ordered walk's stacks follow the scene in LDS (render_kernel, kStackGlobal / kStackSplit)
+  if ((kStack == kStackGlobal || kStack == kStackSplit) && bv.ordered)
+    bv.ostk_off = (int)((lds_layout(kLds, c->nsph, c->nlight, bv.nnodes).end + 31) & ~(size_t)31);
   const int ntx = (od.xw + 8 * kWx - 1) / (8 * kWx), nty = (rows.count + 8 * kWy - 1) / (8 * kWy);
   const long long ntiles = (long long)ntx * nty;
   if (ntiles > (1LL << 30)) return RT_ERR_INVALID_ARG;
@@ -958,9 +1016,30 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     int rc = tile_perm(c, cam, W, H, rows, od, 8 * kWx, 8 * kWy, ntiles, perm);
     if (rc != RT_OK) return rc;
   }
-  hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream,
-                     c->d_geo, c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv,
-                     lg, od, gstack, c->d_counters, ntx, (int)ntiles, xcd_per, sa, perm);
+  RenderArgs ra{};
+  ra.geo = c->d_geo;
+  ra.radius = c->d_rad;
+  ra.mat = c->d_mat;
+  ra.lights = c->d_lights;
+  ra.n = c->nsph;
+  ra.nl = c->nlight;
+  ra.amb = amb;
+  ra.cam = cam;
+  ra.W = W;
+  ra.H = H;
+  ra.depth = depth;
+  ra.rows = rows;
+  ra.bv = bv;
+  ra.lg = lg;
+  ra.od = od;
+  ra.gstack = gstack;
+  ra.counters = c->d_counters;
+  ra.ntx = ntx;
+  ra.ntiles = (int)ntiles;
+  ra.xcd_per = xcd_per;
+  ra.sa = sa;
+  ra.perm = perm;
+  hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
   return RT_OK;
 }
 
