@@ -371,10 +371,14 @@ enum { kStackLds = 0, kStackGlobal = 1, kStackCompact = 2, kStackSplit = 3 };
 template <bool kCull, int kSamples, int kStack, bool kArgMem = false>
 __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                            const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
-                                           int nl, D3 amb, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                                           const BvhArgs &bv, const LgArgs &lg, const OutDesc &od, int x0, int k0,
-                                           StackEnt *stk, const CompactArgs &ca, const SplitArgs &sa,
-                                           Work &work, unsigned long long (&sums)[4]) {
+                                           int nl, D3 amb, const Cam &cam, int W_arg, int H_arg, int depth,
+                                           const Rows &rows_arg, const BvhArgs &bv, const LgArgs &lg,
+                                           const OutDesc &od_arg, int x0, int k0, StackEnt *stk,
+                                           const CompactArgs &ca, const SplitArgs &sa, Work &work,
+                                           unsigned long long (&sums)[4]) {
+  const int W = W_arg, H = H_arg;
+  const Rows &rows = rows_arg;
+  const OutDesc &od = od_arg;
   const int lane = threadIdx.x & 63;
   const int x = x0 + (lane & 7);
   const int k = k0 + (lane >> 3);
@@ -434,8 +438,13 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
   }
   const D3 res = kSamples == 4 ? scale(acc, 0.25) : acc;  // main_gpu.cu:331, 1/4 is exact
   // The pixel's coordinates are recomputed from the lane id (mbcnt) rather
-  // than kept live across the trace, which would spill them to scratch.
+  // than kept live across the trace, which would spill them to scratch; the
+  // output descriptors are re-read from the kernarg segment (kArgMem).
   {
+    const OutDesc &od = kernarg_late<kArgMem, offsetof(RenderArgs, od)>(od_arg);
+    const Rows &rows = kernarg_late<kArgMem, offsetof(RenderArgs, rows)>(rows_arg);
+    const int W = kernarg_late<kArgMem, offsetof(RenderArgs, W)>(W_arg);
+    const int H = kernarg_late<kArgMem, offsetof(RenderArgs, H)>(H_arg);
     const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
     const int x = x0 + (lane & 7);
     const int k = k0 + (lane >> 3);
@@ -625,7 +634,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
 #ifdef RT_STAMPS
   record_timeline(tile * kWg + wave, t_real0, work);
 #endif
-  flush_counts(a.counters, sums, work);
+  flush_counts(kernarg_late<!kLdsGeo, offsetof(RenderArgs, counters)>(a.counters), sums, work);
 }
 
 // Reflection level `level` of the split pipeline (RT_HIP_PIPELINE=3): one
