@@ -657,12 +657,16 @@ __device__ __forceinline__ void stage_scene(unsigned char *smem, const SphGeo *g
       }
     }
   }
-  for (int i = tid; i < nl; i += nt) slight[i] = lights[i];
+  // lights: staged with a staged scene; otherwise read from global memory at
+  // wave-uniform indices, i.e. scalar loads into SGPRs instead of LDS reads
+  // into VGPRs (the light loop is where VGPR pressure peaks)
+  if (kLdsGeo)
+    for (int i = tid; i < nl; i += nt) slight[i] = lights[i];
   __syncthreads();
   g = kLdsGeo ? sgeo : geo;
   rad = kLdsGeo ? srad : radius;
   sm = (kLdsGeo && RT_MAT_LDS) ? smat : mat;
-  sl = slight;
+  sl = kLdsGeo ? slight : lights;
   if (kLdsGeo) {
     bv.nodes = snodes;
     bv.prims = sprims;

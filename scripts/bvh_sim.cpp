@@ -65,6 +65,7 @@ struct Bvh4 {
 };
 
 static long g_maxstk[3] = {0, 0, 0};
+static double g_zero[4][4];  // per class: lane queries, zero-term lanes, wave queries, all-zero waves
 static const std::vector<BvhNode> *g_nodes;
 static const std::vector<int32_t> *g_prims;
 
@@ -263,6 +264,25 @@ int main(int argc, char **argv) {
           nrm[l] = nrmz(hp[l] - s.c[bi[l]]);
         }
         for (size_t L = 0; L < s.lights.size(); L++) {
+          // shadow queries whose Phong term is exactly zero (n.l <= 0 and r.v <= 0)
+          {
+            int nh = 0, nz = 0;
+            for (int l = 0; l < 64; l++) {
+              if (!hit[l]) continue;
+              nh++;
+              V ld = nrmz(s.lights[L] - hp[l]);
+              V view = nrmz(o[l] - hp[l]);
+              V nl2 = ld * -1.0;
+              V r = nl2 - nrm[l] * (2.0 * dot(nl2, nrm[l]));
+              if (dot(nrm[l], ld) <= 0 && dot(r, view) <= 0) nz++;
+            }
+            if (nh) {
+              g_zero[cls][0] += nh;
+              g_zero[cls][1] += nz;
+              g_zero[cls][2] += 1;
+              g_zero[cls][3] += nz == nh;
+            }
+          }
           for (int k = 0; k < NS; k++) {
             long mx_n = 0, mx_t = 0, any = 0;
             for (int l = 0; l < 64; l++) {
@@ -310,6 +330,9 @@ int main(int argc, char **argv) {
                   q.wave_tests / q.wq, q.wave_nodes, q.wave_tests);
     }
   }
+  for (int c = 0; c < 4; c += 2)
+    std::printf("zero-term shadow queries, %s: lanes %.1f %%, whole waves %.1f %%\n", c ? "secondary" : "primary",
+                100 * g_zero[c][1] / g_zero[c][0], 100 * g_zero[c][3] / g_zero[c][2]);
   std::printf("max stack: ordered %ld ordered4 %ld\n", g_maxstk[1], g_maxstk[2]);
   return 0;
 }
