@@ -87,6 +87,7 @@ struct RenderArgs {
   int ntx, ntiles, xcd_per;
   SplitArgs sa;
   const int *perm;
+  unsigned long long *zero_next;  // counters of the next launch, zeroed by workgroup 0 (or nullptr)
 };
 
 // Member `x` (at offset kOff of RenderArgs) re-read from the kernarg segment
@@ -585,6 +586,8 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   // to XCD r % 8: each XCD's L2 serves a few compact image regions while every
   // XCD still samples the whole image.
   const int b = blockIdx.x;
+  if (b == 0 && a.zero_next)
+    for (int i = (int)threadIdx.x; i < kShards * kShardStride; i += (int)blockDim.x) a.zero_next[i] = 0ull;
   int tile = b;
   if (a.perm) {
     if (b >= a.ntiles) return;
@@ -821,7 +824,14 @@ struct rt_ctx {
   int nsph = 0, nlight = 0;
   double amb[3] = {0, 0, 0};
   bool has_scene = false;
+  // Counters: two halves of one allocation, alternating by launch; d_counters
+  // is the half of the latest launch (what rt_render_stats reads).  A
+  // render_kernel launch zeroes the other half for the next launch, so the
+  // default path needs no separate memset (a fill kernel per frame).
   unsigned long long *d_counters = nullptr;
+  unsigned long long *d_ctr_base = nullptr;
+  bool ctr_clean[2] = {true, true};
+  bool zero_pending = false;  // the launch being enqueued zeroes the other half
   unsigned long long *h_counters = nullptr;  // pinned
   // In-stream HIP events around every render launch (a ring), so a caller can
   // time a whole region of launches and read the per-launch durations after.
@@ -1048,6 +1058,10 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.xcd_per = xcd_per;
   ra.sa = sa;
   ra.perm = perm;
+  // zero the other counter half for the next launch (enqueue's alternation)
+  const int next = (int)((c->launches + 1) & 1);
+  ra.zero_next = c->d_ctr_base + (size_t)next * kShards * kShardStride;
+  c->zero_pending = true;
   hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
   return RT_OK;
 }
@@ -1263,7 +1277,12 @@ int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_
 
 int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows &r, const OutDesc &od) {
   RT_TRY(c, hipSetDevice(c->device));
-  RT_TRY(c, hipMemsetAsync(c->d_counters, 0, kShards * kShardStride * sizeof(unsigned long long), c->stream));
+  const int half = (int)(c->launches & 1);
+  c->d_counters = c->d_ctr_base + (size_t)half * kShards * kShardStride;
+  if (!c->ctr_clean[half])
+    RT_TRY(c, hipMemsetAsync(c->d_counters, 0, kShards * kShardStride * sizeof(unsigned long long), c->stream));
+  c->ctr_clean[half] = false;
+  c->zero_pending = false;
   const int slot = (int)(c->launches % rt_ctx::kRing);
   RT_TRY(c, hipEventRecord(c->ev0[slot], c->stream));
   if (r.count > 0) {
@@ -1290,6 +1309,8 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
     RT_TRY(c, hipGetLastError());
   }
   RT_TRY(c, hipEventRecord(c->ev1[slot], c->stream));
+  if (c->zero_pending) c->ctr_clean[(c->launches + 1) & 1] = true;
+  c->zero_pending = false;
   c->launches++;
   return RT_OK;  // the counters are read back by rt_render_stats, after the stream drains
 }
@@ -1342,7 +1363,11 @@ int rt_create(int device, rt_ctx **out) {
   }
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(RT_ERR_HIP);
   c->stream = c->own_stream;
-  if (hipMalloc(&c->d_counters, kShards * kShardStride * sizeof(unsigned long long)) != hipSuccess) return bail(RT_ERR_OUT_OF_MEMORY);
+  if (hipMalloc(&c->d_ctr_base, 2 * kShards * kShardStride * sizeof(unsigned long long)) != hipSuccess)
+    return bail(RT_ERR_OUT_OF_MEMORY);
+  if (hipMemset(c->d_ctr_base, 0, 2 * kShards * kShardStride * sizeof(unsigned long long)) != hipSuccess)
+    return bail(RT_ERR_HIP);
+  c->d_counters = c->d_ctr_base;
   if (hipHostMalloc(&c->h_counters, kShards * kShardStride * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
     return bail(RT_ERR_OUT_OF_MEMORY);
   std::memset(c->h_counters, 0, kShards * kShardStride * sizeof(unsigned long long));
@@ -1358,7 +1383,7 @@ void rt_destroy(rt_ctx *c) {
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
   free_scene(c);
-  if (c->d_counters) (void)hipFree(c->d_counters);
+  if (c->d_ctr_base) (void)hipFree(c->d_ctr_base);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->d_tmp) (void)hipFree(c->d_tmp);
   if (c->wf_buf) (void)hipFree(c->wf_buf);
