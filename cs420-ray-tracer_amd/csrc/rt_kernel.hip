@@ -221,21 +221,25 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
 // sbase[sidx + level * sstride] (depth - 1 levels), unwound innermost first.
 // The wave-uniform base and a 32-bit lane index (not a per-lane 64-bit
 // pointer) keep the stack address out of the registers that spill.
-template <bool kCull, bool kArgMem = false>
+// kPark: a lane's final colour is parked in LDS (park[lane], this wave's
+// slice) when its chain ends instead of being held in registers while the
+// wave's other lanes keep bouncing (6 VGPRs fewer in the level loop).
+template <bool kCull, bool kArgMem = false, bool kPark = false>
 __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                          const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                          int nl, D3 amb, int depth, const BvhArgs &bv, const LgArgs &lg, bool live,
                                          D3 o, D3 d, StackEnt *sbase, unsigned sidx, unsigned sstride, Work &work, unsigned &c_prim,
-                                         unsigned &c_shadow, unsigned &c_reflect) {
+                                         unsigned &c_shadow, unsigned &c_reflect, D3 *park = nullptr) {
   int lev = 0;
   int dleft = depth;
   D3 res = mk(0.0, 0.0, 0.0);     // depth <= 0 -> black (main.cpp:17-18)
   bool alive = live && depth >= 1;
+  const bool traced = alive;
   int key = -1;  // sphere the current ray leaves (-1: camera), groups lanes in sweeps
   c_prim += alive ? 1u : 0u;
   while (__ballot(alive)) {
     int outcome, nkey = 0;
-    D3 color = res, no = o, nd = d;
+    D3 color = kPark ? mk(0.0, 0.0, 0.0) : res, no = o, nd = d;
     double refl = 0.0;
     bounce<kCull, kArgMem>(g, rad, mat, slight, n, nl, amb, bv, lg, alive, o, d, key, dleft, work, c_shadow, outcome,
                            color, refl, no, nd, nkey);
@@ -249,11 +253,13 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
         --dleft;
         ++c_reflect;
       } else {
-        res = color;
+        if (kPark) park[threadIdx.x & 63] = color;
+        else res = color;
         alive = false;
       }
     }
   }
+  if (kPark && traced) res = park[threadIdx.x & 63];
   while (lev > 0) {  // unwind: shade*(1-refl) + reflected*refl, innermost first
     --lev;
     const StackEnt e = sbase[sidx + (unsigned)lev * sstride];
@@ -357,6 +363,7 @@ __device__ __forceinline__ D3 trace_compact(const SphGeo *__restrict__ g, const 
 // semantics: samples summed in order, then * 0.25).  Adds the tile's ray
 // counts to the wave sums.
 struct CompactArgs {
+  D3 *park;  // kStackGlobal with kernarg-resident arguments: this wave's parked colours (LDS)
   StackEnt *gstack;  // [depth-1][npx]
   size_t npx;
   QRay *q;           // LDS
@@ -430,8 +437,9 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
       c = trace_compact<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, pix, ca.gstack, ca.npx,
                                ca.q, ca.qcnt, ca.term, work, c_prim, c_shadow, c_reflect);
     else if (kStack == kStackGlobal)
-      c = trace_wave<kCull, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, ca.gstack, (unsigned)pix, (unsigned)ca.npx,
-                            work, c_prim, c_shadow, c_reflect);
+      c = trace_wave<kCull, kArgMem, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, ca.gstack,
+                                              (unsigned)pix, (unsigned)ca.npx, work, c_prim, c_shadow, c_reflect,
+                                              ca.park);
     else
       c = trace_wave<kCull, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk, (unsigned)lane, 64u, work,
                             c_prim, c_shadow, c_reflect);
@@ -619,6 +627,10 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: keeps tile coordinates in SGPRs
   StackEnt *stk = reinterpret_cast<StackEnt *>(smem + stack_off) + (size_t)wave * kMaxLdsStack * 64;
   CompactArgs ca;
+  ca.park = nullptr;
+  if (!kLdsGeo && kStack == kStackGlobal)  // after the ordered walk's stacks (launch_tiles sizes both)
+    ca.park = reinterpret_cast<D3 *>(smem + stack_off + (a.bv.ordered ? (size_t)kWg * a.bv.odepth * 64 * sizeof(int2) : 0)) +
+              (size_t)wave * 64;
   ca.gstack = a.gstack;
   ca.npx = (size_t)a.rows.count * a.od.xw;
   ca.q = reinterpret_cast<QRay *>(smem + stack_off);
@@ -1015,6 +1027,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   // the kernel places the ordered walk's stacks from these same arguments
   if ((kStack == kStackGlobal || kStack == kStackSplit) && bv.ordered)
     lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
+  if (!kLds && kStack == kStackGlobal) lds += (size_t)kWg * 64 * sizeof(D3);  // parked colours (trace_wave)
   StackEnt *gstack = split_stack;
   if (kStack != kStackLds && kStack != kStackSplit && depth > 1) {
     // the kernel indexes the stack with 32 bits: entry + level * npx < 2^32
