@@ -4,12 +4,14 @@
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
 
 A step renders ONE frame of the workload: each rank traces its cyclic 8-row
-bands through librt_hip.so (rt_render_async on torch's current stream, output
-resident in HBM), then the shards are gathered to rank 0 with RCCL
-(torch.distributed "nccl" = RCCL over xGMI) and unpermuted into the final
-PPM-ordered framebuffer on device.  For N > 1 the frames are pipelined in
-batches (--frames-per-gather, default 4): a batch renders while the previous
-batch's shards travel to rank 0 in one gather.  Total work per step is fixed
+bands through librt_hip.so (on torch's current stream, output resident in
+HBM), then the shards are gathered to rank 0 with RCCL (torch.distributed
+"nccl" = RCCL over xGMI) and unpermuted into the final PPM-ordered
+framebuffer on device.  Frames are rendered in batches of
+--frames-per-launch (default 16), one rt_render_frames_async launch per batch,
+so the slowest tiles of one frame overlap the other frames' work; for N > 1
+a batch renders while the previous batch's shards travel to rank 0 in one
+gather.  Every frame is rendered and delivered in full.  Total work per step is fixed
 as N grows ("scaling": "strong").  value = rays of the frame x K / max-over-ranks wall
 time of the K timed steps.
 
@@ -109,10 +111,13 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     r.set_stream(stream.cuda_stream)  # the kernel runs on torch's stream: events and RCCL order with it
     rows = rt_hip.rows_for_shard(H, BAND, rank, world) if dist_on else rt_hip.rt_rows(1, 0, 1, H)
     R = rows.count
-    # two shard / gather buffers of `batch` frames each: a batch renders while
-    # the previous one is gathered to rank 0 by one RCCL gather (rt_frames)
-    F = batch if dist_on else 1
+    # two shard / gather buffers of `batch` frames each: a batch is rendered by
+    # ONE launch (rt_render_frames_async) while the previous one is gathered to
+    # rank 0 by one RCCL gather (rt_frames); at N = 1 the batches alternate
+    # between the two buffers the same way, without the gather
+    F = batch
     shards = [torch.empty((F, R, W, 3), dtype=torch.uint8, device=f"cuda:{device}") for _ in range(2)]
+    cams = [cam] * F  # a frame sequence of the metric's view
     gathered = image = None
     if dist_on and rank == 0:
         gathered = [list(torch.empty((world, F, R, W, 3), dtype=torch.uint8, device=f"cuda:{device}").unbind(0))
@@ -122,6 +127,13 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     def render(shard):
         r.render_async(cam, W, H, D, rows, shard.data_ptr())
 
+    def render_batch(view):  # view: [n, R, W, 3], frame j at view[j]
+        n = view.shape[0]
+        if n == 1:
+            render(view[0])
+        else:
+            r.render_frames_async(cams[:n], W, H, D, rows, view.data_ptr(), R * W * 3)
+
     def unpermute(g, j):
         # g: per-rank views of one [world, F, R, W, 3] buffer; frame j of rank r
         # starts (r * F + j) * R rows in, i.e. rank-major with F * R rows per rank
@@ -129,13 +141,18 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
 
     def frames(n):
         if dist_on:
-            rt_frames.run_frames(dist, n, rank, render, shards, gathered, unpermute if rank == 0 else None, F)
+            rt_frames.run_frames(dist, n, rank, render, shards, gathered, unpermute if rank == 0 else None, F,
+                                 render_batch)
         else:
-            for i in range(n):
-                render(shards[i & 1][0])
+            done, b = 0, 0
+            while done < n:
+                m = min(F, n - done)
+                render_batch(shards[b & 1][:m])
+                done, b = done + m, b + 1
 
     frames(warmup)
-    st = r.stats()  # syncs; ray counts of this rank's shard (identical every step)
+    render(shards[0][0])  # one single-frame launch (untimed): the ray counts of ONE frame of this rank's shard
+    st = r.stats()  # syncs
     r.kernel_times()  # drop warmup launches from the history
     if dist_on:
         dist.barrier()
@@ -146,19 +163,20 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ktimes = r.kernel_times(max(steps, 1))
+    ktimes = r.kernel_times(max(steps, 1))  # one entry per launch (F frames each, the last maybe fewer)
     kmean = sum(ktimes) / len(ktimes)
+    kframe = sum(ktimes) / max(steps, 1)  # kernel time per frame
     my_rays = st.rays
     tests_exact, tests_cull = st.tests_exact, st.tests_cull
     if dist_on:
-        t = torch.tensor([elapsed, kmean], dtype=torch.float64, device=f"cuda:{device}")
+        t = torch.tensor([elapsed, kframe], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kmax = t.tolist()
         n = torch.tensor([my_rays], dtype=torch.int64, device=f"cuda:{device}")
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
         frame_rays = int(n.item())
     else:
-        kmax = kmean
+        kmax = kframe
         frame_rays = my_rays
     assembled_ok = None
     if dist_on and rank == 0 and steps > 0:
@@ -171,7 +189,8 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     r.close()
     return {"assembled_ok": assembled_ok, "scene": scene_name, "scene_file": scene_file, "W": W, "H": H, "D": D, "spheres": scene.num_spheres,
             "lights": scene.num_lights, "frame_rays": frame_rays, "rank_rays": my_rays, "elapsed": elapsed,
-            "kernel_ms_mean": kmean, "kernel_ms_max_rank": kmax, "kernel_ms_min": min(ktimes),
+            "kernel_ms_mean": kmean, "kernel_ms_per_frame": kframe, "kernel_ms_per_frame_max_rank": kmax,
+            "kernel_ms_min": min(ktimes), "frames_per_launch": F,
             "launches_timed": len(ktimes), "rows_per_rank": R, "tests_exact": tests_exact,
             "tests_cull": tests_cull, "cull": cull}
 
@@ -184,8 +203,9 @@ def main():
     ap.add_argument("--workload", default="synth200_1920x1080_d4", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-also", action="store_true", help="skip the complex.txt north-star line item")
-    ap.add_argument("--frames-per-gather", type=int, default=4,
-                    help="N > 1: frames rendered per RCCL gather to rank 0 (one collective per batch)")
+    ap.add_argument("--frames-per-launch", "--frames-per-gather", dest="frames_per_launch", type=int, default=16,
+                    help="frames rendered by one kernel launch (rt_render_frames_async, 1..16); for N > 1 also "
+                         "the frames per RCCL gather to rank 0 (one collective per batch)")
     ap.add_argument("--force-dist", action="store_true",
                     help="rehearsal: run the N > 1 data path (RCCL process group, shard gather, unpermute) at N = 1")
     ap.add_argument("--brute-force", action="store_true",
@@ -205,7 +225,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world)
 
     cull = not args.brute_force
-    batch = max(1, args.frames_per_gather)
+    batch = max(1, min(16, args.frames_per_launch))  # RT_MAX_FRAMES
     m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local, cull, batch, dist_on)
     also = {}
     if not args.no_also and args.workload != "complex_1920x1080_d4":
@@ -214,13 +234,13 @@ def main():
         also["complex_1920x1080_d4"] = {
             "mrays_per_s": round(a["frame_rays"] * max(args.steps // 2, 5) / a["elapsed"] / 1e6, 2),
             "ms_per_frame": round(a["elapsed"] / max(args.steps // 2, 5) * 1e3, 4),
-            "kernel_ms_mean": round(a["kernel_ms_mean"], 4), "rays_per_frame": a["frame_rays"],
+            "kernel_ms_per_frame": round(a["kernel_ms_per_frame"], 4), "rays_per_frame": a["frame_rays"],
             "target_mrays_per_s": 1000}
 
     if rank == 0:
         value = m["frame_rays"] * args.steps / m["elapsed"] / 1e6
-        k_s = m["kernel_ms_mean"] * 1e-3
-        # executed work of one launch (device counters), not the brute-force count
+        k_s = m["kernel_ms_per_frame"] * 1e-3  # launch time / frames per launch
+        # executed work of one frame (device counters), not the brute-force count
         flops = FLOP_PER_TEST * m["tests_exact"] + FLOP_PER_CULL * m["tests_cull"]
         achieved = flops / k_s / 1e12
         brute = FLOP_PER_TEST * m["spheres"] * m["rank_rays"] / k_s / 1e12
@@ -249,20 +269,23 @@ def main():
                        "depth": m["D"], "spheres": m["spheres"], "lights": m["lights"],
                        "rays_per_frame": m["frame_rays"],
                        **({"assembled_frame_equals_single_gpu_render": m["assembled_ok"]} if dist_on else {}),
-                       "parallelism": f"rows cyclic {BAND}-row bands x {world} GPU" +
+                       "frames_per_launch": batch,
+                       "parallelism": f"rows cyclic {BAND}-row bands x {world} GPU, {batch} frames per launch" +
                                       (f" + RCCL gather to rank 0 every {batch} frames" if dist_on else "")},
             # achieved = SURVEY 8(d)'s algorithmic FLOPs (25 per ray-sphere pair, every
             # ray against every sphere) over the measured kernel time.  The kernel
             # prunes pairs exactly (cull bounds, BVH, shadow grids), so this
             # brute-force-equivalent rate can exceed the VALU peak; the executed
-            # work and the PMC-measured VALU use are listed beside it.
+            # work and the PMC-measured VALU use are listed beside it.  One
+            # launch renders `batch` frames; rates are per launch = per frame.
             "roofline": {"bound": "valu", "achieved": round(brute, 3), "peak": FP64_VALU_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(brute / FP64_VALU_PEAK_TFLOPS, 4),
                          "traffic": traffic,
                          "kernel": "rtk::render_kernel (fp64 VALU; no dense contraction, so no MFMA roof)",
                          "per_unit": f"{FLOP_PER_TEST} FLOP per ray-sphere pair x {m['spheres']} spheres x "
-                                     f"{m['rank_rays']} rays per launch (SURVEY 8(d))",
-                         "algorithmic_flops_per_launch": FLOP_PER_TEST * m["spheres"] * m["rank_rays"],
+                                     f"{m['rank_rays']} rays per frame x {batch} frames per launch (SURVEY 8(d))",
+                         "algorithmic_flops_per_launch": FLOP_PER_TEST * m["spheres"] * m["rank_rays"] * batch,
+                         "algorithmic_flops_per_frame": FLOP_PER_TEST * m["spheres"] * m["rank_rays"],
                          "executed": {"exact_tests": m["tests_exact"], "cull_tests": m["tests_cull"],
                                       "test_tflops": round(achieved, 3),
                                       "frac_of_brute_force_tests": round(
@@ -274,10 +297,12 @@ def main():
                          "culling": m["cull"],
                          "kernel_ms_mean": round(m["kernel_ms_mean"], 4),
                          "kernel_ms_min": round(m["kernel_ms_min"], 4),
+                         "kernel_ms_per_frame": round(m["kernel_ms_per_frame"], 4),
+                         "frames_per_launch": batch,
                          "launches_timed": m["launches_timed"]},
             "hbm_write": {"achieved": round(out_bytes / k_s / 1e9, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                           "frac": round(out_bytes / k_s / 1e9 / HBM_PEAK_GBPS, 6),
-                          "bytes_per_launch": out_bytes},
+                          "bytes_per_frame": out_bytes, "bytes_per_launch": out_bytes * batch},
             "also": also,
         }
         if world == 1 and not args.no_cpu_baseline:

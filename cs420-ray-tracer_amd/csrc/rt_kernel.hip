@@ -50,10 +50,12 @@ constexpr int kMaxLdsStack = 4;  // levels of the LDS reflection stack (render_k
 // rows of `rows`, rt_render); RT_FB_RGB8 with full = 1: a W x H RGB8 image in
 // PPM row order; RT_FB_F32X3 / RT_FB_F64X3: the reference's framebuffer,
 // index j*W + x with j = 0 the bottom row (src/main.cpp:156, kernel.cu:112),
-// unquantised.  Pixels x0 <= x < x0 + xw are written.
+// unquantised.  Pixels x0 <= x < x0 + xw are written.  Frame f of a
+// multi-frame launch (RT_FB_RGB8, full = 0) starts fstride bytes after frame f-1.
 struct OutDesc {
   void *ptr;
   int fmt, full, x0, xw;
+  long long fstride;
 };
 
 // kStackSplit: level 0 here, the reflection levels through the ray queues of
@@ -76,7 +78,8 @@ struct RenderArgs {
   const LightD *lights;
   int n, nl;
   D3 amb;
-  Cam cam;
+  Cam cam[RT_MAX_FRAMES];  // frame f's camera (rt_render_frames_async); cam[0] otherwise
+  int frames;              // frames of this launch: launch slot b renders frame b % frames of tile slot b / frames
   int W, H, depth;
   Rows rows;
   BvhArgs bv;
@@ -97,6 +100,17 @@ struct RenderArgs {
 // v_writelane in the level and light loops.  The empty asm makes the kernarg
 // pointer opaque, so the scalar loads happen at this point and their
 // registers are free again afterwards.  kLate = false returns x itself.
+template <bool kLate, size_t kOff, class T>
+__device__ __forceinline__ const T &kernarg_late(const T &x);
+
+// Frame f's camera, read from the kernarg segment (a dynamic index into the
+// by-value kernel argument would copy the array to scratch).
+__device__ __forceinline__ const Cam &kernarg_cam(int f) {
+  typedef const __attribute__((address_space(4))) unsigned char KB;
+  KB *p = (KB *)__builtin_amdgcn_kernarg_segment_ptr();
+  return *(const Cam *)(p + offsetof(RenderArgs, cam) + (size_t)f * sizeof(Cam));
+}
+
 template <bool kLate, size_t kOff, class T>
 __device__ __forceinline__ const T &kernarg_late(const T &x) {
   if constexpr (!kLate) {
@@ -365,7 +379,8 @@ __device__ __forceinline__ D3 trace_compact(const SphGeo *__restrict__ g, const 
 struct CompactArgs {
   D3 *park;  // kStackGlobal with kernarg-resident arguments: this wave's parked colours (LDS)
   StackEnt *gstack;  // [depth-1][npx]
-  size_t npx;
+  size_t npx;        // level stride: pixels of all frames of the launch
+  unsigned fpx;      // this wave's frame's first stack entry (frame * pixels per frame)
   QRay *q;           // LDS
   int *qcnt;         // LDS
   TermRec *term;     // LDS
@@ -383,7 +398,7 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
                                            const Rows &rows_arg, const BvhArgs &bv, const LgArgs &lg,
                                            const OutDesc &od_arg, int x0, int k0, StackEnt *stk,
                                            const CompactArgs &ca, const SplitArgs &sa, Work &work,
-                                           unsigned long long (&sums)[4]) {
+                                           unsigned long long (&sums)[4], int frame = 0) {
   const int W = W_arg, H = H_arg;
   const Rows &rows = rows_arg;
   const OutDesc &od = od_arg;
@@ -438,8 +453,8 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
                                ca.q, ca.qcnt, ca.term, work, c_prim, c_shadow, c_reflect);
     else if (kStack == kStackGlobal)
       c = trace_wave<kCull, kArgMem, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, ca.gstack,
-                                              (unsigned)pix, (unsigned)ca.npx, work, c_prim, c_shadow, c_reflect,
-                                              ca.park);
+                                              (unsigned)pix + ca.fpx, (unsigned)ca.npx, work, c_prim, c_shadow,
+                                              c_reflect, ca.park);
     else
       c = trace_wave<kCull, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk, (unsigned)lane, 64u, work,
                             c_prim, c_shadow, c_reflect);
@@ -478,7 +493,8 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
     const int c = lane & 7, rb = lane & ~7;
     const unsigned long long rowmask = 0xFFull << rb;
     const bool whole = (__ballot(put) & rowmask) == rowmask;
-    uint8_t *row = static_cast<uint8_t *>(od.ptr) + ((size_t)(od.full ? y : k) * W + (x - c)) * 3;
+    uint8_t *row = static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride +
+                   ((size_t)(od.full ? y : k) * W + (x - c)) * 3;
     const bool packed = whole && ((reinterpret_cast<uintptr_t>(row) & 3u) == 0);
     const int p0 = (4 * c) / 3;  // dword c holds bytes 4c..4c+3: pixels p0, p0+1
     const unsigned v0 = __shfl(v, rb + (p0 < 7 ? p0 : 7), 64), v1 = __shfl(v, rb + (p0 + 1 < 7 ? p0 + 1 : 7), 64);
@@ -596,11 +612,15 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   const int b = blockIdx.x;
   if (b == 0 && a.zero_next)
     for (int i = (int)threadIdx.x; i < kShards * kShardStride; i += (int)blockDim.x) a.zero_next[i] = 0ull;
-  int tile = b;
+  // the frames of a multi-frame launch share the tile order: slots b of one
+  // tile slot are adjacent, so every frame's copy of a heavy tile starts early
+  const int nf = a.frames;
+  const int slot = nf > 1 ? b / nf : b, frame = nf > 1 ? b - slot * nf : 0;
+  int tile = slot;
   if (a.perm) {
-    if (b >= a.ntiles) return;
-    tile = a.perm[b];  // heaviest predicted tiles first
-  } else if (a.xcd_per > 0) {
+    if (slot >= a.ntiles) return;
+    tile = a.perm[slot];  // heaviest predicted tiles first
+  } else if (a.xcd_per > 0) {  // single-frame launches only (launch_tiles)
     const int m = b >> 3;  // this workgroup's rank on its XCD
     tile = ((m / a.xcd_per) * 8 + (b & 7)) * a.xcd_per + m % a.xcd_per;
   }
@@ -632,7 +652,8 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
     ca.park = reinterpret_cast<D3 *>(smem + stack_off + (a.bv.ordered ? (size_t)kWg * a.bv.odepth * 64 * sizeof(int2) : 0)) +
               (size_t)wave * 64;
   ca.gstack = a.gstack;
-  ca.npx = (size_t)a.rows.count * a.od.xw;
+  ca.npx = (size_t)a.rows.count * a.od.xw * nf;
+  ca.fpx = (unsigned)((size_t)a.rows.count * a.od.xw * frame);
   ca.q = reinterpret_cast<QRay *>(smem + stack_off);
   ca.term = reinterpret_cast<TermRec *>(smem + stack_off + (size_t)kWaves * 64 * sizeof(QRay));
   ca.qcnt = reinterpret_cast<int *>(smem + stack_off + (size_t)kWaves * 64 * (sizeof(QRay) + sizeof(TermRec)));
@@ -642,9 +663,11 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
 #ifdef RT_STAMPS
   const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  trace_tile<kCull, kSamples, kStack, !kLdsGeo>(g, rad, sm, slight, a.n, a.nl, a.amb, a.cam, a.W, a.H, a.depth, a.rows,
-                                                bv, a.lg, a.od, a.od.x0 + tx * (8 * kWx) + (wave % kWx) * 8,
-                                                ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, a.sa, work, sums);
+  trace_tile<kCull, kSamples, kStack, !kLdsGeo>(g, rad, sm, slight, a.n, a.nl, a.amb, kernarg_cam(frame), a.W, a.H,
+                                                a.depth, a.rows, bv, a.lg, a.od,
+                                                a.od.x0 + tx * (8 * kWx) + (wave % kWx) * 8,
+                                                ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, a.sa, work, sums,
+                                                frame);
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
   record_timeline(tile * kWg + wave, t_real0, work);
@@ -859,6 +882,9 @@ struct rt_ctx {
   // RT_HIP_STACK: 0 LDS reflection stack (persistent kernel above depth 5),
   // 1 global per-pixel stack, 2 global stack + workgroup-compacted levels
   int stack_mode = 1;
+  // frames of the launch being enqueued (rt_render_frames_async; 1 otherwise) and their cameras
+  int nframes = 1;
+  const rt_camera *fcams = nullptr;
   int xcd_map = 0;  // RT_HIP_XCD_MAP: visits per XCD (runs of ntiles/(8*visits) tiles); 0 = launch order
   unsigned char *cstack_buf = nullptr;
   size_t cstack_bytes = 0;
@@ -968,6 +994,12 @@ LgArgs lg_args(const rt_ctx *c) {
   return g;
 }
 
+Cam to_cam(const rt_camera &cm) {
+  return Cam{cm.position[0], cm.position[1], cm.position[2], cm.forward[0], cm.forward[1], cm.forward[2],
+             cm.right[0],    cm.right[1],    cm.right[2],    cm.up[0],      cm.up[1],      cm.up[2],
+             cm.scale};
+}
+
 // The tile launch order for this view (rt_sched.h), on the device; rebuilt
 // only when the camera, the image/shard geometry, the tile size or the scene
 // changed since the last build.
@@ -1016,11 +1048,14 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     bv.ostk_off = (int)((lds_layout(kLds, c->nsph, c->nlight, bv.nnodes).end + 31) & ~(size_t)31);
   const int ntx = (od.xw + 8 * kWx - 1) / (8 * kWx), nty = (rows.count + 8 * kWy - 1) / (8 * kWy);
   const long long ntiles = (long long)ntx * nty;
-  if (ntiles > (1LL << 30)) return RT_ERR_INVALID_ARG;
+  // frames of this launch (rt_render_frames_async): the global reflection stack only
+  const int nf = c->nframes;
+  if (nf < 1 || nf > RT_MAX_FRAMES || (nf > 1 && kStack != kStackGlobal)) return RT_ERR_INVALID_ARG;
+  if (ntiles * nf > (1LL << 30)) return RT_ERR_INVALID_ARG;
   // runs of tiles per XCD visit (see render_kernel); grid rounded up to whole rounds
-  const int xcd_per = c->xcd_map > 0 ? (int)std::max(1LL, ntiles / (8LL * c->xcd_map)) : 0;
+  const int xcd_per = (c->xcd_map > 0 && nf == 1) ? (int)std::max(1LL, ntiles / (8LL * c->xcd_map)) : 0;
   const long long rounds = xcd_per ? (ntiles + 8LL * xcd_per - 1) / (8LL * xcd_per) : 0;
-  const dim3 grid(xcd_per ? (unsigned)(rounds * 8 * xcd_per) : (unsigned)ntiles);
+  const dim3 grid(xcd_per ? (unsigned)(rounds * 8 * xcd_per) : (unsigned)(ntiles * nf));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   lds = ((lds + 31) & ~(size_t)31) +
         (kStack == kStackCompact ? kLdsCompactBytes : kStack == kStackLds ? kLdsStackBytes : 0);
@@ -1031,8 +1066,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   StackEnt *gstack = split_stack;
   if (kStack != kStackLds && kStack != kStackSplit && depth > 1) {
     // the kernel indexes the stack with 32 bits: entry + level * npx < 2^32
-    if ((unsigned long long)(depth - 1) * rows.count * od.xw >= (1ull << 32)) return RT_ERR_INVALID_ARG;
-    const size_t need = (size_t)(depth - 1) * rows.count * od.xw * sizeof(StackEnt);
+    if ((unsigned long long)(depth - 1) * rows.count * od.xw * nf >= (1ull << 32)) return RT_ERR_INVALID_ARG;
+    const size_t need = (size_t)(depth - 1) * rows.count * od.xw * nf * sizeof(StackEnt);
     if (c->cstack_bytes < need) {
       RT_TRY(c, hipStreamSynchronize(c->stream));
       if (c->cstack_buf) (void)hipFree(c->cstack_buf);
@@ -1056,7 +1091,9 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.n = c->nsph;
   ra.nl = c->nlight;
   ra.amb = amb;
-  ra.cam = cam;
+  ra.cam[0] = cam;
+  for (int f = 1; f < nf; f++) ra.cam[f] = to_cam(c->fcams[f]);
+  ra.frames = nf;
   ra.W = W;
   ra.H = H;
   ra.depth = depth;
@@ -1289,6 +1326,7 @@ int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_
 }
 
 int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows &r, const OutDesc &od) {
+  if (c->nframes > 1 && (c->pipeline != 0 || c->stack_mode != kStackGlobal)) return RT_ERR_INVALID_ARG;
   RT_TRY(c, hipSetDevice(c->device));
   const int half = (int)(c->launches & 1);
   c->d_counters = c->d_ctr_base + (size_t)half * kShards * kShardStride;
@@ -1299,9 +1337,7 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
   const int slot = (int)(c->launches % rt_ctx::kRing);
   RT_TRY(c, hipEventRecord(c->ev0[slot], c->stream));
   if (r.count > 0) {
-    Cam cam{cm->position[0], cm->position[1], cm->position[2], cm->forward[0], cm->forward[1], cm->forward[2],
-            cm->right[0],    cm->right[1],    cm->right[2],    cm->up[0],      cm->up[1],      cm->up[2],
-            cm->scale};
+    const Cam cam = to_cam(*cm);
     // the scene and its BVH are staged in LDS when they fit (lds_layout)
     const int nn = (c->bvh_on && c->cull) ? c->bvh_nodes : 0;
     const bool lds_geo = c->lds_scene && lds_layout(true, c->nsph, c->nlight, nn).end <= kLdsBudget;
@@ -1595,6 +1631,22 @@ int rt_render_async(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, co
   int rc = validate(c, cam, W, H, depth, rows, out, r);
   if (rc != RT_OK) return rc;
   return enqueue(c, cam, W, H, depth, r, OutDesc{out, RT_FB_RGB8, 0, 0, W});
+}
+
+int rt_render_frames_async(rt_ctx *c, const rt_camera *cams, int nframes, int W, int H, int depth,
+                           const rt_rows *rows, uint8_t *out, size_t frame_stride) {
+  Rows r;
+  int rc = validate(c, cams, W, H, depth, rows, out, r);
+  if (rc != RT_OK) return rc;
+  if (nframes < 1 || nframes > RT_MAX_FRAMES) return RT_ERR_INVALID_ARG;
+  if (nframes > 1 && (frame_stride < (size_t)r.count * W * 3 || frame_stride > (size_t)1 << 62))
+    return RT_ERR_INVALID_ARG;
+  c->nframes = nframes;
+  c->fcams = cams;
+  rc = enqueue(c, cams, W, H, depth, r, OutDesc{out, RT_FB_RGB8, 0, 0, W, (long long)frame_stride});
+  c->nframes = 1;
+  c->fcams = nullptr;
+  return rc;
 }
 
 int rt_render_stats(rt_ctx *c, rt_stats *st) {

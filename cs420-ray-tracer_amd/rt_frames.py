@@ -12,6 +12,10 @@ waits for that gather (Work.wait() orders streams, it does not block the host
 under NCCL) and rank 0 reassembles the batch's frames then.  So on every rank
 the rendering of batch i overlaps the gather of batch i-1, and every frame's
 image is complete once the loop has drained.
+
+With `render_batch` the frames of a batch are rendered by ONE call (one
+rt_render_frames_async launch), so a rank's slowest tiles of one frame overlap
+the other frames' tiles instead of ending every launch.
 """
 from __future__ import annotations
 
@@ -20,12 +24,14 @@ from typing import Callable, Sequence
 
 def run_frames(dist, steps: int, rank: int, render: Callable[[object], None], shards: Sequence,
                gathered: Sequence | None, unpermute: Callable[[Sequence, int], None] | None,
-               batch: int = 1) -> None:
+               batch: int = 1, render_batch: Callable[[object], None] | None = None) -> None:
     """render(view) enqueues one frame into `view` (a [R, W, 3] slice of a
     shard buffer); shards[k] is buffer k ([batch, R, W, 3]); on rank 0,
     gathered[k] is the list of per-rank receive tensors ([batch, R, W, 3]) for
     buffer k and unpermute(gathered[k], j) enqueues the reassembly of frame j
-    of that buffer.  `steps` frames are rendered in batches of `batch`."""
+    of that buffer.  `steps` frames are rendered in batches of `batch`;
+    render_batch(view), if given, enqueues all frames of a [n, R, W, 3] view
+    at once instead of n render() calls."""
     works = [None, None]
     counts = [0, 0]
 
@@ -42,8 +48,11 @@ def run_frames(dist, steps: int, rank: int, render: Callable[[object], None], sh
         if works[k] is not None:
             retire(k)  # batch b-2: its shard buffer is free, rank 0 reassembles it
         n = min(batch, steps - done)
-        for j in range(n):
-            render(shards[k][j])
+        if render_batch is not None:
+            render_batch(shards[k][:n])
+        else:
+            for j in range(n):
+                render(shards[k][j])
         recv = [g[:n] for g in gathered[k]] if rank == 0 else None
         works[k] = dist.gather(shards[k][:n], recv, dst=0, async_op=True)
         counts[k] = n

@@ -22,7 +22,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(HERE, "librt_hip.so")
 
 RT_MAX_DEPTH = 64
-ABI_VERSION = 2  # RT_HIP_ABI_VERSION in include/rt_hip.h
+ABI_VERSION = 3  # RT_HIP_ABI_VERSION in include/rt_hip.h
+MAX_FRAMES = 16  # RT_MAX_FRAMES
 
 
 class RtError(RuntimeError):
@@ -93,6 +94,8 @@ SIGNATURES = {
                             C.c_int, C.POINTER(rt_stats)]),
     "rt_render_async": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.POINTER(rt_rows), _P]),
     "rt_render_stats": (C.c_int, [_P, C.POINTER(rt_stats)]),
+    "rt_render_frames_async": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.POINTER(rt_rows), _P, C.c_size_t]),
     "rt_kernel_times": (C.c_int, [_P, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int)]),
     "rt_unpermute_rows": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     "rt_render_tile": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -253,6 +256,16 @@ class Renderer:
         _check(lib().rt_render_async(self._ctx, C.byref(cam), width, height, depth,
                                      C.byref(rows) if rows is not None else None, C.c_void_p(out_device_ptr)),
                "rt_render_async", self._ctx)
+
+    def render_frames_async(self, cams, width: int, height: int, depth: int, rows: rt_rows | None,
+                            out_device_ptr: int, frame_stride: int):
+        """rt_render_frames_async: len(cams) frames (<= MAX_FRAMES) in one launch, frame f
+        (seen through cams[f]) at out_device_ptr + f * frame_stride."""
+        arr = (rt_camera * len(cams))(*cams)
+        _check(lib().rt_render_frames_async(self._ctx, arr, len(cams), width, height, depth,
+                                            C.byref(rows) if rows is not None else None,
+                                            C.c_void_p(out_device_ptr), frame_stride),
+               "rt_render_frames_async", self._ctx)
 
     def set_antialias(self, samples: int):
         """1 = the serial path, 4 = the reference GPU's `-a` mode (main_gpu.cu:249-333)."""

@@ -15,6 +15,8 @@
  *   rt_render                       <- the serial pixel loop  src/main.cpp:146-157 (trace_ray :16-58),
  *                                      the OpenMP loop :185-199, and launch_gpu_kernel src/kernel.cu:185-200
  *   rt_render_async                 <- launch_gpu_kernel(..., cudaStream_t) src/kernel.cu:185-200
+ *   rt_render_frames_async          <- (new) the pixel loop over a sequence of frames in one launch
+ *                                      (frame f = rt_render_async with cams[f])
  *   rt_write_ppm                    <- write_ppm()            src/main.cpp:69-91
  *   rt_kernel_times                 <- cudaEventElapsedTime around the kernel, src/main_gpu.cu:496-519
  *   rt_unpermute_rows               <- (new) reassembly of the multi-GPU row shards
@@ -38,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 2
+#define RT_HIP_ABI_VERSION 3
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -160,6 +162,21 @@ int rt_render(rt_ctx *ctx, const rt_camera *cam, int width, int height, int dept
 int rt_render_async(rt_ctx *ctx, const rt_camera *cam, int width, int height, int depth, const rt_rows *rows,
                     uint8_t *rgb_out_device);
 int rt_render_stats(rt_ctx *ctx, rt_stats *stats);
+
+/* Most frames one rt_render_frames_async launch renders. */
+#define RT_MAX_FRAMES 16
+/* Asynchronous render of `nframes` frames (1..RT_MAX_FRAMES) of the uploaded
+ * scene in ONE kernel launch, frame f seen through cams[f]: a frame sequence
+ * of the per-frame pixel loop src/main.cpp:146-157, each frame exactly what
+ * rt_render_async(ctx, &cams[f], ...) writes, into DEVICE memory at
+ * rgb_out_device + f * frame_stride (frame_stride >= rows' count * width * 3
+ * bytes).  The tiles of all frames share one launch, so the long reflection
+ * chains of one frame overlap the others' work instead of each frame ending
+ * on its slowest tiles.  Counts as ONE launch for rt_kernel_times; the stats
+ * of rt_render_stats are the sums over its frames.  Requires the default
+ * render path (no RT_HIP_PIPELINE / RT_HIP_PERSIST / RT_HIP_STACK != 1). */
+int rt_render_frames_async(rt_ctx *ctx, const rt_camera *cams, int nframes, int width, int height, int depth,
+                           const rt_rows *rows, uint8_t *rgb_out_device, size_t frame_stride);
 
 /* Durations (ms, HIP events recorded in-stream around each render kernel) of
  * the render launches issued since the previous call, oldest first, at most

@@ -50,6 +50,9 @@ W, H, D = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080,
 sc = rt_hip.Scene.load(os.path.join(REPO, "cs420-ray-tracer_amd", "scenes", scene + ".txt"))
 r = rt_hip.Renderer(0)
 r.upload(sc)
+# SHARD=r/G renders rank r's cyclic 8-row bands of G (the N = G bench's per-rank launch)
+shard = os.environ.get("SHARD")
+rows = rt_hip.rows_for_shard(H, 8, *(int(x) for x in shard.split("/"))) if shard else None
 for _ in range(4):
-    _, st = r.render(sc.camera(), W, H, D)
+    _, st = r.render(sc.camera(), W, H, D, rows)
 print("kernel ms", st.kernel_ms)

@@ -1,0 +1,172 @@
+"""GPU parity of multi-frame launches (rt_render_frames_async): every frame of a
+launch is byte-identical to the golden image / to the single-frame render of
+its own camera, and the launch's ray counts are the sums over its frames."""
+import numpy as np
+import pytest
+
+from conftest import diff_summary, golden_rgb, manifest, scene_path
+
+pytestmark = pytest.mark.gpu
+
+
+def _load(r, name):
+    import rt_hip
+
+    m = manifest()[name]
+    sc = rt_hip.Scene.load(scene_path(m["scene"]))
+    r.upload(sc)
+    return sc, m
+
+
+def _frames(r, cams, W, H, D, rows=None, pad=0):
+    """Render len(cams) frames in one launch; returns [F, R, W, 3] numpy and stats."""
+    import torch
+
+    R = rows.count if rows is not None else H
+    stride = R * W * 3 + pad
+    buf = torch.full((len(cams) * stride,), 77, dtype=torch.uint8, device="cuda:0")
+    r.render_frames_async(cams, W, H, D, rows, buf.data_ptr(), stride)
+    st = r.stats()
+    host = buf.cpu().numpy()
+    frames = np.stack([host[f * stride:f * stride + R * W * 3].reshape(R, W, 3) for f in range(len(cams))])
+    gaps = [host[f * stride + R * W * 3:(f + 1) * stride] for f in range(len(cams))]
+    return frames, st, gaps
+
+
+def _single(r, cam, W, H, D, rows=None):
+    rgb, st = r.render(cam, W, H, D, rows=rows)
+    return bytes(rgb), st
+
+
+def _moved(cam, k):
+    """The scene camera moved sideways and zoomed a little, k steps (still a valid basis)."""
+    import rt_hip
+
+    c = rt_hip.rt_camera()
+    for f in ("position", "forward", "right", "up"):
+        getattr(c, f)[:] = list(getattr(cam, f))
+    c.position[0] += 0.37 * k
+    c.position[1] -= 0.11 * k
+    c.scale = cam.scale * (1.0 + 0.05 * k)
+    return c
+
+
+@pytest.mark.parametrize("name,F", [("complex_97x61_d4", 2), ("complex_97x61_d4", 16), ("medium_1280x720_d10", 3),
+                                    ("synth200_1920x1080_d4", 8), ("synth10k_384x216_d6", 5)])
+def test_frames_equal_golden(gpu_renderer, name, F):
+    sc, m = _load(gpu_renderer, name)
+    frames, st, gaps = _frames(gpu_renderer, [sc.camera()] * F, m["width"], m["height"], m["depth"], pad=13)
+    want = golden_rgb(name)
+    for f in range(F):
+        assert frames[f].tobytes() == want, f"frame {f}: {diff_summary(frames[f].tobytes(), want)}"
+        assert (gaps[f] == 77).all(), "bytes between frames were written"
+    rays = m["rays"]
+    assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (F * rays["primary"], F * rays["shadow"],
+                                                                   F * rays["reflect"])
+
+
+@pytest.mark.parametrize("name", ["complex_97x61_d4", "synth200_1920x1080_d4"])
+def test_frames_distinct_cameras(gpu_renderer, name):
+    sc, m = _load(gpu_renderer, name)
+    W, H, D = m["width"], m["height"], m["depth"]
+    cams = [_moved(sc.camera(), k) for k in (0, 3, -2, 1, 5, -4)]
+    frames, st, _ = _frames(gpu_renderer, cams, W, H, D)
+    total = [0, 0, 0]
+    for f, cam in enumerate(cams):
+        want, s1 = _single(gpu_renderer, cam, W, H, D)
+        assert frames[f].tobytes() == want, f"frame {f}: {diff_summary(frames[f].tobytes(), want)}"
+        total = [total[0] + s1.rays_primary, total[1] + s1.rays_shadow, total[2] + s1.rays_reflect]
+    assert [st.rays_primary, st.rays_shadow, st.rays_reflect] == total
+    assert frames[0].tobytes() == golden_rgb(name)  # k = 0 is the scene camera
+    assert frames[1].tobytes() != frames[0].tobytes()
+
+
+@pytest.mark.parametrize("G,band,F", [(3, 8, 4), (8, 8, 7), (5, 1, 2)])
+def test_frames_row_shards(gpu_renderer, G, band, F):
+    import rt_hip
+
+    name = "complex_97x61_d4"
+    sc, m = _load(gpu_renderer, name)
+    W, H, D = m["width"], m["height"], m["depth"]
+    cams = [_moved(sc.camera(), k) for k in range(F)]
+    for r in range(G):
+        rows = rt_hip.rows_for_shard(H, band, r, G)
+        frames, _, _ = _frames(gpu_renderer, cams, W, H, D, rows)
+        for f in range(F):
+            want, _ = _single(gpu_renderer, cams[f], W, H, D, rows)
+            assert frames[f].tobytes() == want, (r, f)
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2, 7])
+def test_frames_depth_edges(gpu_renderer, depth):
+    sc, m = _load(gpu_renderer, "complex_97x61_d4")
+    cams = [_moved(sc.camera(), k) for k in (0, 2, 4)]
+    frames, _, _ = _frames(gpu_renderer, cams, m["width"], m["height"], depth)
+    for f, cam in enumerate(cams):
+        want, _ = _single(gpu_renderer, cam, m["width"], m["height"], depth)
+        assert frames[f].tobytes() == want, f
+
+
+def test_frames_antialias(gpu_renderer):
+    sc, m = _load(gpu_renderer, "complex_97x61_d4")
+    cams = [_moved(sc.camera(), k) for k in (0, 1)]
+    gpu_renderer.set_antialias(4)
+    try:
+        frames, _, _ = _frames(gpu_renderer, cams, m["width"], m["height"], m["depth"])
+        for f, cam in enumerate(cams):
+            want, _ = _single(gpu_renderer, cam, m["width"], m["height"], m["depth"])
+            assert frames[f].tobytes() == want, f
+    finally:
+        gpu_renderer.set_antialias(1)
+
+
+@pytest.mark.parametrize("env", [{"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_SCHED": "0"}, {"RT_HIP_XCD_MAP": "2"}],
+                         ids=["lds-scene", "scanline", "xcd-map"])
+def test_frames_knobs(monkeypatch, env):
+    import rt_hip
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    r = rt_hip.Renderer(0)
+    try:
+        sc, m = _load(r, "synth200_1920x1080_d4")
+        frames, _, _ = _frames(r, [sc.camera()] * 3, m["width"], m["height"], m["depth"])
+        for f in range(3):
+            assert frames[f].tobytes() == golden_rgb("synth200_1920x1080_d4"), f
+    finally:
+        r.close()
+
+
+def test_frames_argument_errors(gpu_renderer):
+    import torch
+    import rt_hip
+
+    sc, m = _load(gpu_renderer, "complex_97x61_d4")
+    W, H, D = m["width"], m["height"], m["depth"]
+    buf = torch.empty((17 * H * W * 3,), dtype=torch.uint8, device="cuda:0")
+    cam = sc.camera()
+    for cams, stride in (([], H * W * 3), ([cam] * 17, H * W * 3), ([cam] * 2, H * W * 3 - 1)):
+        with pytest.raises(rt_hip.RtError):
+            gpu_renderer.render_frames_async(cams, W, H, D, None, buf.data_ptr(), stride)
+    # one frame ignores the stride, like rt_render_async
+    gpu_renderer.render_frames_async([cam], W, H, D, None, buf.data_ptr(), 0)
+    gpu_renderer.stats()
+    assert buf[:H * W * 3].cpu().numpy().tobytes() == golden_rgb("complex_97x61_d4")
+
+
+@pytest.mark.parametrize("env", [{"RT_HIP_PIPELINE": "1"}, {"RT_HIP_STACK": "0"}], ids=["queues", "lds-stack"])
+def test_frames_need_default_path(monkeypatch, env):
+    import torch
+    import rt_hip
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    r = rt_hip.Renderer(0)
+    try:
+        sc, m = _load(r, "complex_97x61_d4")
+        W, H, D = m["width"], m["height"], m["depth"]
+        buf = torch.empty((2 * H * W * 3,), dtype=torch.uint8, device="cuda:0")
+        with pytest.raises(rt_hip.RtError):
+            r.render_frames_async([sc.camera()] * 2, W, H, D, None, buf.data_ptr(), H * W * 3)
+    finally:
+        r.close()

@@ -75,7 +75,7 @@ def test_gloo_gather_reassembles_golden(world, name):
     assert rays == sum(manifest()[name]["rays"].values())
 
 
-def _pipelined_worker(rank, world, port, batch, q):
+def _pipelined_worker(rank, world, port, batch, q, batched=False):
     """bench.py's pipelined frame loop (rt_frames.run_frames) under gloo: frame f
     of rank r fills its shard with (f, r, row); every reassembled frame must be
     exact and arrive in order, with `batch` frames per gather (steps not a
@@ -108,19 +108,25 @@ def _pipelined_worker(rank, world, port, batch, q):
                              band)
         seen.append(img[:, 0, 0].tolist())
 
-    rt_frames.run_frames(dist, steps, rank, render, shards, gathered, unpermute if rank == 0 else None, batch)
+    def render_batch(view):  # one call per batch (bench.py's rt_render_frames_async path)
+        for j in range(view.shape[0]):
+            render(view[j])
+
+    rt_frames.run_frames(dist, steps, rank, render, shards, gathered, unpermute if rank == 0 else None, batch,
+                         render_batch if batched else None)
     if rank == 0:
         q.put(seen)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,batch", [(2, 1), (3, 1), (2, 4), (3, 3)])
-def test_gloo_pipelined_frames(world, batch):
+@pytest.mark.parametrize("world,batch,batched", [(2, 1, False), (3, 1, False), (2, 4, False), (3, 3, False),
+                                                 (2, 4, True), (3, 3, True)])
+def test_gloo_pipelined_frames(world, batch, batched):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, batch, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, batch, q, batched)) for r in range(world)]
     for p in procs:
         p.start()
     seen = q.get(timeout=120)
