@@ -198,8 +198,8 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--workload", default="synth200_1920x1080_d4", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-also", action="store_true", help="skip the complex.txt north-star line item")
@@ -249,7 +249,9 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 pmc_rec = json.load(f).get(args.workload, {})
-            traffic = pmc_rec.get("hbm_bytes_per_launch")
+            traffic = pmc_rec.get("hbm_bytes_per_frame")
+            if traffic is not None:
+                traffic *= batch  # per launch, like algorithmic_flops_per_launch
         out_bytes = m["W"] * m["rows_per_rank"] * 3
         line = {
             "metric": METRIC,
@@ -290,10 +292,12 @@ def main():
                                       "test_tflops": round(achieved, 3),
                                       "frac_of_brute_force_tests": round(
                                           m["tests_exact"] / max(1, m["spheres"] * m["rank_rays"]), 6)},
-                         "pmc": {k: pmc_rec[k] for k in ("valu_busy", "fp64_flops_per_launch", "fetch_bytes",
-                                                         "write_bytes", "source") if k in pmc_rec},
-                         "pmc_fp64_tflops": (round(pmc_rec["fp64_flops_per_launch"] / k_s / 1e12, 3)
-                                             if "fp64_flops_per_launch" in pmc_rec else None),
+                         # PMC counters per FRAME (scripts/make_pmc_json.py); bytes: fetch/write per frame
+                         "pmc": {k: pmc_rec[k] for k in ("valu_busy", "fp64_flops_per_frame", "fetch_bytes",
+                                                         "write_bytes", "hbm_bytes_per_frame", "source")
+                                 if k in pmc_rec},
+                         "pmc_fp64_tflops": (round(pmc_rec["fp64_flops_per_frame"] / k_s / 1e12, 3)
+                                             if "fp64_flops_per_frame" in pmc_rec else None),
                          "culling": m["cull"],
                          "kernel_ms_mean": round(m["kernel_ms_mean"], 4),
                          "kernel_ms_min": round(m["kernel_ms_min"], 4),

@@ -10,7 +10,7 @@ cd /tmp
 i=0
 while IFS= read -r counters; do
   [ -z "$counters" ] && continue
-  timeout -k 10 300 rocprofv3 --pmc $counters --output-format csv -d "$OUT/p$i" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-also --workload "$W" --steps 10 --warmup 2 ${BENCH_ARGS} > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $counters --output-format csv -d "$OUT/p$i" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-also --workload "$W" --steps 32 --warmup 16 ${BENCH_ARGS} > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   i=$((i+1))
 done < "${PASSES:-$ROOT/scripts/pmc_passes.txt}"
 echo "pmc passes: $i"

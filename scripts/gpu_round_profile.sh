@@ -15,7 +15,7 @@ timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { t
 cat "$OUT/bench.json"
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-also --steps 50 --warmup 5 > "$OUT/trace_bench.json" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-also --steps 64 --warmup 16 > "$OUT/trace_bench.json" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 1; }
 echo "trace ok"
 for w in synth200_1920x1080_d4 complex_1920x1080_d4 synth10k_3840x2160_d6; do
   PASSES="$ROOT/scripts/pmc_traffic_passes.txt" TAG="round_$TAG/pmc_$w" WORKLOAD=$w bash "$ROOT/scripts/gpu_pmc.sh" || exit 1

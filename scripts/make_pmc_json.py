@@ -3,13 +3,16 @@
 
   python scripts/make_pmc_json.py WORKLOAD PMC_DIR [KERNEL_SUBSTR]
 
-Per render launch (mean over the profiled launches):
-  hbm_bytes_per_launch = (FETCH_SIZE + WRITE_SIZE) * 1024  (rocprofv3 reports KiB;
+Per FRAME: a render dispatch of g threads renders g / g_min frames (g_min =
+the smallest render dispatch of the run, bench.py's single-frame stats launch;
+multi-frame launches are rt_render_frames_async), and every counter is summed
+over the render dispatches and divided by the frames they rendered:
+  hbm_bytes_per_frame = (FETCH_SIZE + WRITE_SIZE) * 1024  (rocprofv3 reports KiB;
       the gfx950 x2 FETCH_SIZE correction of MI355X_MICROARCH.md applies to wide
       16-B/lane streaming reads, which this kernel does not issue, so the raw
       value is used; fetch and write are also listed separately)
   valu_busy = SQ_ACTIVE_INST_VALU * 4 / (SIMDs * GRBM_GUI_ACTIVE / XCDs)
-  fp64_flops_per_launch = 64 * (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions
+  fp64_flops_per_frame = 64 * (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions
       (an upper bound: it assumes every lane of the wave is active)
 """
 import collections
@@ -27,25 +30,30 @@ def main():
     kern = sys.argv[3] if len(sys.argv) > 3 else "render_"
     vals = {}
     for f in sorted(glob.glob(f"{base}/p*/run_counter_collection.csv")):
-        agg = collections.defaultdict(list)
-        for r in csv.DictReader(open(f)):
-            if kern in r["Kernel_Name"]:
-                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        rows = [r for r in csv.DictReader(open(f)) if kern in r["Kernel_Name"]]
+        if not rows:
+            continue
+        gmin = min(int(r["Grid_Size"]) for r in rows)
+        agg = collections.defaultdict(float)
+        frames = collections.defaultdict(float)
+        for r in rows:
+            agg[r["Counter_Name"]] += float(r["Counter_Value"])
+            frames[r["Counter_Name"]] += int(r["Grid_Size"]) / gmin
         for k, v in agg.items():
-            vals[k] = sum(v) / len(v)
+            vals[k] = v / frames[k]
     out = {}
     if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
         out["fetch_bytes"] = round(vals["FETCH_SIZE"] * 1024)
         out["write_bytes"] = round(vals["WRITE_SIZE"] * 1024)
-        out["hbm_bytes_per_launch"] = out["fetch_bytes"] + out["write_bytes"]
+        out["hbm_bytes_per_frame"] = out["fetch_bytes"] + out["write_bytes"]
     if "SQ_ACTIVE_INST_VALU" in vals and "GRBM_GUI_ACTIVE" in vals:
         cycles = vals["GRBM_GUI_ACTIVE"] / XCDS
-        out["kernel_cycles"] = round(cycles)
+        out["kernel_cycles_per_frame"] = round(cycles)
         out["valu_busy"] = round(vals["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cycles), 4)
     f64 = [vals.get("SQ_INSTS_VALU_%s_F64" % k) for k in ("ADD", "MUL", "FMA", "TRANS")]
     if None not in f64:
-        out["fp64_flops_per_launch"] = round(64 * (f64[0] + f64[1] + 2 * f64[2] + f64[3]))
-        out["valu_insts_per_launch"] = round(vals.get("SQ_INSTS_VALU", 0))
+        out["fp64_flops_per_frame"] = round(64 * (f64[0] + f64[1] + 2 * f64[2] + f64[3]))
+        out["valu_insts_per_frame"] = round(vals.get("SQ_INSTS_VALU", 0))
     out["source"] = os.path.relpath(base, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     out["counters"] = {k: round(v, 1) for k, v in sorted(vals.items())}
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
