@@ -139,10 +139,32 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
         # starts (r * F + j) * R rows in, i.e. rank-major with F * R rows per rank
         r.unpermute(g[0].data_ptr() + j * R * W * 3, image.data_ptr(), W, H, BAND, world, F * R)
 
+    class Side:
+        """rank 0's reassembly stream (rt_frames.run_frames(side=...)): the unpermute
+        kernels run there, overlapping the next batch's render on the main stream."""
+
+        def __init__(self):
+            self.main = stream
+            self.s = torch.cuda.Stream(device=f"cuda:{device}")
+            self.ev = [torch.cuda.Event(), torch.cuda.Event()]
+
+        def begin(self, k):
+            self.s.wait_stream(self.main)  # the gather of buffer k (Work.wait ordered it on main)
+            r.set_stream(self.s.cuda_stream)
+
+        def end(self, k):
+            r.set_stream(self.main.cuda_stream)
+            self.ev[k].record(self.s)
+
+        def join(self, k):
+            self.main.wait_event(self.ev[k])
+
+    side = Side() if dist_on and rank == 0 else None
+
     def frames(n):
         if dist_on:
             rt_frames.run_frames(dist, n, rank, render, shards, gathered, unpermute if rank == 0 else None, F,
-                                 render_batch)
+                                 render_batch, side)
         else:
             done, b = 0, 0
             while done < n:
@@ -211,6 +233,11 @@ def main():
     ap.add_argument("--brute-force", action="store_true",
                     help="disable the exact per-wave sphere culling: every ray tests every sphere")
     args = ap.parse_args()
+
+    # The JSON line is the only thing on stdout: RCCL's banner and any other
+    # library output written to fd 1 go to stderr instead.
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     world, rank, local = dist_env()
     import torch  # loads torch's HIP runtime first; librt_hip.so binds to it
@@ -314,7 +341,7 @@ def main():
             # ray_openmp's loop on the host cores this job may use (16 on the GPU box)
             line["cpu_baseline_all_cores"] = cpu_baseline(m["scene_file"], m["W"], m["H"], m["D"],
                                                           m["frame_rays"], threads=min(16, os.cpu_count() or 1))
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()

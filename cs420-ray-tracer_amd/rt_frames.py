@@ -15,7 +15,11 @@ image is complete once the loop has drained.
 
 With `render_batch` the frames of a batch are rendered by ONE call (one
 rt_render_frames_async launch), so a rank's slowest tiles of one frame overlap
-the other frames' tiles instead of ending every launch.
+the other frames' tiles instead of ending every launch.  With `side`, rank 0
+reassembles a batch on a second stream (side.begin(k) ... side.end(k)), so the
+memory-bound unpermute overlaps the VALU-bound render of the next batch
+instead of queueing behind it; side.join(k) orders the next gather into
+receive buffer k after that reassembly.
 """
 from __future__ import annotations
 
@@ -24,7 +28,7 @@ from typing import Callable, Sequence
 
 def run_frames(dist, steps: int, rank: int, render: Callable[[object], None], shards: Sequence,
                gathered: Sequence | None, unpermute: Callable[[Sequence, int], None] | None,
-               batch: int = 1, render_batch: Callable[[object], None] | None = None) -> None:
+               batch: int = 1, render_batch: Callable[[object], None] | None = None, side=None) -> None:
     """render(view) enqueues one frame into `view` (a [R, W, 3] slice of a
     shard buffer); shards[k] is buffer k ([batch, R, W, 3]); on rank 0,
     gathered[k] is the list of per-rank receive tensors ([batch, R, W, 3]) for
@@ -39,8 +43,12 @@ def run_frames(dist, steps: int, rank: int, render: Callable[[object], None], sh
         works[k].wait()
         works[k] = None
         if rank == 0 and unpermute is not None:
+            if side is not None:
+                side.begin(k)
             for j in range(counts[k]):
                 unpermute(gathered[k], j)
+            if side is not None:
+                side.end(k)
 
     done, b = 0, 0
     while done < steps:
@@ -54,6 +62,8 @@ def run_frames(dist, steps: int, rank: int, render: Callable[[object], None], sh
             for j in range(n):
                 render(shards[k][j])
         recv = [g[:n] for g in gathered[k]] if rank == 0 else None
+        if rank == 0 and side is not None:
+            side.join(k)  # buffer k's previous batch has been reassembled
         works[k] = dist.gather(shards[k][:n], recv, dst=0, async_op=True)
         counts[k] = n
         done += n

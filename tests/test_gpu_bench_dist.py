@@ -13,14 +13,16 @@ from conftest import REPO
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("batch", ["1", "4"])
+@pytest.mark.parametrize("batch", ["1", "4", "16"])
 def test_bench_force_dist_reassembles_frame(batch):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29540 + int(batch)))
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--force-dist", "--no-cpu-baseline",
-                          "--no-also", "--steps", "7", "--warmup", "1", "--frames-per-gather", batch,
+                          "--no-also", "--steps", "7", "--warmup", "1", "--frames-per-launch", batch,
                           "--workload", "medium_1920x1080_d2"],
                          capture_output=True, text=True, timeout=150, env=env, cwd=REPO)
     assert out.returncode == 0, out.stderr[-2000:]
-    line = json.loads(out.stdout.strip().splitlines()[-1])
+    lines = out.stdout.strip().splitlines()
+    assert len(lines) == 1, out.stdout[-2000:]  # RCCL's banner goes to stderr
+    line = json.loads(lines[0])
     assert line["config"]["assembled_frame_equals_single_gpu_render"] is True
     assert line["n_gpus"] == 1 and line["value"] > 0

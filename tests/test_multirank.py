@@ -75,6 +75,29 @@ def test_gloo_gather_reassembles_golden(world, name):
     assert rays == sum(manifest()[name]["rays"].values())
 
 
+class _Side:
+    """Records rt_frames' side-stream protocol: begin/end around each batch's
+    reassembly, join(k) before buffer k is gathered into again."""
+
+    def __init__(self):
+        self.log = []
+        self.open = None
+
+    def begin(self, k):
+        assert self.open is None
+        self.open = k
+        self.log.append(("begin", k))
+
+    def end(self, k):
+        assert self.open == k
+        self.open = None
+        self.log.append(("end", k))
+
+    def join(self, k):
+        assert self.open is None
+        self.log.append(("join", k))
+
+
 def _pipelined_worker(rank, world, port, batch, q, batched=False):
     """bench.py's pipelined frame loop (rt_frames.run_frames) under gloo: frame f
     of rank r fills its shard with (f, r, row); every reassembled frame must be
@@ -112,8 +135,14 @@ def _pipelined_worker(rank, world, port, batch, q, batched=False):
         for j in range(view.shape[0]):
             render(view[j])
 
+    side = _Side() if (batched and rank == 0) else None
     rt_frames.run_frames(dist, steps, rank, render, shards, gathered, unpermute if rank == 0 else None, batch,
-                         render_batch if batched else None)
+                         render_batch if batched else None, side)
+    if side is not None:
+        # every reassembly is bracketed, and buffer k is joined before each gather into it
+        nb = -(-steps // batch)
+        assert [e for e in side.log if e[0] == "begin"] == [("begin", b & 1) for b in range(nb)]
+        assert [e for e in side.log if e[0] == "join"] == [("join", b & 1) for b in range(nb)]
     if rank == 0:
         q.put(seen)
     dist.barrier()
