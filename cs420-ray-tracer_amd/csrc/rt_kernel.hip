@@ -530,6 +530,172 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
   sums[3] += wave_sum(c_neg);
 }
 
+// kStackMerge: one wave traces kMergeTiles tiles and merges their reflection
+// rays before tracing them.  Level 0 runs tile by tile (one lane per pixel,
+// coherent); a pixel whose chain ends there is stored at once.  The rays it
+// spawns (typically a handful per tile: 0.34 M reflection rays for 2.07 M
+// pixels on synth200) wait in a per-wave LDS queue (< 64 entries) until a
+// tile's spawns and the queue fill a wave: then those 64 rays run their
+// remaining levels together (chain), each lane unwinding its own pixel's
+// [level][pixel] stack and storing it.  So the incoherent levels cost one
+// wave pass per 64 rays instead of one per tile that has any: measured per
+// reflection level, level 2 of synth200 (41 K rays) cost 0.047 ms and level 3
+// (8 K rays) 0.021 ms with one tile per wave.  No barriers: the wave is its
+// own workgroup.  RGB8 row-compact output, one sample per pixel.
+#ifndef RT_MERGE_TILES
+#define RT_MERGE_TILES 4
+#endif
+constexpr int kMergeTiles = RT_MERGE_TILES;
+constexpr int kStackMerge = 4;
+
+// Stores a pixel's final colour (quantised as write_ppm, main.cpp:85) at out + 3 pix.
+__device__ __forceinline__ void store_px(uint8_t *out, unsigned pix, D3 c, bool img, unsigned &c_neg) {
+  int q0 = 0, q1 = 0, q2 = 0;  // padding rows of a shard: zeros
+  if (img) {
+    q0 = quantize(c.x), q1 = quantize(c.y), q2 = quantize(c.z);
+    c_neg += (q0 < 0) + (q1 < 0) + (q2 < 0);
+  }
+  uint8_t *px = out + (size_t)pix * 3;
+  px[0] = (uint8_t)(q0 < 0 ? 0 : q0);
+  px[1] = (uint8_t)(q1 < 0 ? 0 : q1);
+  px[2] = (uint8_t)(q2 < 0 ? 0 : q2);
+}
+
+// kMergeTiles tiles of one frame for one wave (see kStackMerge).  Every lane
+// holds at most one ray: (o, d, key = the sphere it leaves, dleft = depth
+// left, pix, lev = stack entries its pixel has).  One bounce() per iteration
+// for all lanes holding a ray:
+//   * a tile pass loads the next tile's camera rays into all lanes (level 0);
+//     the reflection rays it spawns join the queue unless they and the queue
+//     fill the wave (or no tile is left), then the queued rays fill the lanes
+//     that spawned none;
+//   * a chain pass bounces the lanes' rays (any level >= 1) and refills the
+//     lanes whose chain ended from the queue.
+// A chain that ends unwinds its pixel's stack (sbase[sidx + level * sstride],
+// innermost first, main.cpp:54) and stores the pixel.
+template <bool kCull>
+__device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                            const SphMat *__restrict__ mat, const LightD *__restrict__ slight,
+                                            const RenderArgs &a, int group, int frame, const CompactArgs &ca,
+                                            QRay *q, Work &work, unsigned long long (&sums)[4]) {
+  const int lane = (int)(threadIdx.x & 63);
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  unsigned c_prim = 0, c_shadow = 0, c_reflect = 0, c_neg = 0;
+  const int depth = a.depth;
+  const unsigned sstride = (unsigned)ca.npx;
+  int qn = 0;        // queued rays q[0 .. qn), wave-uniform, < 64 between passes
+  int next = 0;      // next tile of the group
+  bool act = false;  // this lane holds a ray
+  D3 o = mk(0.0, 0.0, 0.0), d = o;
+  int key = -1, dleft = 0, lev = 0;
+  unsigned pix = 0;
+  // pops queued rays into the lanes without one (lanes ranked by lane id)
+  auto refill = [&](unsigned long long busy) {
+    const int take = (64 - __popcll(busy)) < qn ? (64 - __popcll(busy)) : qn;
+    const int r = (int)__popcll(~busy & lt);
+    if (!act && r < take) {
+      const QRay &e = q[qn - 1 - r];
+      o = mk(e.ox, e.oy, e.oz);
+      d = mk(e.dx, e.dy, e.dz);
+      key = e.key;
+      dleft = e.dleft;
+      pix = (unsigned)e.pix;
+      lev = 1;
+      act = true;
+    }
+    qn -= take;
+  };
+  while (true) {
+    const int ntiles = kernarg_late<true, offsetof(RenderArgs, ntiles)>(a.ntiles);
+    const int nt = ntiles - group * kMergeTiles < kMergeTiles ? ntiles - group * kMergeTiles : kMergeTiles;
+    bool tile_pass = false;
+    if (__ballot(act) == 0) {
+      if (next < nt) {  // camera rays of the next tile: camera.h:17-25, main.cpp:151-154 (as trace_tile)
+        const int *perm = kernarg_late<true, offsetof(RenderArgs, perm)>(a.perm);
+        const int slot = group * kMergeTiles + next;
+        const int tile = perm ? perm[slot] : slot;
+        const int ntx = kernarg_late<true, offsetof(RenderArgs, ntx)>(a.ntx);
+        const int tx = tile % ntx, ty = tile / ntx;
+        const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
+        const Rows &rows = kernarg_late<true, offsetof(RenderArgs, rows)>(a.rows);
+        const int W = kernarg_late<true, offsetof(RenderArgs, W)>(a.W);
+        const int H = kernarg_late<true, offsetof(RenderArgs, H)>(a.H);
+        const int x = tx * 8 + (lane & 7);
+        const int k = ty * 8 + (lane >> 3);
+        const bool in_tile = x < W && k < rows.count;
+        const long long y = (long long)(k / rows.band) * rows.band * rows.stride +
+                            (long long)rows.first * rows.band + (k % rows.band);
+        const bool in_img = in_tile && y < H;
+        const int j = H - 1 - (int)(in_img ? y : 0);  // reference row (main.cpp:74)
+        const Cam &cam = kernarg_cam(frame);
+        const double u = (double)x / (W - 1), v = (double)j / (H - 1);
+        const double su = ((u - 0.5) * cam.scale) * 1.0, sv = (v - 0.5) * cam.scale;
+        const D3 dir = add(add(mk(cam.fx, cam.fy, cam.fz), scale(mk(cam.rx, cam.ry, cam.rz), su)),
+                           scale(mk(cam.ux, cam.uy, cam.uz), sv));
+        d = normalized(normalized(dir));
+        o = mk(cam.px, cam.py, cam.pz);
+        pix = (unsigned)(k * W + x);
+        key = -1;
+        dleft = depth;
+        lev = 0;
+        act = in_img && depth >= 1;
+        c_prim += act ? 1u : 0u;
+        if (in_tile && !act)  // depth <= 0 -> black (main.cpp:17-18); padding rows -> zeros
+          store_px(static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride, pix, mk(0.0, 0.0, 0.0),
+                   in_img, c_neg);
+        ++next;
+        tile_pass = true;
+        if (__ballot(act) == 0) continue;
+      } else if (qn > 0) {
+        refill(0ull);
+      } else {
+        break;
+      }
+    }
+    int outcome = 0, nkey = 0;
+    D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
+    double refl = 0.0;
+    bounce<kCull, true>(g, rad, mat, slight, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft, work, c_shadow,
+                        outcome, color, refl, no, nd, nkey);
+    const unsigned sidx = pix + ca.fpx;
+    if (act) {
+      if (outcome == kSpawned) {
+        ca.gstack[sidx + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
+        ++lev;
+        o = no;
+        d = nd;
+        key = nkey;
+        --dleft;
+        ++c_reflect;
+      } else {  // the chain ends: unwind its pixel's stack and store it
+        D3 res = color;
+        while (lev > 0) {
+          --lev;
+          const StackEnt e = ca.gstack[sidx + (unsigned)lev * sstride];
+          res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
+        }
+        const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
+        store_px(static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride, pix, res, true, c_neg);
+        act = false;
+      }
+    }
+    const unsigned long long busy = __ballot(act);
+    if (tile_pass && next < nt && __popcll(busy) + qn < 64) {
+      // this tile's reflection rays wait for the next tiles' (queue < 64 entries)
+      if (act)
+        q[qn + (int)__popcll(busy & lt)] = QRay{o.x, o.y, o.z, d.x, d.y, d.z, 0, dleft, key, (int)pix};
+      qn += __popcll(busy);
+      act = false;
+    } else if (qn > 0 && busy != ~0ull) {
+      refill(busy);  // lanes without a ray take queued ones
+    }
+  }
+  sums[0] += wave_sum(c_prim);
+  sums[1] += wave_sum(c_shadow);
+  sums[2] += wave_sum(c_reflect);
+  sums[3] += wave_sum(c_neg);
+}
+
 // Flushes a wave's ray counts and work counters into its counter shard.
 __device__ __forceinline__ void flush_counts(unsigned long long *counters, const unsigned long long (&sums)[4],
                                              const Work &work) {
@@ -594,7 +760,7 @@ constexpr int kWaves = 4;  // 2x2 tiles of 8x8 pixels per workgroup (persistent 
 // no wave's slot waits for its slowest neighbour.
 template <bool kLdsGeo, int kStack>
 constexpr int wg_waves() {
-  return (kLdsGeo || (kStack != 1 && kStack != 3)) ? 4 : 1;
+  return (kLdsGeo || (kStack != 1 && kStack != 3 && kStack != 4)) ? 4 : 1;
 }
 // LDS after the staged scene: the 4-level reflection stack per wave, or
 // (kCompact) the workgroup's ray queue, terminal colours and queue count.
@@ -617,14 +783,18 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   const int nf = a.frames;
   const int slot = nf > 1 ? b / nf : b, frame = nf > 1 ? b - slot * nf : 0;
   int tile = slot;
-  if (a.perm) {
-    if (slot >= a.ntiles) return;
-    tile = a.perm[slot];  // heaviest predicted tiles first
-  } else if (a.xcd_per > 0) {  // single-frame launches only (launch_tiles)
-    const int m = b >> 3;  // this workgroup's rank on its XCD
-    tile = ((m / a.xcd_per) * 8 + (b & 7)) * a.xcd_per + m % a.xcd_per;
+  if constexpr (kStack == kStackMerge) {
+    if (slot * kMergeTiles >= a.ntiles) return;  // slot = this wave's group of kMergeTiles tile slots
+  } else {
+    if (a.perm) {
+      if (slot >= a.ntiles) return;
+      tile = a.perm[slot];  // heaviest predicted tiles first
+    } else if (a.xcd_per > 0) {  // single-frame launches only (launch_tiles)
+      const int m = b >> 3;  // this workgroup's rank on its XCD
+      tile = ((m / a.xcd_per) * 8 + (b & 7)) * a.xcd_per + m % a.xcd_per;
+    }
+    if (tile >= a.ntiles) return;  // workgroup-uniform, before any barrier
   }
-  if (tile >= a.ntiles) return;  // workgroup-uniform, before any barrier
   const int tx = tile % a.ntx, ty = tile / a.ntx;
   extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
   const SphGeo *g;
@@ -648,7 +818,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   StackEnt *stk = reinterpret_cast<StackEnt *>(smem + stack_off) + (size_t)wave * kMaxLdsStack * 64;
   CompactArgs ca;
   ca.park = nullptr;
-  if (!kLdsGeo && kStack == kStackGlobal)  // after the ordered walk's stacks (launch_tiles sizes both)
+  if (!kLdsGeo && (kStack == kStackGlobal || kStack == kStackMerge))  // after the ordered walk's stacks (launch_tiles sizes both)
     ca.park = reinterpret_cast<D3 *>(smem + stack_off + (a.bv.ordered ? (size_t)kWg * a.bv.odepth * 64 * sizeof(int2) : 0)) +
               (size_t)wave * 64;
   ca.gstack = a.gstack;
@@ -663,11 +833,17 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
 #ifdef RT_STAMPS
   const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  trace_tile<kCull, kSamples, kStack, !kLdsGeo>(g, rad, sm, slight, a.n, a.nl, a.amb, kernarg_cam(frame), a.W, a.H,
-                                                a.depth, a.rows, bv, a.lg, a.od,
-                                                a.od.x0 + tx * (8 * kWx) + (wave % kWx) * 8,
-                                                ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, a.sa, work, sums,
-                                                frame);
+  if constexpr (kStack == kStackMerge && !kLdsGeo && kSamples == 1) {
+    // the wave's ray queue sits where trace_wave parks colours (launch_tiles)
+    QRay *q = reinterpret_cast<QRay *>(ca.park);
+    merge_tiles<kCull>(g, rad, sm, slight, a, slot, frame, ca, q, work, sums);
+  } else {
+    trace_tile<kCull, kSamples, kStack, !kLdsGeo>(g, rad, sm, slight, a.n, a.nl, a.amb, kernarg_cam(frame), a.W, a.H,
+                                                  a.depth, a.rows, bv, a.lg, a.od,
+                                                  a.od.x0 + tx * (8 * kWx) + (wave % kWx) * 8,
+                                                  ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, a.sa, work,
+                                                  sums, frame);
+  }
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
   record_timeline(tile * kWg + wave, t_real0, work);
@@ -881,7 +1057,7 @@ struct rt_ctx {
   int samples = 1;  // 4: the antialias mode (rt_set_antialias)
   // RT_HIP_STACK: 0 LDS reflection stack (persistent kernel above depth 5),
   // 1 global per-pixel stack, 2 global stack + workgroup-compacted levels
-  int stack_mode = 1;
+  int stack_mode = 4;  // RT_HIP_STACK: 4 merged reflection levels (default), 1 per-pixel global stack, 0 LDS, 2 compacted
   // frames of the launch being enqueued (rt_render_frames_async; 1 otherwise) and their cameras
   int nframes = 1;
   const rt_camera *fcams = nullptr;
@@ -1043,26 +1219,31 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
   constexpr int kWg = wg_waves<kLds, kStack>(), kWx = kWg == 4 ? 2 : 1, kWy = kWg / kWx;
-  // the ordered walk's stacks follow the scene in LDS (render_kernel, kStackGlobal / kStackSplit)
-  if ((kStack == kStackGlobal || kStack == kStackSplit) && bv.ordered)
+  // the ordered walk's stacks follow the scene in LDS (render_kernel, kStackGlobal / kStackSplit / kStackMerge)
+  if ((kStack == kStackGlobal || kStack == kStackSplit || kStack == kStackMerge) && bv.ordered)
     bv.ostk_off = (int)((lds_layout(kLds, c->nsph, c->nlight, bv.nnodes).end + 31) & ~(size_t)31);
   const int ntx = (od.xw + 8 * kWx - 1) / (8 * kWx), nty = (rows.count + 8 * kWy - 1) / (8 * kWy);
   const long long ntiles = (long long)ntx * nty;
   // frames of this launch (rt_render_frames_async): the global reflection stack only
   const int nf = c->nframes;
-  if (nf < 1 || nf > RT_MAX_FRAMES || (nf > 1 && kStack != kStackGlobal)) return RT_ERR_INVALID_ARG;
+  if (nf < 1 || nf > RT_MAX_FRAMES || (nf > 1 && kStack != kStackGlobal && kStack != kStackMerge))
+    return RT_ERR_INVALID_ARG;
+  // kStackMerge: one wave per kMergeTiles consecutive tile slots
+  const long long nslots = kStack == kStackMerge ? (ntiles + kMergeTiles - 1) / kMergeTiles : ntiles;
   if (ntiles * nf > (1LL << 30)) return RT_ERR_INVALID_ARG;
   // runs of tiles per XCD visit (see render_kernel); grid rounded up to whole rounds
-  const int xcd_per = (c->xcd_map > 0 && nf == 1) ? (int)std::max(1LL, ntiles / (8LL * c->xcd_map)) : 0;
+  const int xcd_per = (c->xcd_map > 0 && nf == 1 && kStack != kStackMerge)
+                        ? (int)std::max(1LL, ntiles / (8LL * c->xcd_map)) : 0;
   const long long rounds = xcd_per ? (ntiles + 8LL * xcd_per - 1) / (8LL * xcd_per) : 0;
-  const dim3 grid(xcd_per ? (unsigned)(rounds * 8 * xcd_per) : (unsigned)(ntiles * nf));
+  const dim3 grid(xcd_per ? (unsigned)(rounds * 8 * xcd_per) : (unsigned)(nslots * nf));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   lds = ((lds + 31) & ~(size_t)31) +
         (kStack == kStackCompact ? kLdsCompactBytes : kStack == kStackLds ? kLdsStackBytes : 0);
   // the kernel places the ordered walk's stacks from these same arguments
-  if ((kStack == kStackGlobal || kStack == kStackSplit) && bv.ordered)
+  if ((kStack == kStackGlobal || kStack == kStackSplit || kStack == kStackMerge) && bv.ordered)
     lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
   if (!kLds && kStack == kStackGlobal) lds += (size_t)kWg * 64 * sizeof(D3);  // parked colours (trace_wave)
+  if (kStack == kStackMerge) lds += (size_t)64 * sizeof(QRay);                 // the wave's ray queue (merge_tiles)
   StackEnt *gstack = split_stack;
   if (kStack != kStackLds && kStack != kStackSplit && depth > 1) {
     // the kernel indexes the stack with 32 bits: entry + level * npx < 2^32
@@ -1158,6 +1339,14 @@ int launch_render4(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dept
                    const OutDesc &od) {
   if (c->stack_mode == kStackCompact)
     return launch_tiles<kLds, kCull, kSamples, kStackCompact>(c, lds, cam, W, H, depth, rows, od);
+  if (c->stack_mode == kStackMerge) {
+    // merged reflection levels: RGB8 row-compact output, one sample, scene through L2;
+    // other outputs take the per-pixel global stack
+    if constexpr (!kLds && kSamples == 1)
+      if (od.fmt == RT_FB_RGB8 && !od.full && od.x0 == 0 && od.xw == W)
+        return launch_tiles<kLds, kCull, 1, kStackMerge>(c, lds, cam, W, H, depth, rows, od);
+    return launch_tiles<kLds, kCull, kSamples, kStackGlobal>(c, lds, cam, W, H, depth, rows, od);
+  }
   if (c->stack_mode == kStackGlobal)
     return launch_tiles<kLds, kCull, kSamples, kStackGlobal>(c, lds, cam, W, H, depth, rows, od);
   if (c->persist || depth - 1 > kMaxLdsStack) return launch_persist3<kLds, kCull, kSamples>(c, lds, cam, W, H, depth,
@@ -1326,7 +1515,8 @@ int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_
 }
 
 int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows &r, const OutDesc &od) {
-  if (c->nframes > 1 && (c->pipeline != 0 || c->stack_mode != kStackGlobal)) return RT_ERR_INVALID_ARG;
+  if (c->nframes > 1 && (c->pipeline != 0 || (c->stack_mode != kStackGlobal && c->stack_mode != kStackMerge)))
+    return RT_ERR_INVALID_ARG;
   RT_TRY(c, hipSetDevice(c->device));
   const int half = (int)(c->launches & 1);
   c->d_counters = c->d_ctr_base + (size_t)half * kShards * kShardStride;
@@ -1394,7 +1584,10 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_PERSIST")) c->persist = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_LDS_SCENE")) c->lds_scene = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_SCHED")) c->sched = std::atoi(e) != 0;
-  if (const char *e = std::getenv("RT_HIP_STACK")) c->stack_mode = std::max(0, std::min(2, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_STACK")) {
+    const int m = std::max(0, std::min(4, std::atoi(e)));
+    c->stack_mode = m == kStackSplit ? kStackGlobal : m;  // 3 is the split pipeline's own mode
+  }
   if (const char *e = std::getenv("RT_HIP_XCD_MAP")) c->xcd_map = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_BVH_ORDERED")) c->bvh_ordered = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH4")) c->bvh_wide = std::atoi(e) != 0;

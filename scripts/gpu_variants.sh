@@ -13,11 +13,11 @@ i=0
 while IFS= read -r v; do
   [ -z "$v" ] && continue
   for rep in 1 2; do
-    env $v timeout -k 10 300 python bench.py --no-cpu-baseline --steps 40 ${BENCH_ARGS} > gpurun_out/${TAG}_$i.json 2> gpurun_out/${TAG}_$i.err; rc=$?
+    env $v timeout -k 10 300 python bench.py --no-cpu-baseline --steps 64 ${BENCH_ARGS} > gpurun_out/${TAG}_$i.json 2> gpurun_out/${TAG}_$i.err; rc=$?
     [ $rc -eq 0 ] || { echo "variant [$v] rc=$rc"; tail -5 gpurun_out/${TAG}_$i.err; exit $rc; }
     python -c "
 import json; d=json.load(open('gpurun_out/${TAG}_$i.json')); a=d['also'].get('complex_1920x1080_d4',{})
-print('%-60s synth200 %8.1f Mrays/s  k=%.4f ms  complex %8.1f  k=%.4f' % ('$v', d['value'], d['roofline']['kernel_ms_mean'], a.get('mrays_per_s',0), a.get('kernel_ms_mean',0)))"
+print('%-60s synth200 %8.1f Mrays/s  k=%.4f ms/frame  complex %8.1f  k=%.4f' % ('$v', d['value'], d['roofline']['kernel_ms_per_frame'], a.get('mrays_per_s',0), a.get('kernel_ms_per_frame',0)))"
   done
   i=$((i+1))
 done < "${VARIANTS:-scripts/variants.txt}"

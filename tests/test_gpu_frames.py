@@ -120,8 +120,9 @@ def test_frames_antialias(gpu_renderer):
         gpu_renderer.set_antialias(1)
 
 
-@pytest.mark.parametrize("env", [{"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_SCHED": "0"}, {"RT_HIP_XCD_MAP": "2"}],
-                         ids=["lds-scene", "scanline", "xcd-map"])
+@pytest.mark.parametrize("env", [{"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_SCHED": "0"}, {"RT_HIP_XCD_MAP": "2"},
+                                 {"RT_HIP_STACK": "1"}, {"RT_HIP_STACK": "4"}],
+                         ids=["lds-scene", "scanline", "xcd-map", "global-stack", "merge"])
 def test_frames_knobs(monkeypatch, env):
     import rt_hip
 

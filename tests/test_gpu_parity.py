@@ -402,9 +402,11 @@ def test_pipelines_random_scenes(pipeline_renderer, seed):
 
 @pytest.fixture(params=[{"RT_HIP_STACK": "0"}, {"RT_HIP_STACK": "2"}, {"RT_HIP_XCD_MAP": "0"},
                         {"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_LDS_SCENE": "1", "RT_HIP_STACK": "0"},
-                        {"RT_HIP_PERSIST": "1", "RT_HIP_STACK": "0"}, {"RT_HIP_SCHED": "0"}],
+                        {"RT_HIP_PERSIST": "1", "RT_HIP_STACK": "0"}, {"RT_HIP_SCHED": "0"},
+                        {"RT_HIP_STACK": "1"}, {"RT_HIP_STACK": "4"}, {"RT_HIP_STACK": "4", "RT_HIP_SCHED": "0"},
+                        {"RT_HIP_STACK": "4", "RT_HIP_LDS_SCENE": "1"}],
                 ids=["lds-stack", "compact", "no-xcd-map", "lds-scene", "lds-scene-lds-stack", "persist",
-                     "scanline-order"])
+                     "scanline-order", "global-stack", "merge", "merge-scanline", "merge-lds-scene"])
 def stack_renderer(request, monkeypatch):
     """Non-default kernel layouts (RT_HIP_STACK=0: LDS reflection stack, the
     persistent kernel above depth 5; 2: workgroup-compacted reflection levels;
