@@ -68,6 +68,7 @@ struct SplitArgs {
   uint8_t *nlev;      // [npx]
 };
 
+struct QRay;
 // All arguments of render_kernel in one struct: its only kernel parameter, so
 // it sits at offset 0 of the kernarg segment and a member can be re-read from
 // there by offsetof (kernarg_late).
@@ -91,6 +92,8 @@ struct RenderArgs {
   SplitArgs sa;
   const int *perm;
   unsigned long long *zero_next;  // counters of the next launch, zeroed by workgroup 0 (or nullptr)
+  QRay *dq;                       // kStackMerge: deferred deep rays, [kShards][dq_cap] (render_deferred)
+  int dq_cap;                     // entries per shard segment; 0 = no deferral
 };
 
 // Member `x` (at offset kOff of RenderArgs) re-read from the kernarg segment
@@ -547,6 +550,17 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
 #endif
 constexpr int kMergeTiles = RT_MERGE_TILES;
 constexpr int kStackMerge = 4;
+// Rays of reflection level >= kDeferLevel leave the merged megakernel for
+// render_deferred, a second kernel over all deferred rays of the launch; the
+// per-shard count lives in u64 slot kDeferSlot of the launch's counter shards.
+#ifndef RT_DEFER_LEVEL
+#define RT_DEFER_LEVEL 2
+#endif
+constexpr int kDeferLevel = RT_DEFER_LEVEL;
+#ifndef RT_DEFER_CAP_DIV
+#define RT_DEFER_CAP_DIV 8  // deferred-queue room: 1 / RT_DEFER_CAP_DIV of the launch's pixels
+#endif
+constexpr int kDeferSlot = 7;
 
 // Stores a pixel's final colour (quantised as write_ppm, main.cpp:85) at out + 3 pix.
 __device__ __forceinline__ void store_px(uint8_t *out, unsigned pix, D3 c, bool img, unsigned &c_neg) {
@@ -658,6 +672,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     bounce<kCull, true>(g, rad, mat, slight, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft, work, c_shadow,
                         outcome, color, refl, no, nd, nkey);
     const unsigned sidx = pix + ca.fpx;
+    bool defer = false;
     if (act) {
       if (outcome == kSpawned) {
         ca.gstack[sidx + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
@@ -667,6 +682,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         key = nkey;
         --dleft;
         ++c_reflect;
+        defer = lev >= kDeferLevel;
       } else {  // the chain ends: unwind its pixel's stack and store it
         D3 res = color;
         while (lev > 0) {
@@ -677,6 +693,27 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
         store_px(static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride, pix, res, true, c_neg);
         act = false;
+      }
+    }
+    // rays of level >= kDeferLevel go to the launch's deferred queue (render_deferred),
+    // as far as its shard segment has room; the others continue here
+    const unsigned long long dm = __ballot(defer);
+    if (dm) {
+      const int cap = kernarg_late<true, offsetof(RenderArgs, dq_cap)>(a.dq_cap);
+      if (cap > 0) {
+        unsigned long long base = 0;
+        const int first = __builtin_ctzll(dm);
+        if (lane == first) base = atomicAdd(&counter_shard(kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters))[kDeferSlot],
+                                            (unsigned long long)__popcll(dm));
+        base = __shfl(base, first, 64);
+        const unsigned long long slot = base + (unsigned long long)__popcll(dm & lt);
+        if (defer && slot < (unsigned long long)cap) {
+          QRay *dq = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq);
+          const unsigned wg = blockIdx.x;
+          dq[(size_t)(wg % kShards) * (size_t)cap + slot] =
+              QRay{o.x, o.y, o.z, d.x, d.y, d.z, lev, dleft, key, (int)sidx};
+          act = false;
+        }
       }
     }
     const unsigned long long busy = __ballot(act);
@@ -849,6 +886,76 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   record_timeline(tile * kWg + wave, t_real0, work);
 #endif
   flush_counts(kernarg_late<!kLdsGeo, offsetof(RenderArgs, counters)>(a.counters), sums, work);
+}
+
+// The deferred rays of a kStackMerge launch (level >= kDeferLevel, typically
+// 2-3 % of its rays but the least coherent): one wave per workgroup,
+// workgroup b serves shard segment b % kShards and takes its chunks of 64
+// rays b / kShards, + gridDim / kShards, ...  Each lane runs its ray's chain
+// to the end exactly as merge_tiles would have (bounce, stack entries at its
+// pixel's [level][pixel] slots), unwinds the pixel's whole stack -- the
+// levels merge_tiles wrote first -- and stores the pixel.
+template <bool kCull>
+__global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const RenderArgs a) {
+  const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards, step = gridDim.x / kShards;
+  const int cap = a.dq_cap;
+  const unsigned long long cnt = a.counters[(size_t)shard * kShardStride + kDeferSlot];
+  const unsigned n_dq = (unsigned)(cnt < (unsigned long long)cap ? cnt : (unsigned long long)cap);
+  if (first * 64u >= n_dq) return;
+  const int lane = (int)(threadIdx.x & 63);
+  const unsigned npx_frame = (unsigned)((size_t)a.rows.count * a.od.xw);
+  const unsigned sstride = npx_frame * (unsigned)a.frames;
+  Work work;
+  unsigned c_shadow = 0, c_reflect = 0, c_neg = 0;
+  for (unsigned c = first; c * 64u < n_dq; c += step) {
+    const unsigned i = c * 64u + (unsigned)lane;
+    bool act = i < n_dq;
+    D3 o = mk(0.0, 0.0, 0.0), d = o;
+    int key = -1, dleft = 0, lev = 0;
+    unsigned pixg = 0;
+    if (act) {
+      const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[(size_t)shard * (size_t)cap + i];
+      o = mk(e.ox, e.oy, e.oz);
+      d = mk(e.dx, e.dy, e.dz);
+      lev = e.orig;
+      dleft = e.dleft;
+      key = e.key;
+      pixg = (unsigned)e.pix;
+    }
+    while (__ballot(act)) {
+      int outcome = 0, nkey = 0;
+      D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
+      double refl = 0.0;
+      bounce<kCull, true>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft,
+                          work, c_shadow, outcome, color, refl, no, nd, nkey);
+      if (act) {
+        StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, gstack)>(a.gstack);
+        if (outcome == kSpawned) {
+          gs[pixg + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
+          ++lev;
+          o = no;
+          d = nd;
+          key = nkey;
+          --dleft;
+          ++c_reflect;
+        } else {
+          D3 res = color;
+          while (lev > 0) {  // main.cpp:54, innermost first
+            --lev;
+            const StackEnt e = gs[pixg + (unsigned)lev * sstride];
+            res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
+          }
+          const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
+          const unsigned f = pixg / npx_frame;
+          store_px(static_cast<uint8_t *>(od.ptr) + (size_t)f * (size_t)od.fstride, pixg - f * npx_frame, res, true,
+                   c_neg);
+          act = false;
+        }
+      }
+    }
+  }
+  unsigned long long sums[4] = {0ull, wave_sum(c_shadow), wave_sum(c_reflect), wave_sum(c_neg)};
+  flush_counts(kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters), sums, work);
 }
 
 // Reflection level `level` of the split pipeline (RT_HIP_PIPELINE=3): one
@@ -1058,6 +1165,9 @@ struct rt_ctx {
   // RT_HIP_STACK: 0 LDS reflection stack (persistent kernel above depth 5),
   // 1 global per-pixel stack, 2 global stack + workgroup-compacted levels
   int stack_mode = 4;  // RT_HIP_STACK: 4 merged reflection levels (default), 1 per-pixel global stack, 0 LDS, 2 compacted
+  bool defer = true;          // RT_HIP_DEFER: kStackMerge defers rays of level >= kDeferLevel to render_deferred
+  QRay *dq_buf = nullptr;     // its queue, grow-only
+  size_t dq_bytes = 0;
   // frames of the launch being enqueued (rt_render_frames_async; 1 otherwise) and their cameras
   int nframes = 1;
   const rt_camera *fcams = nullptr;
@@ -1293,7 +1403,32 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   const int next = (int)((c->launches + 1) & 1);
   ra.zero_next = c->d_ctr_base + (size_t)next * kShards * kShardStride;
   c->zero_pending = true;
+  ra.dq = nullptr;
+  ra.dq_cap = 0;
+  if (kStack == kStackMerge && c->defer && depth > kDeferLevel) {
+    // room for 1/8 of the launch's pixels (deferred rays are ~2 % on synth200); a ray
+    // that finds its shard segment full simply continues in its merge_tiles lane
+    const size_t npx = (size_t)rows.count * od.xw * nf;
+    const size_t cap = std::max<size_t>(64, ((npx / kShards / RT_DEFER_CAP_DIV) + 63) & ~(size_t)63);
+    const size_t need = cap * kShards * sizeof(QRay);
+    if (c->dq_bytes < need) {
+      RT_TRY(c, hipStreamSynchronize(c->stream));
+      if (c->dq_buf) (void)hipFree(c->dq_buf);
+      c->dq_buf = nullptr;
+      c->dq_bytes = 0;
+      RT_TRY(c, hipMalloc(&c->dq_buf, need));
+      c->dq_bytes = need;
+    }
+    if (cap < (size_t)1 << 30) {
+      ra.dq = c->dq_buf;
+      ra.dq_cap = (int)cap;
+    }
+  }
   hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
+  if constexpr (kStack == kStackMerge) {
+    if (ra.dq_cap > 0)  // 48 one-wave workgroups per shard segment
+      hipLaunchKernelGGL((render_deferred<kCull>), dim3(48 * kShards), dim3(64), lds, c->stream, ra);
+  }
   return RT_OK;
 }
 
@@ -1340,11 +1475,16 @@ int launch_render4(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dept
   if (c->stack_mode == kStackCompact)
     return launch_tiles<kLds, kCull, kSamples, kStackCompact>(c, lds, cam, W, H, depth, rows, od);
   if (c->stack_mode == kStackMerge) {
-    // merged reflection levels: RGB8 row-compact output, one sample, scene through L2;
-    // other outputs take the per-pixel global stack
-    if constexpr (!kLds && kSamples == 1)
-      if (od.fmt == RT_FB_RGB8 && !od.full && od.x0 == 0 && od.xw == W)
+    // merged reflection levels: RGB8 row-compact output, one sample, scene through L2,
+    // and only while the wave's LDS (BVH stacks + ray queue) still allows the
+    // 12 waves per CU its registers allow (synth10k's 22-entry stacks do not:
+    // 10 waves, 12 % slower); otherwise the per-pixel global stack
+    if constexpr (!kLds && kSamples == 1) {
+      const BvhArgs bv = bvh_args(c, cam);
+      const size_t wave_lds = (bv.ordered ? (size_t)bv.odepth * 64 * sizeof(int2) : 0) + 64 * sizeof(QRay);
+      if (od.fmt == RT_FB_RGB8 && !od.full && od.x0 == 0 && od.xw == W && 12 * (wave_lds + 32) <= 160 * 1024)
         return launch_tiles<kLds, kCull, 1, kStackMerge>(c, lds, cam, W, H, depth, rows, od);
+    }
     return launch_tiles<kLds, kCull, kSamples, kStackGlobal>(c, lds, cam, W, H, depth, rows, od);
   }
   if (c->stack_mode == kStackGlobal)
@@ -1592,6 +1732,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH_ORDERED")) c->bvh_ordered = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH4")) c->bvh_wide = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(256, std::atoi(e)));
   auto bail = [&](int rc) {
     rt_destroy(c);
@@ -1631,6 +1772,7 @@ void rt_destroy(rt_ctx *c) {
   if (c->wf_buf) (void)hipFree(c->wf_buf);
   if (c->stack_buf) (void)hipFree(c->stack_buf);
   if (c->cstack_buf) (void)hipFree(c->cstack_buf);
+  if (c->dq_buf) (void)hipFree(c->dq_buf);
   if (c->d_perm) (void)hipFree(c->d_perm);
   if (c->h_perm) (void)hipHostFree(c->h_perm);
   for (int i = 0; i < rt_ctx::kRing; i++) {
