@@ -6,7 +6,9 @@
 Per FRAME: a render dispatch of g threads renders g / g_min frames (g_min =
 the smallest render dispatch of the run, bench.py's single-frame stats launch;
 multi-frame launches are rt_render_frames_async), and every counter is summed
-over the render dispatches and divided by the frames they rendered:
+over the render dispatches -- each with the render_deferred dispatch that
+follows it (the launch's deep reflection rays) -- and divided by the frames
+they rendered:
   hbm_bytes_per_frame = (FETCH_SIZE + WRITE_SIZE) * 1024  (rocprofv3 reports KiB;
       the gfx950 x2 FETCH_SIZE correction of MI355X_MICROARCH.md applies to wide
       16-B/lane streaming reads, which this kernel does not issue, so the raw
@@ -31,14 +33,19 @@ def main():
     vals = {}
     for f in sorted(glob.glob(f"{base}/p*/run_counter_collection.csv")):
         rows = [r for r in csv.DictReader(open(f)) if kern in r["Kernel_Name"]]
-        if not rows:
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        main = [r for r in rows if "render_deferred" not in r["Kernel_Name"]]
+        if not main:
             continue
-        gmin = min(int(r["Grid_Size"]) for r in rows)
+        gmin = min(int(r["Grid_Size"]) for r in main)
         agg = collections.defaultdict(float)
         frames = collections.defaultdict(float)
         for r in rows:
+            # render_deferred (the deep rays of the render launch just before it) adds its
+            # counters to that launch; frames are counted on the render launches only
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
-            frames[r["Counter_Name"]] += int(r["Grid_Size"]) / gmin
+            if "render_deferred" not in r["Kernel_Name"]:
+                frames[r["Counter_Name"]] += int(r["Grid_Size"]) / gmin
         for k, v in agg.items():
             vals[k] = v / frames[k]
     out = {}
