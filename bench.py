@@ -208,13 +208,26 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
         r.render_async(cam, W, H, D, rt_hip.rt_rows(1, 0, 1, H), full.data_ptr())
         torch.cuda.synchronize()
         assembled_ok = bool(torch.equal(full, image))
+    gather_ms = None
+    if dist_on and steps > 0:
+        # untimed: one batch's RCCL gather to rank 0 alone ("plus the
+        # gather time"), mean of 5, in-stream events around the collective
+        dist.barrier()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            dist.gather(shards[0], gathered[0] if rank == 0 else None, dst=0)
+        e1.record()
+        torch.cuda.synchronize()
+        gather_ms = e0.elapsed_time(e1) / 5
     r.close()
     return {"assembled_ok": assembled_ok, "scene": scene_name, "scene_file": scene_file, "W": W, "H": H, "D": D, "spheres": scene.num_spheres,
             "lights": scene.num_lights, "frame_rays": frame_rays, "rank_rays": my_rays, "elapsed": elapsed,
             "kernel_ms_mean": kmean, "kernel_ms_per_frame": kframe, "kernel_ms_per_frame_max_rank": kmax,
             "kernel_ms_min": min(ktimes), "frames_per_launch": F,
             "launches_timed": len(ktimes), "rows_per_rank": R, "tests_exact": tests_exact,
-            "tests_cull": tests_cull, "cull": cull}
+            "tests_cull": tests_cull, "cull": cull, "gather_ms_per_batch": gather_ms}
 
 
 def main():
@@ -299,6 +312,15 @@ def main():
                        "rays_per_frame": m["frame_rays"],
                        **({"assembled_frame_equals_single_gpu_render": m["assembled_ok"]} if dist_on else {}),
                        "frames_per_launch": batch,
+                       # the slowest rank's kernel time per frame and, for N > 1,
+                       # one batch's gather to rank 0 measured alone (overlapped with rendering
+                       # in the timed loop)
+                       "kernel_ms_per_frame_max_rank": round(m["kernel_ms_per_frame_max_rank"], 4),
+                       "kernel_only_mrays_per_s": round(m["frame_rays"] / m["kernel_ms_per_frame_max_rank"] / 1e3,
+                                                        1),
+                       **({"gather_ms_per_batch": round(m["gather_ms_per_batch"], 4),
+                           "gather_ms_per_frame": round(m["gather_ms_per_batch"] / batch, 4)}
+                          if m.get("gather_ms_per_batch") is not None else {}),
                        "parallelism": f"rows cyclic {BAND}-row bands x {world} GPU, {batch} frames per launch" +
                                       (f" + RCCL gather to rank 0 every {batch} frames" if dist_on else "")},
             # achieved = SURVEY 8(d)'s algorithmic FLOPs (25 per ray-sphere pair, every

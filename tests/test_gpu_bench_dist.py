@@ -26,3 +26,4 @@ def test_bench_force_dist_reassembles_frame(batch):
     line = json.loads(lines[0])
     assert line["config"]["assembled_frame_equals_single_gpu_render"] is True
     assert line["n_gpus"] == 1 and line["value"] > 0
+    assert line["config"]["gather_ms_per_batch"] > 0 and line["config"]["kernel_ms_per_frame_max_rank"] > 0
