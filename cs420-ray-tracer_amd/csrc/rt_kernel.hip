@@ -907,22 +907,36 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
   const unsigned sstride = npx_frame * (unsigned)a.frames;
   Work work;
   unsigned c_shadow = 0, c_reflect = 0, c_neg = 0;
-  for (unsigned c = first; c * 64u < n_dq; c += step) {
-    const unsigned i = c * 64u + (unsigned)lane;
-    bool act = i < n_dq;
-    D3 o = mk(0.0, 0.0, 0.0), d = o;
-    int key = -1, dleft = 0, lev = 0;
-    unsigned pixg = 0;
-    if (act) {
-      const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[(size_t)shard * (size_t)cap + i];
-      o = mk(e.ox, e.oy, e.oz);
-      d = mk(e.dx, e.dy, e.dz);
-      lev = e.orig;
-      dleft = e.dleft;
-      key = e.key;
-      pixg = (unsigned)e.pix;
+  // This workgroup's entries, in order: chunk first, first + step, ...; entry
+  // k of that stream is queue index (first + (k / 64) * step) * 64 + k % 64.
+  // A lane whose chain ends takes the stream's next entry, so the wave stays
+  // full until the stream runs out instead of finishing each chunk's longest
+  // chain with its other lanes idle.
+  unsigned kk = 0;  // next stream entry (wave-uniform)
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  bool act = false;
+  D3 o = mk(0.0, 0.0, 0.0), d = o;
+  int key = -1, dleft = 0, lev = 0;
+  unsigned pixg = 0;
+  while (true) {
+    const unsigned long long idle = ~__ballot(act);
+    if (idle) {
+      const unsigned k = kk + (unsigned)__popcll(idle & lt);
+      const unsigned i = (first + (k >> 6) * step) * 64u + (k & 63u);
+      if (!act && i < n_dq) {
+        const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[(size_t)shard * (size_t)cap + i];
+        o = mk(e.ox, e.oy, e.oz);
+        d = mk(e.dx, e.dy, e.dz);
+        lev = e.orig;
+        dleft = e.dleft;
+        key = e.key;
+        pixg = (unsigned)e.pix;
+        act = true;
+      }
+      kk += (unsigned)__popcll(idle);
     }
-    while (__ballot(act)) {
+    if (__ballot(act) == 0) break;
+    {
       int outcome = 0, nkey = 0;
       D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
       double refl = 0.0;
