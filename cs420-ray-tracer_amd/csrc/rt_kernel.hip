@@ -94,6 +94,7 @@ struct RenderArgs {
   unsigned long long *zero_next;  // counters of the next launch, zeroed by workgroup 0 (or nullptr)
   QRay *dq;                       // kStackMerge: deferred deep rays, [kShards][dq_cap] (render_deferred)
   int dq_cap;                     // entries per shard segment; 0 = no deferral
+  int merge_q;                    // kStackMerge: LDS ray-queue entries per wave (16..64)
 };
 
 // Member `x` (at offset kOff of RenderArgs) re-read from the kernarg segment
@@ -597,7 +598,8 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
   unsigned c_prim = 0, c_shadow = 0, c_reflect = 0, c_neg = 0;
   const int depth = a.depth;
   const unsigned sstride = (unsigned)ca.npx;
-  int qn = 0;        // queued rays q[0 .. qn), wave-uniform, < 64 between passes
+  int qn = 0;        // queued rays q[0 .. qn), wave-uniform, < Q between passes
+  const int Q = kernarg_late<true, offsetof(RenderArgs, merge_q)>(a.merge_q);
   int next = 0;      // next tile of the group
   bool act = false;  // this lane holds a ray
   D3 o = mk(0.0, 0.0, 0.0), d = o;
@@ -717,8 +719,8 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
       }
     }
     const unsigned long long busy = __ballot(act);
-    if (tile_pass && next < nt && __popcll(busy) + qn < 64) {
-      // this tile's reflection rays wait for the next tiles' (queue < 64 entries)
+    if (tile_pass && next < nt && __popcll(busy) + qn < Q) {
+      // this tile's reflection rays wait for the next tiles' (queue < Q entries)
       if (act)
         q[qn + (int)__popcll(busy & lt)] = QRay{o.x, o.y, o.z, d.x, d.y, d.z, 0, dleft, key, (int)pix};
       qn += __popcll(busy);
@@ -1180,6 +1182,8 @@ struct rt_ctx {
   // 1 global per-pixel stack, 2 global stack + workgroup-compacted levels
   int stack_mode = 4;  // RT_HIP_STACK: 4 merged reflection levels (default), 1 per-pixel global stack, 0 LDS, 2 compacted
   bool defer = true;          // RT_HIP_DEFER: kStackMerge defers rays of level >= kDeferLevel to render_deferred
+  int merge_q = 64;           // kStackMerge: the launch's LDS queue entries per wave (launch_render4 picks it)
+  int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (16, 32 or 64)
   QRay *dq_buf = nullptr;     // its queue, grow-only
   size_t dq_bytes = 0;
   // frames of the launch being enqueued (rt_render_frames_async; 1 otherwise) and their cameras
@@ -1367,7 +1371,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   if ((kStack == kStackGlobal || kStack == kStackSplit || kStack == kStackMerge) && bv.ordered)
     lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
   if (!kLds && kStack == kStackGlobal) lds += (size_t)kWg * 64 * sizeof(D3);  // parked colours (trace_wave)
-  if (kStack == kStackMerge) lds += (size_t)64 * sizeof(QRay);                 // the wave's ray queue (merge_tiles)
+  if (kStack == kStackMerge) lds += (size_t)c->merge_q * sizeof(QRay);         // the wave's ray queue (merge_tiles)
   StackEnt *gstack = split_stack;
   if (kStack != kStackLds && kStack != kStackSplit && depth > 1) {
     // the kernel indexes the stack with 32 bits: entry + level * npx < 2^32
@@ -1419,6 +1423,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   c->zero_pending = true;
   ra.dq = nullptr;
   ra.dq_cap = 0;
+  ra.merge_q = c->merge_q;
   if (kStack == kStackMerge && c->defer && depth > kDeferLevel) {
     // room for 1/8 of the launch's pixels (deferred rays are ~2 % on synth200); a ray
     // that finds its shard segment full simply continues in its merge_tiles lane
@@ -1495,9 +1500,13 @@ int launch_render4(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dept
     // 10 waves, 12 % slower); otherwise the per-pixel global stack
     if constexpr (!kLds && kSamples == 1) {
       const BvhArgs bv = bvh_args(c, cam);
-      const size_t wave_lds = (bv.ordered ? (size_t)bv.odepth * 64 * sizeof(int2) : 0) + 64 * sizeof(QRay);
-      if (od.fmt == RT_FB_RGB8 && !od.full && od.x0 == 0 && od.xw == W && 12 * (wave_lds + 32) <= 160 * 1024)
-        return launch_tiles<kLds, kCull, 1, kStackMerge>(c, lds, cam, W, H, depth, rows, od);
+      const size_t stacks = bv.ordered ? (size_t)bv.odepth * 64 * sizeof(int2) : 0;
+      if (od.fmt == RT_FB_RGB8 && !od.full && od.x0 == 0 && od.xw == W)
+        for (int q = c->merge_q_max; q >= 16; q /= 2)  // the longest queue that keeps 12 waves per CU
+          if (12 * (stacks + (size_t)q * sizeof(QRay) + ((lds + 31) & ~(size_t)31)) <= 160 * 1024) {
+            c->merge_q = q;
+            return launch_tiles<kLds, kCull, 1, kStackMerge>(c, lds, cam, W, H, depth, rows, od);
+          }
     }
     return launch_tiles<kLds, kCull, kSamples, kStackGlobal>(c, lds, cam, W, H, depth, rows, od);
   }
@@ -1747,6 +1756,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH4")) c->bvh_wide = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(16, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(256, std::atoi(e)));
   auto bail = [&](int rc) {
     rt_destroy(c);
