@@ -95,6 +95,7 @@ struct RenderArgs {
   QRay *dq;                       // kStackMerge: deferred deep rays, [kShards][dq_cap] (render_deferred)
   int dq_cap;                     // entries per shard segment; 0 = no deferral
   int merge_q;                    // kStackMerge: LDS ray-queue entries per wave (16..64)
+  int defer_level;                // kStackMerge: rays of this reflection level and deeper are deferred
 };
 
 // Member `x` (at offset kOff of RenderArgs) re-read from the kernarg segment
@@ -684,7 +685,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         key = nkey;
         --dleft;
         ++c_reflect;
-        defer = lev >= kDeferLevel;
+        defer = lev >= kernarg_late<true, offsetof(RenderArgs, defer_level)>(a.defer_level);
       } else {  // the chain ends: unwind its pixel's stack and store it
         D3 res = color;
         while (lev > 0) {
@@ -1184,6 +1185,7 @@ struct rt_ctx {
   bool defer = true;          // RT_HIP_DEFER: kStackMerge defers rays of level >= kDeferLevel to render_deferred
   int merge_q = 64;           // kStackMerge: the launch's LDS queue entries per wave (launch_render4 picks it)
   int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (16, 32 or 64)
+  int defer_level = kDeferLevel;  // RT_HIP_DEFER_LEVEL (>= 1)
   QRay *dq_buf = nullptr;     // its queue, grow-only
   size_t dq_bytes = 0;
   // frames of the launch being enqueued (rt_render_frames_async; 1 otherwise) and their cameras
@@ -1424,7 +1426,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.dq = nullptr;
   ra.dq_cap = 0;
   ra.merge_q = c->merge_q;
-  if (kStack == kStackMerge && c->defer && depth > kDeferLevel) {
+  ra.defer_level = c->defer_level;
+  if (kStack == kStackMerge && c->defer && depth > c->defer_level) {
     // room for 1/8 of the launch's pixels (deferred rays are ~2 % on synth200); a ray
     // that finds its shard segment full simply continues in its merge_tiles lane
     const size_t npx = (size_t)rows.count * od.xw * nf;
@@ -1756,6 +1759,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH4")) c->bvh_wide = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_DEFER_LEVEL")) c->defer_level = std::max(1, std::min(RT_MAX_DEPTH, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(16, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(256, std::atoi(e)));
   auto bail = [&](int rc) {

@@ -405,10 +405,10 @@ def test_pipelines_random_scenes(pipeline_renderer, seed):
                         {"RT_HIP_PERSIST": "1", "RT_HIP_STACK": "0"}, {"RT_HIP_SCHED": "0"},
                         {"RT_HIP_STACK": "1"}, {"RT_HIP_STACK": "4"}, {"RT_HIP_STACK": "4", "RT_HIP_SCHED": "0"},
                         {"RT_HIP_STACK": "4", "RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_MERGE_Q": "16"},
-                        {"RT_HIP_DEFER": "0"}],
+                        {"RT_HIP_DEFER": "0"}, {"RT_HIP_DEFER_LEVEL": "1"}, {"RT_HIP_DEFER_LEVEL": "3"}],
                 ids=["lds-stack", "compact", "no-xcd-map", "lds-scene", "lds-scene-lds-stack", "persist",
                      "scanline-order", "global-stack", "merge", "merge-scanline", "merge-lds-scene", "merge-queue-16",
-                     "no-defer"])
+                     "no-defer", "defer-level-1", "defer-level-3"])
 def stack_renderer(request, monkeypatch):
     """Non-default kernel layouts (RT_HIP_STACK=0: LDS reflection stack, the
     persistent kernel above depth 5; 2: workgroup-compacted reflection levels;
