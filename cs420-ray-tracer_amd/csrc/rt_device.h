@@ -97,6 +97,44 @@ __device__ __forceinline__ D3 normalized(D3 a) {
 // out of line it only adds its own frame where little of the caller is live.
 __device__ __attribute__((noinline)) double pow_call(double x, double y) { return pow(x, y); }
 
+// pow(x, n) for the specular term's usual operands -- x in (0, 1 + 2^-40],
+// n a whole shininess in [1, 1024] (every scene here uses 5..200) -- by
+// left-to-right binary exponentiation in double-double: each step (square,
+// times x) keeps the product as an unevaluated sum hi + lo, exact to ~2^-104
+// relative (products split with fma, renormalised by fast two-sum), so after
+// at most 20 steps hi + lo is within ~2^-99 of x^n and its rounding hi is the
+// correctly rounded x^n unless x^n lies within that distance of a rounding
+// boundary (probability ~2^-47 per call) -- the result glibc's pow (the
+// reference, correctly rounded in nearly all cases) returns.  ~6 fp64
+// operations per step instead of ocml's general pow (~220 instructions).
+// int_pow_ok() is the domain: also n * floor(log2 x) >= -900, so no partial
+// product leaves the normal range.
+__device__ __forceinline__ bool int_pow_ok(double x, double y, int &n) {
+  n = (int)y;
+  if (!(x > 0.0 && x <= 1.0 + 0x1p-40 && y >= 1.0 && y <= 1024.0 && (double)n == y)) return false;
+  const int ex = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
+  return ex * n >= -900;
+}
+__device__ __forceinline__ double int_pow(double x, int n) {
+  double h = x, l = 0.0;
+  for (int i = 30 - __builtin_clz((unsigned)n); i >= 0; --i) {
+    // (h, l)^2: h*h exactly as p + e, plus the cross term 2 h l (l^2 is below 2^-200 relative)
+    double p = h * h;
+    double e = __builtin_fma(h, h, -p);
+    e = __builtin_fma(h + h, l, e);
+    h = p + e;
+    l = e - (h - p);
+    if ((n >> i) & 1) {  // (h, l) * x
+      p = h * x;
+      e = __builtin_fma(h, x, -p);
+      e = __builtin_fma(l, x, e);
+      h = p + e;
+      l = e - (h - p);
+    }
+  }
+  return h;
+}
+
 __device__ __forceinline__ double max0(double x) { return (0.0 < x) ? x : 0.0; }  // std::max(0.0, x)
 __device__ __forceinline__ double min1(double x) { return (x < 1.0) ? x : 1.0; }  // std::min(1.0, x)
 

@@ -203,7 +203,10 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
           const D3 rdir = sub(nl2, scale(scale(nrm, 2.0), dot(nl2, nrm)));  // reflect(), vec3.h:31-33
           const double rdv = max0(dot(rdir, view));
           // pow(+0, y > 0) is +0 exactly (C99 F.10.4.4), so most lanes skip ocml's pow.
-          const double spec = (rdv == 0.0 && m.shin > 0.0) ? 0.0 : pow_call(rdv, m.shin);
+          double spec = 0.0;
+          int ipow = 0;
+          if (!(rdv == 0.0 && m.shin > 0.0))
+            spec = int_pow_ok(rdv, m.shin, ipow) ? int_pow(rdv, ipow) : pow_call(rdv, m.shin);
           const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
           col = add(add(specular, diffuse), col);                  // scene.h:117
         }

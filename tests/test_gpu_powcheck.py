@@ -1,0 +1,50 @@
+"""The specular term's pow on the GPU against the reference's (glibc pow, via
+numpy on the host): ocml's general pow and rtk::int_pow (rt_device.h,
+double-double binary exponentiation for whole shininess) on 4M operand pairs
+shaped like the renderer's (rdv in (0, 1], many near 1; shininess 1..256).
+glibc's pow is within 0.52 ulp, not always correctly rounded, so neither
+device pow matches it everywhere; int_pow is correctly rounded in nearly all
+cases and disagrees with glibc 150x less often than ocml's pow (0.09 % vs
+14 % of these pairs, always by 1 ulp)."""
+import ctypes as C
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+LIB = os.path.join(REPO, "tests", "native", "libpowcheck.so")
+
+
+@pytest.mark.gpu
+def test_int_pow_vs_glibc_and_ocml():
+    import torch  # noqa: F401  (brings up the HIP runtime the way the product does)
+
+    lib = C.CDLL(LIB)
+    P = C.POINTER(C.c_double)
+    lib.powcheck_run.argtypes = [P, C.POINTER(C.c_int), P, P, C.c_longlong]
+    rng = np.random.default_rng(420)
+    count = 1 << 22
+    x = rng.random(count)
+    near = rng.random(count) < 0.5
+    x[near] = 1.0 - x[near] * 1e-3
+    x = np.clip(x, 1e-300, 1.0)
+    n = rng.integers(1, 257, count).astype(np.int32)
+    n[: count // 4] = rng.choice(np.array([5, 10, 15, 20, 50, 100, 200], np.int32), count // 4)
+    ocml, dd = np.empty(count), np.empty(count)
+    assert lib.powcheck_run(x.ctypes.data_as(P), n.ctypes.data_as(C.POINTER(C.c_int)), ocml.ctypes.data_as(P),
+                            dd.ctypes.data_as(P), count) == 0
+    # glibc's pow itself (math.pow calls the C library's pow); numpy's power may
+    # take a SIMD implementation of its own on AVX-512 hosts
+    ref = np.fromiter(map(math.pow, x.tolist(), n.astype(np.float64).tolist()), np.float64, count)
+    used = dd >= 0  # int_pow's domain (x^n >= 2^-900)
+    assert used.mean() > 0.9
+    bad_dd = np.count_nonzero(dd[used] != ref[used])
+    bad_ocml = np.count_nonzero(ocml[used] != ref[used])
+    ulp = np.spacing(ref[used])
+    assert np.all(np.abs(dd[used] - ref[used]) <= ulp * 1.0001), "int_pow more than 1 ulp from glibc"
+    print(f"mismatches vs glibc over {used.sum()} pairs: int_pow {bad_dd}, ocml pow {bad_ocml}")
+    # measured: int_pow 3,869 (0.09 %, where glibc is not correctly rounded), ocml 570,344 (14 %)
+    assert bad_dd <= 0.005 * used.sum() and bad_dd <= bad_ocml
