@@ -562,6 +562,9 @@ constexpr int kStackMerge = 4;
 #define RT_DEFER_LEVEL 2
 #endif
 constexpr int kDeferLevel = RT_DEFER_LEVEL;
+#ifndef RT_DEFER_WGS
+#define RT_DEFER_WGS 48  // render_deferred workgroups (one wave each) per shard segment
+#endif
 #ifndef RT_DEFER_CAP_DIV
 #define RT_DEFER_CAP_DIV 8  // deferred-queue room: 1 / RT_DEFER_CAP_DIV of the launch's pixels
 #endif
@@ -1452,7 +1455,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
   if constexpr (kStack == kStackMerge) {
     if (ra.dq_cap > 0)  // 48 one-wave workgroups per shard segment
-      hipLaunchKernelGGL((render_deferred<kCull>), dim3(48 * kShards), dim3(64), lds, c->stream, ra);
+      hipLaunchKernelGGL((render_deferred<kCull>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
   }
   return RT_OK;
 }
