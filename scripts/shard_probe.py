@@ -38,7 +38,8 @@ def launch(rows):
         r.render_frames_async([cam] * fpl, W, H, D, rows, out.data_ptr(), rows.count * W * 3)
 
 
-for G in (1, 2, 4, 8):
+GS = tuple(int(g) for g in os.environ.get("GS", "1,2,4,8").split(","))
+for G in GS:
     per = []
     for k in range(G):
         rows = rt_hip.rows_for_shard(H, band, k, G) if G > 1 else rt_hip.rt_rows(1, 0, 1, H)
@@ -51,8 +52,10 @@ for G in (1, 2, 4, 8):
         per.append(sum(kt) / len(kt) / fpl)
     res[f"G{G}"] = {"max_ms": round(max(per), 4), "mean_ms": round(sum(per) / G, 4),
                     "shard_ms": [round(x, 4) for x in per]}
-full = res["G1"]["max_ms"]
-for G in (2, 4, 8):
-    res[f"G{G}"]["kernel_eff"] = round(full / (G * res[f"G{G}"]["max_ms"]), 3)
+if "G1" in res:
+    full = res["G1"]["max_ms"]
+    for G in GS:
+        if G > 1:
+            res[f"G{G}"]["kernel_eff"] = round(full / (G * res[f"G{G}"]["max_ms"]), 3)
 print(json.dumps(res))
 r.close()
