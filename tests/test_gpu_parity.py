@@ -100,6 +100,24 @@ def test_unpermute_kernel(gpu_renderer):
     assert image.cpu().numpy().tobytes() == golden_rgb(name)
 
 
+@pytest.mark.parametrize("W,G,band,off", [(1920, 8, 8, 0), (100, 3, 8, 0), (100, 3, 8, 4), (64, 5, 1, 1),
+                                          (97, 2, 16, 0)])
+def test_unpermute_copy_widths(gpu_renderer, W, G, band, off):
+    """The unpermute's 16-byte, 4-byte and byte copy paths (row bytes W*3 and
+    buffer offsets decide which) against the host permutation."""
+    import torch
+
+    H = 75
+    R = -(-(-(-H // band)) // G) * band
+    src = torch.randint(0, 256, (off + G * R * W * 3,), dtype=torch.uint8, device="cuda:0")
+    dst = torch.zeros((off + H * W * 3,), dtype=torch.uint8, device="cuda:0")
+    gpu_renderer.unpermute(src.data_ptr() + off, dst.data_ptr() + off, W, H, band, G, R)
+    gpu_renderer.stats()
+    s = src[off:].cpu().numpy().reshape(G, R, W * 3)
+    want = np.stack([s[(y // band) % G][(y // band // G) * band + y % band] for y in range(H)])
+    assert dst[off:].cpu().numpy().reshape(H, W * 3).tobytes() == want.tobytes()
+
+
 def test_async_on_external_stream(gpu_renderer):
     import torch
     import rt_hip
