@@ -347,6 +347,10 @@ def main():
                                  if k in pmc_rec},
                          "pmc_fp64_tflops": (round(pmc_rec["fp64_flops_per_frame"] / k_s / 1e12, 3)
                                              if "fp64_flops_per_frame" in pmc_rec else None),
+                         # the hardware's side of the same roof: the fraction of SIMD cycles
+                         # issuing VALU instructions (rocprofv3 PMC, per frame); `frac`
+                         # above counts brute-force-equivalent work and so exceeds 1
+                         "valu_busy_frac": pmc_rec.get("valu_busy"),
                          "culling": m["cull"],
                          "kernel_ms_mean": round(m["kernel_ms_mean"], 4),
                          "kernel_ms_min": round(m["kernel_ms_min"], 4),
