@@ -1890,7 +1890,7 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     br[i] = s->spheres[i].radius;
   }
   const bool big = n > kBvhAlwaysAbove;
-  c->bvh_leaf = c->bvh_leaf_opt ? c->bvh_leaf_opt : (big ? 2 : 4);
+  c->bvh_leaf = c->bvh_leaf_opt ? c->bvh_leaf_opt : 2;  // 2 measured +0.6..0.9 % over 4 with the merged levels
   c->lg_n = c->lg_n_opt ? c->lg_n_opt : (big ? 256 : 128);
   std::vector<BvhNode> nodes;
   std::vector<int32_t> prims;

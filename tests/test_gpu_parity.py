@@ -292,8 +292,8 @@ def test_cull_equals_bruteforce_at_4k(gpu_renderer):
 
 @pytest.fixture(params=[{"RT_HIP_BVH_ALWAYS": "1"}, {"RT_HIP_BVH_MIN": "0"}, {"RT_HIP_BVH": "0"},
                         {"RT_HIP_BVH_MIN": "0", "RT_HIP_LANE_SWEEP": "100000"},
-                        {"RT_HIP_BVH_ALWAYS": "1", "RT_HIP_BVH4": "0"}],
-                ids=["bvh-always", "bvh-min0", "bvh-off", "lane-sweep", "bvh-always-two-child"])
+                        {"RT_HIP_BVH_ALWAYS": "1", "RT_HIP_BVH4": "0"}, {"RT_HIP_BVH_LEAF": "4"}],
+                ids=["bvh-always", "bvh-min0", "bvh-off", "lane-sweep", "bvh-always-two-child", "leaf-4"])
 def bvh_renderer(request, monkeypatch):
     """A fresh context per BVH policy (the knobs are read at rt_create)."""
     import rt_hip
