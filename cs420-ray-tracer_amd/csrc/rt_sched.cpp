@@ -4,6 +4,10 @@
 #include <algorithm>
 #include <cmath>
 
+#ifndef RT_SCHED_BLOCKS
+#define RT_SCHED_BLOCKS 1
+#endif
+
 namespace rtk {
 
 namespace {
@@ -83,11 +87,25 @@ void tile_order(const SchedView &v, const std::vector<SchedSphere> &refl, std::v
     for (int ty = 0; ty < nty; ++ty)
       if (yhi[ty] >= ymin && ylo[ty] <= ymax) bump(ty, tx0, tx1);
   }
-  // counting sort, heaviest class first, scanline order within a class
+  // counting sort, heaviest class first; within a class the tiles follow 2x2
+  // blocks in scanline order of the blocks, so the consecutive slots one
+  // merged wave takes (kMergeTiles = 4) are a 16x16-pixel square, whose
+  // reflection rays are more alike than those of a 32x8 strip
+  std::vector<int> order;
+  order.reserve((size_t)ntiles);
+#if RT_SCHED_BLOCKS
+  for (int by = 0; by < nty; by += 2)
+    for (int bx = 0; bx < ntx; bx += 2)
+      for (int j = 0; j < 2; ++j)
+        for (int i = 0; i < 2; ++i)
+          if (by + j < nty && bx + i < ntx) order.push_back((by + j) * ntx + bx + i);
+#else
+  for (long long t = 0; t < ntiles; ++t) order.push_back((int)t);
+#endif
   long long start[kClasses + 1] = {};
   for (long long t = 0; t < ntiles; ++t) ++start[kClasses - 1 - cls[(size_t)t] + 1];
   for (int k = 0; k < kClasses; ++k) start[k + 1] += start[k];
-  for (long long t = 0; t < ntiles; ++t) perm[(size_t)start[kClasses - 1 - cls[(size_t)t]]++] = (int)t;
+  for (const int t : order) perm[(size_t)start[kClasses - 1 - cls[(size_t)t]]++] = t;
 }
 
 }  // namespace rtk
