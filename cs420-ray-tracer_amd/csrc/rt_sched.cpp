@@ -93,7 +93,18 @@ void tile_order(const SchedView &v, const std::vector<SchedSphere> &refl, std::v
   // reflection rays are more alike than those of a 32x8 strip
   std::vector<int> order;
   order.reserve((size_t)ntiles);
-#if RT_SCHED_BLOCKS
+#if RT_SCHED_BLOCKS == 2
+  // Z order over the whole tile grid: 2x2 blocks of 2x2 blocks, ...
+  for (long long t = 0; t < ntiles; ++t) order.push_back((int)t);
+  auto morton = [ntx](int t) {
+    const unsigned x = (unsigned)(t % ntx), y = (unsigned)(t / ntx);
+    unsigned long long m = 0;
+    for (int b = 0; b < 16; ++b)
+      m |= (unsigned long long)((x >> b) & 1u) << (2 * b) | (unsigned long long)((y >> b) & 1u) << (2 * b + 1);
+    return m;
+  };
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return morton(a) < morton(b); });
+#elif RT_SCHED_BLOCKS
   for (int by = 0; by < nty; by += 2)
     for (int bx = 0; bx < ntx; bx += 2)
       for (int j = 0; j < 2; ++j)
