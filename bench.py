@@ -16,9 +16,17 @@ as N grows ("scaling": "strong").  value = rays of the frame x K / max-over-rank
 time of the K timed steps.
 
 Also reported:
-  roofline      fp64 VALU roof of the render kernel: algorithmic FLOPs per
-                launch (25 per ray-sphere test x spheres x rays)
-                / mean in-stream HIP-event kernel time of the timed launches.
+  roofline      fp64 VALU roof of the render kernels (render_kernel +
+                render_deferred): the fp64 FLOPs they EXECUTE per frame (rocprofv3
+                PMC: 64 x (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions,
+                profiles/pmc_traffic.json, checked against the kernel sources'
+                hash) / the in-stream HIP-event kernel time per frame of the
+                timed launches, vs the 78.6 TFLOP/s fp64 vector peak; VALU busy
+                and the fp64 share of VALU issue beside it; traffic = HBM bytes
+                per launch (FETCH_SIZE x 2, the gfx950 correction, + WRITE_SIZE).
+                SURVEY 8(d)'s brute-force count (25 FLOP x spheres x rays) is
+                `algorithmic_equivalent`: the kernel prunes pairs exactly, so
+                that rate measures the algorithm and exceeds the peak.
   hbm_write     the north star's HBM-write roofline: W*H*3 bytes per frame.
   cpu_baseline  the reference's own trace_ray (oracle/_ref/ref_render, built
                 from /root/reference/src/main.cpp) on 1 host core, same
@@ -28,6 +36,7 @@ Also reported:
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import platform
@@ -54,6 +63,17 @@ FLOP_PER_CULL = 34          # rtk::keep(): 3 sub, |v.a| 5, v x a 9, |v x a|^2 5,
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X vector FP64 (spec; 256 CU x 2.4 GHz x 128 FLOP/clk)
 HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 BAND = 8
+# the sources the PMC record in profiles/pmc_traffic.json must have been measured with
+KERNEL_SOURCES = ("rt_kernel.hip", "rt_device.h", "rt_bvh.cpp", "rt_bvh.h", "rt_lightgrid.cpp", "rt_lightgrid.h",
+                  "rt_sched.cpp", "rt_sched.h")
+
+
+def kernel_source_sha() -> str:
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(PKG, "csrc", name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
 
 
 def dist_env():
@@ -172,7 +192,9 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
                 render_batch(shards[b & 1][:m])
                 done, b = done + m, b + 1
 
-    frames(warmup)
+    # at least one full batch: the launch shape of the timed region has run
+    # once (scratch sized, tile order built) before the clock starts
+    frames(max(warmup, F))
     render(shards[0][0])  # one single-frame launch (untimed): the ray counts of ONE frame of this rank's shard
     st = r.stats()  # syncs
     r.kernel_times()  # drop warmup launches from the history
@@ -194,12 +216,18 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
         t = torch.tensor([elapsed, kframe], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kmax = t.tolist()
+        per_rank = [torch.zeros(1, dtype=torch.float64, device=f"cuda:{device}") for _ in range(world)]
+        dist.all_gather(per_rank, torch.tensor([kframe], dtype=torch.float64, device=f"cuda:{device}"))
+        rank_kernel_ms = [round(float(x.item()), 5) for x in per_rank]
+        seen_world = dist.get_world_size()
         n = torch.tensor([my_rays], dtype=torch.int64, device=f"cuda:{device}")
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
         frame_rays = int(n.item())
     else:
         kmax = kframe
         frame_rays = my_rays
+        rank_kernel_ms = [round(kframe, 5)]
+        seen_world = 1
     assembled_ok = None
     if dist_on and rank == 0 and steps > 0:
         # untimed: the last frame reassembled from the gathered shards must equal
@@ -227,7 +255,9 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
             "kernel_ms_mean": kmean, "kernel_ms_per_frame": kframe, "kernel_ms_per_frame_max_rank": kmax,
             "kernel_ms_min": min(ktimes), "frames_per_launch": F,
             "launches_timed": len(ktimes), "rows_per_rank": R, "tests_exact": tests_exact,
-            "tests_cull": tests_cull, "cull": cull, "gather_ms_per_batch": gather_ms}
+            "tests_cull": tests_cull, "cull": cull, "gather_ms_per_batch": gather_ms,
+            "rank_kernel_ms_per_frame": rank_kernel_ms, "world_size_seen": seen_world,
+            "warmup_frames_rendered": max(warmup, F)}
 
 
 def main():

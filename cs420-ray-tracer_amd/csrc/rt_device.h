@@ -43,6 +43,10 @@ struct LightD {
 struct D3 {
   double x, y, z;
 };
+// One entry of a pixel's reflection stack (main.cpp:54): A = shade*(1-refl), and refl.
+struct StackEnt {  // 32 B
+  double ax, ay, az, refl;
+};
 __device__ __forceinline__ D3 mk(double x, double y, double z) { return D3{x, y, z}; }
 __device__ __forceinline__ D3 add(D3 a, D3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ D3 sub(D3 a, D3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -377,7 +381,6 @@ struct BvhArgs {
   const BvhNode4 *n4;
   int root4;
   int wide;
-  int lane_sweep;  // scenes of at most this many spheres: loose lanes sweep every leaf slot instead (lane_sweep())
   int ordered;  // the host allows the ordered walk (tree depth <= kOrderedStack)
   int odepth;   // stack entries per lane (the tree depth)
   int2 *ostk;
@@ -608,35 +611,6 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
   }
 }
 
-// The loose-group fallback without the tree: every lane runs the leaf loop of
-// bvh_walk over all n leaf slots (the same fp32 line prefilter, then
-// leaf_fn(sphere) for survivors).  The slot index is wave-uniform, so the
-// prefilter records are scalar broadcasts and the lanes never diverge on the
-// traversal itself -- for small scenes this beats divergent per-lane walks of
-// incoherent (reflection) rays.  A slot whose sphere lies wholly beyond
-// tmax_fn() along the line is skipped: any root of it has t >= (w.d)/|d|^2 - R
-// (R the grown fp32 radius, |d| = 1 +- 2^-50), and tmax_fn() carries the
-// 2e-6 * (diameter + |t|) margin, far above the fp32 error of w.d
-// (~3 * 2^-24 * diameter).
-template <typename T, typename F>
-__device__ __forceinline__ void lane_sweep(const BvhArgs &bv, int n, D3 o, D3 d, T &&tmax_fn, Work &work,
-                                           F &&leaf_fn) {
-  const float ox = (float)(o.x - bv.c0x), oy = (float)(o.y - bv.c0y), oz = (float)(o.z - bv.c0z);
-  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
-  const float dd = (dx * dx + dy * dy + dz * dz) * (1.0f + 1e-5f);
-  work.cull += (unsigned)n;
-  for (int k = 0; k < n; ++k) {
-    const float4 q = bv.pf[k];
-    const float wx = q.x - ox, wy = q.y - oy, wz = q.z - oz;
-    const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
-    const float R = q.w + bv.pmargin;
-    if (cx * cx + cy * cy + cz * cz > R * R * dd) continue;
-    const float ta = wx * dx + wy * dy + wz * dz;
-    if ((double)(ta - R) > tmax_fn()) continue;
-    if (!leaf_fn((int)bv.prims[k])) return;
-  }
-}
-
 // LDS layout of a staged scene: sphere geometry, radii, lights and, when the
 // scene is staged (lds_geo) and has a BVH, its nodes and leaf sphere indices.
 // The host sizes the dynamic LDS with the same function.
@@ -837,8 +811,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       test(i);
       return true;
     };
-    if (n <= bv.lane_sweep) lane_sweep(bv, n, o, d, tmax, work, leaf);
-    else if (has_ordered_stack(bv) && bv.wide) bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
+    if (has_ordered_stack(bv) && bv.wide) bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
     else if (has_ordered_stack(bv)) bvh_walk_ordered(bv, o, d, tmax, work, leaf);
     else bvh_walk(bv, o, d, tmax, work, leaf);
   }

@@ -28,7 +28,6 @@
 #pragma clang fp contract(off)
 
 #include "rt_device.h"
-#include "rt_wavefront.h"
 #include "rt_sched.h"
 
 #include <cmath>
@@ -44,7 +43,6 @@ constexpr int kTl = 16;  // u64 per wave
 __device__ unsigned long long g_timeline[kTimelineWaves * kTl];
 #endif
 
-constexpr int kMaxLdsStack = 4;  // levels of the LDS reflection stack (render_kernel)
 
 // Output of a launch.  RT_FB_RGB8 with full = 0: rows.count x W RGB8 (the
 // rows of `rows`, rt_render); RT_FB_RGB8 with full = 1: a W x H RGB8 image in
@@ -58,17 +56,13 @@ struct OutDesc {
   long long fstride;
 };
 
-// kStackSplit: level 0 here, the reflection levels through the ray queues of
-// rt_wavefront.h (wf_bounce), the unwind in wf_resolve.
-struct SplitArgs {
-  RayRec *rayq;       // [kShards][seg_cap]
-  unsigned *ray_cnt;  // [depth+1][kShards]
-  int seg_cap;
-  Term *term;         // [npx]
-  uint8_t *nlev;      // [npx]
+// A queued ray of the merged levels (merge_tiles' LDS queue, render_deferred's
+// global queue): origin, direction, stack level, depth left, the sphere it
+// leaves, and its pixel.
+struct QRay {  // 64 B
+  double ox, oy, oz, dx, dy, dz;
+  int orig, dleft, key, pix;
 };
-
-struct QRay;
 // All arguments of render_kernel in one struct: its only kernel parameter, so
 // it sits at offset 0 of the kernarg segment and a member can be re-read from
 // there by offsetof (kernarg_late).
@@ -88,8 +82,7 @@ struct RenderArgs {
   OutDesc od;
   StackEnt *gstack;
   unsigned long long *counters;
-  int ntx, ntiles, xcd_per;
-  SplitArgs sa;
+  int ntx, ntiles;
   const int *perm;
   unsigned long long *zero_next;  // counters of the next launch, zeroed by workgroup 0 (or nullptr)
   QRay *dq;                       // kStackMerge: deferred deep rays, [kShards][dq_cap] (render_deferred)
@@ -290,122 +283,27 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
   return res;
 }
 
-// Workgroup-compacted trace_ray.  Level 0 runs one lane per pixel (coherent
-// 8x8 tiles); the reflection rays it spawns, typically a few dozen of the
-// workgroup's 256 pixels, are appended to an LDS queue and the next level
-// runs them packed into the first waves, so the incoherent levels pay for
-// the rays they trace instead of a whole wave per tile.  Each pixel keeps
-// its (shade*(1-refl), refl) entries in `gstack` ([level][pixel], global
-// memory) and its final colour + level count in `term` (LDS); the unwind is
-// per pixel, innermost level first, exactly as trace_wave / main.cpp:54.
-struct QRay {  // 64 B
-  double ox, oy, oz, dx, dy, dz;
-  int orig, dleft, key, pix;
-};
-struct TermRec {  // 32 B
-  double r, g, b;
-  int nlev, pad;
-};
-template <bool kCull>
-__device__ __forceinline__ D3 trace_compact(const SphGeo *__restrict__ g, const double *__restrict__ rad,
-                                            const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
-                                            int nl, D3 amb, int depth, const BvhArgs &bv, const LgArgs &lg,
-                                            bool live, D3 o, D3 d, int pix, StackEnt *__restrict__ gstack,
-                                            size_t npx, QRay *q, int *qcnt, TermRec *term, Work &work,
-                                            unsigned &c_prim, unsigned &c_shadow, unsigned &c_reflect) {
-  const int t = threadIdx.x, lane = t & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  // appends this wave's spawned rays to the LDS queue
-  auto push = [&](bool spawn, const QRay &r) {
-    const unsigned long long m = __ballot(spawn);
-    int base = 0;
-    if (lane == 0 && m) base = atomicAdd(qcnt, (int)__popcll(m));
-    base = __shfl(base, 0, 64);
-    if (spawn) q[base + (int)__popcll(m & lt)] = r;
-  };
-  if (t == 0) *qcnt = 0;
-  __syncthreads();
-  {  // level 0: this lane's camera ray
-    const bool alive = live && depth >= 1;
-    c_prim += alive ? 1u : 0u;
-    int outcome = 0, nkey = 0;
-    D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;  // depth <= 0 -> black (main.cpp:17-18)
-    double refl = 0.0;
-    if (__ballot(alive))
-      bounce<kCull>(g, rad, mat, slight, n, nl, amb, bv, lg, alive, o, d, -1, depth, work, c_shadow, outcome, color,
-                    refl, no, nd, nkey);
-    const bool spawn = alive && outcome == kSpawned;
-    if (live) term[t] = TermRec{color.x, color.y, color.z, 0, 0};
-    if (spawn) {
-      gstack[pix] = StackEnt{color.x, color.y, color.z, refl};
-      ++c_reflect;
-    }
-    push(spawn, QRay{no.x, no.y, no.z, nd.x, nd.y, nd.z, t, depth - 1, nkey, pix});
-  }
-  __syncthreads();
-  for (int lev = 1; lev < depth; ++lev) {
-    const int nq = *qcnt;
-    if (nq == 0) break;  // workgroup-uniform
-    const bool act = t < nq;
-    QRay r = q[act ? t : 0];
-    __syncthreads();
-    if (t == 0) *qcnt = 0;
-    __syncthreads();
-    if (__ballot(act)) {
-      int outcome = 0, nkey = 0;
-      D3 color = mk(0.0, 0.0, 0.0), no = mk(r.ox, r.oy, r.oz), nd = mk(r.dx, r.dy, r.dz);
-      double refl = 0.0;
-      bounce<kCull>(g, rad, mat, slight, n, nl, amb, bv, lg, act, mk(r.ox, r.oy, r.oz), mk(r.dx, r.dy, r.dz), r.key,
-                    r.dleft, work, c_shadow, outcome, color, refl, no, nd, nkey);
-      const bool spawn = act && outcome == kSpawned;
-      if (act) term[r.orig] = TermRec{color.x, color.y, color.z, lev, 0};
-      if (spawn) {
-        gstack[(size_t)lev * npx + r.pix] = StackEnt{color.x, color.y, color.z, refl};
-        ++c_reflect;
-      }
-      push(spawn, QRay{no.x, no.y, no.z, nd.x, nd.y, nd.z, r.orig, r.dleft - 1, nkey, r.pix});
-    }
-    __syncthreads();
-  }
-  D3 res = mk(0.0, 0.0, 0.0);
-  if (live) {
-    const TermRec e0 = term[t];
-    res = mk(e0.r, e0.g, e0.b);
-    for (int lev = e0.nlev - 1; lev >= 0; --lev) {  // unwind, innermost first
-      const StackEnt e = gstack[(size_t)lev * npx + pix];
-      res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
-    }
-  }
-  return res;
-}
-
-
 // One 8x8 tile of pixels, one lane per pixel; `samples` = 1 (the serial
 // path) or 4 (main_gpu.cu:249-333's antialias offsets, in fp64 serial
 // semantics: samples summed in order, then * 0.25).  Adds the tile's ray
 // counts to the wave sums.
 struct CompactArgs {
-  D3 *park;  // kStackGlobal with kernarg-resident arguments: this wave's parked colours (LDS)
+  D3 *park;          // kStackGlobal with kernarg-resident arguments: this wave's parked colours (LDS)
   StackEnt *gstack;  // [depth-1][npx]
   size_t npx;        // level stride: pixels of all frames of the launch
   unsigned fpx;      // this wave's frame's first stack entry (frame * pixels per frame)
-  QRay *q;           // LDS
-  int *qcnt;         // LDS
-  TermRec *term;     // LDS
 };
 
-// Reflection stack placement: kStackLds = [level][lane] per wave in LDS (4
-// levels), kStackGlobal = [level][pixel] in global memory (any depth),
-// kStackCompact = global, with the workgroup-compacted levels of trace_compact.
-// kStackSplit = level 0 only, the rest queued (SplitArgs).
-enum { kStackLds = 0, kStackGlobal = 1, kStackCompact = 2, kStackSplit = 3 };
+// Reflection stack placement: kStackGlobal = [level][pixel] in global memory
+// (any depth, one tile per wave: trace_wave); kStackMerge = the same stack with
+// merged reflection levels (merge_tiles, below).
+enum { kStackGlobal = 1, kStackMerge = 4 };
 template <bool kCull, int kSamples, int kStack, bool kArgMem = false>
 __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                            const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                            int nl, D3 amb, const Cam &cam, int W_arg, int H_arg, int depth,
                                            const Rows &rows_arg, const BvhArgs &bv, const LgArgs &lg,
-                                           const OutDesc &od_arg, int x0, int k0, StackEnt *stk,
-                                           const CompactArgs &ca, const SplitArgs &sa, Work &work,
+                                           const OutDesc &od_arg, int x0, int k0, const CompactArgs &ca, Work &work,
                                            unsigned long long (&sums)[4], int frame = 0) {
   const int W = W_arg, H = H_arg;
   const Rows &rows = rows_arg;
@@ -431,41 +329,10 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
                        scale(mk(cam.ux, cam.uy, cam.uz), sv));
     const D3 d = normalized(normalized(dir));  // get_ray normalises, Ray() normalises again
     const D3 o = mk(cam.px, cam.py, cam.pz);
-    D3 c;
     const int pix = k * od.xw + (x - od.x0);
-    if (kStack == kStackSplit) {  // level 0; spawned rays go to the level-1 queue
-      const bool alive = in_img && depth >= 1;
-      c_prim += alive ? 1u : 0u;
-      int outcome = 0, nkey = 0;
-      D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;  // depth <= 0 -> black (main.cpp:17-18)
-      double refl = 0.0;
-      if (__ballot(alive))
-        bounce<kCull, kArgMem>(g, rad, mat, slight, n, nl, amb, bv, lg, alive, o, d, -1, depth, work, c_shadow,
-                               outcome, color, refl, no, nd, nkey);
-      const bool spawn = alive && outcome == kSpawned;
-      if (in_img && !spawn) {
-        sa.term[pix] = Term{color.x, color.y, color.z};
-        sa.nlev[pix] = 0;
-      }
-      if (spawn) {
-        ca.gstack[pix] = StackEnt{color.x, color.y, color.z, refl};
-        ++c_reflect;
-      }
-      const unsigned shard = blockIdx.x % kShards;
-      const unsigned slot = wave_append(spawn, &sa.ray_cnt[1 * kShards + shard]);
-      if (spawn)
-        sa.rayq[(size_t)shard * sa.seg_cap + slot] = RayRec{no.x, no.y, no.z, nd.x, nd.y, nd.z, pix, depth - 1, nkey, 0};
-      c = color;
-    } else if (kStack == kStackCompact)
-      c = trace_compact<kCull>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, pix, ca.gstack, ca.npx,
-                               ca.q, ca.qcnt, ca.term, work, c_prim, c_shadow, c_reflect);
-    else if (kStack == kStackGlobal)
-      c = trace_wave<kCull, kArgMem, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, ca.gstack,
-                                              (unsigned)pix + ca.fpx, (unsigned)ca.npx, work, c_prim, c_shadow,
-                                              c_reflect, ca.park);
-    else
-      c = trace_wave<kCull, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d, stk, (unsigned)lane, 64u, work,
-                            c_prim, c_shadow, c_reflect);
+    const D3 c = trace_wave<kCull, kArgMem, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d,
+                                                     ca.gstack, (unsigned)pix + ca.fpx, (unsigned)ca.npx, work,
+                                                     c_prim, c_shadow, c_reflect, ca.park);
     acc = kSamples == 1 ? c : add(acc, c);  // serial: the colour itself; AA: from 0 in sample order (main_gpu.cu:250, 327)
   }
   const D3 res = kSamples == 4 ? scale(acc, 0.25) : acc;  // main_gpu.cu:331, 1/4 is exact
@@ -485,9 +352,7 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
                         (k % rows.band);
     const bool in_img = in_tile && y < H;
     const int j = H - 1 - (int)(in_img ? y : 0);
-  if (kStack == kStackSplit) {
-    // the colour is written by wf_resolve once the queued levels are done
-  } else if (od.fmt == RT_FB_RGB8) {
+  if (od.fmt == RT_FB_RGB8) {
     // RGB8: a tile row of 8 pixels is 24 contiguous bytes.  When the whole row
     // is written and dword aligned, lanes 0-5 of the row store it as 6 dwords
     // assembled with two shuffles; otherwise every lane stores its 3 bytes.
@@ -554,7 +419,6 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
 #define RT_MERGE_TILES 4
 #endif
 constexpr int kMergeTiles = RT_MERGE_TILES;
-constexpr int kStackMerge = 4;
 // Rays of reflection level >= kDeferLevel leave the merged megakernel for
 // render_deferred, a second kernel over all deferred rays of the launch; the
 // per-shard count lives in u64 slot kDeferSlot of the launch's counter shards.
@@ -798,29 +662,19 @@ __device__ __forceinline__ void record_timeline(unsigned wave_id, unsigned long 
 #ifndef RT_MIN_WAVES_PER_EU
 #define RT_MIN_WAVES_PER_EU 3  // caps VGPRs at 168: three waves per SIMD
 #endif
-// One wave per 8x8 tile (2x2 tiles per workgroup for kWaves = 4); the
-// reflection stack (depth <= 5) lives in LDS after the staged scene.
-constexpr int kWaves = 4;  // 2x2 tiles of 8x8 pixels per workgroup (persistent kernel, LDS sizes)
-// Waves per render_kernel workgroup: 4 (2x2 tiles) when the workgroup shares
-// LDS (a staged scene, the LDS stack or the compaction queue); 1 otherwise, so
-// no wave's slot waits for its slowest neighbour.
-template <bool kLdsGeo, int kStack>
+// Waves per render_kernel workgroup: 4 (2x2 tiles of 8x8 pixels) when the
+// workgroup shares a scene staged in LDS; 1 otherwise, so no wave's slot
+// waits for its slowest neighbour.
+template <bool kLdsGeo>
 constexpr int wg_waves() {
-  return (kLdsGeo || (kStack != 1 && kStack != 3 && kStack != 4)) ? 4 : 1;
+  return kLdsGeo ? 4 : 1;
 }
-// LDS after the staged scene: the 4-level reflection stack per wave, or
-// (kCompact) the workgroup's ray queue, terminal colours and queue count.
-constexpr size_t kLdsStackBytes = (size_t)kWaves * 64 * kMaxLdsStack * sizeof(StackEnt);
-constexpr size_t kLdsCompactBytes = (size_t)kWaves * 64 * (sizeof(QRay) + sizeof(TermRec)) + 32;
 
 template <bool kLdsGeo, bool kCull, int kSamples, int kStack>
-__global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PER_EU) void render_kernel(
+__global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) void render_kernel(
     const RenderArgs a) {
-  // Workgroups are dealt to the 8 XCDs round robin (b % 8).  perm: the host's
-  // launch order (rt_sched.h).  Otherwise, with xcd_per > 0 the
-  // scanline-ordered tiles are cut into runs of `xcd_per` tiles and run r goes
-  // to XCD r % 8: each XCD's L2 serves a few compact image regions while every
-  // XCD still samples the whole image.
+  // Workgroups are dealt to the 8 XCDs round robin (b % 8), so every image
+  // region is spread over all XCDs.  perm: the host's launch order (rt_sched.h).
   const int b = blockIdx.x;
   if (b == 0 && a.zero_next)
     for (int i = (int)threadIdx.x; i < kShards * kShardStride; i += (int)blockDim.x) a.zero_next[i] = 0ull;
@@ -835,9 +689,6 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
     if (a.perm) {
       if (slot >= a.ntiles) return;
       tile = a.perm[slot];  // heaviest predicted tiles first
-    } else if (a.xcd_per > 0) {  // single-frame launches only (launch_tiles)
-      const int m = b >> 3;  // this workgroup's rank on its XCD
-      tile = ((m / a.xcd_per) * 8 + (b & 7)) * a.xcd_per + m % a.xcd_per;
     }
     if (tile >= a.ntiles) return;  // workgroup-uniform, before any barrier
   }
@@ -855,24 +706,20 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
   stage_scene<kLdsGeo>(smem, a.geo, a.radius, a.mat, a.lights, a.n, a.nl, bv_local, g, rad, sm, slight);
   const size_t stack_off = (lds_layout(kLdsGeo, a.n, a.nl, a.bv.nnodes).end + 31) & ~(size_t)31;
   // the ordered BVH walk's per-lane stacks, [wave][entry][lane], after the scene
-  if (kLdsGeo && (kStack == kStackGlobal || kStack == kStackSplit) && bv_local.ordered)
+  if (kLdsGeo && bv_local.ordered)
     bv_local.ostk = reinterpret_cast<int2 *>(smem + stack_off) + (size_t)(threadIdx.x >> 6) * bv_local.odepth * 64;
   const BvhArgs &bv = kLdsGeo ? bv_local : a.bv;
-  constexpr int kWg = wg_waves<kLdsGeo, kStack>();
+  constexpr int kWg = wg_waves<kLdsGeo>();
   constexpr int kWx = kWg == 4 ? 2 : 1;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: keeps tile coordinates in SGPRs
-  StackEnt *stk = reinterpret_cast<StackEnt *>(smem + stack_off) + (size_t)wave * kMaxLdsStack * 64;
   CompactArgs ca;
   ca.park = nullptr;
-  if (!kLdsGeo && (kStack == kStackGlobal || kStack == kStackMerge))  // after the ordered walk's stacks (launch_tiles sizes both)
+  if (!kLdsGeo)  // after the ordered walk's stacks (launch_tiles sizes both)
     ca.park = reinterpret_cast<D3 *>(smem + stack_off + (a.bv.ordered ? (size_t)kWg * a.bv.odepth * 64 * sizeof(int2) : 0)) +
               (size_t)wave * 64;
   ca.gstack = a.gstack;
   ca.npx = (size_t)a.rows.count * a.od.xw * nf;
   ca.fpx = (unsigned)((size_t)a.rows.count * a.od.xw * frame);
-  ca.q = reinterpret_cast<QRay *>(smem + stack_off);
-  ca.term = reinterpret_cast<TermRec *>(smem + stack_off + (size_t)kWaves * 64 * sizeof(QRay));
-  ca.qcnt = reinterpret_cast<int *>(smem + stack_off + (size_t)kWaves * 64 * (sizeof(QRay) + sizeof(TermRec)));
   Work work;
   unsigned long long sums[4] = {0, 0, 0, 0};
   RT_T0(t_wave);
@@ -887,7 +734,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo, kStack>()), RT_MIN_WAVES_PE
     trace_tile<kCull, kSamples, kStack, !kLdsGeo>(g, rad, sm, slight, a.n, a.nl, a.amb, kernarg_cam(frame), a.W, a.H,
                                                   a.depth, a.rows, bv, a.lg, a.od,
                                                   a.od.x0 + tx * (8 * kWx) + (wave % kWx) * 8,
-                                                  ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, stk, ca, a.sa, work,
+                                                  ty * (8 * (kWg / kWx)) + (wave / kWx) * 8, ca, work,
                                                   sums, frame);
   }
   RT_ACC(work, 5, t_wave);
@@ -981,129 +828,6 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
   flush_counts(kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters), sums, work);
 }
 
-// Reflection level `level` of the split pipeline (RT_HIP_PIPELINE=3): one
-// lane per queued ray, a persistent grid-stride loop over the level's queue
-// segment (workgroup b serves segment b % kShards), the megakernel's bounce()
-// with its ordered BVH walk.  Level L reads ray buffer L & 1 and appends the
-// rays it spawns to buffer (L + 1) & 1; a chain that ends writes its colour
-// and level count for wf_resolve.
-template <bool kLdsGeo, bool kCull>
-__global__ __launch_bounds__(256) void wf_bounce(WfArgs a, int level) {
-  const unsigned shard = blockIdx.x % kShards, j = blockIdx.x / kShards, nj = gridDim.x / kShards;
-  const unsigned cnt = a.ray_cnt[level * kShards + shard];
-  if (j * 256u >= cnt) return;  // workgroup-uniform, before any barrier
-  RayRec *const bufs[2] = {a.rayq, reinterpret_cast<RayRec *>(a.hitq)};
-  const RayRec *__restrict__ rq = bufs[level & 1] + (size_t)shard * a.seg_cap;
-  RayRec *__restrict__ wq = bufs[(level + 1) & 1] + (size_t)shard * a.seg_cap;
-  extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
-  const SphGeo *g;
-  const double *rad;
-  const LightD *lights;
-  BvhArgs bv;
-  stage<kLdsGeo>(a, smem, g, rad, lights, bv);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (bv.ordered)
-    bv.ostk = reinterpret_cast<int2 *>(smem + ((lds_layout(kLdsGeo, a.n, a.nl, a.bv.nnodes).end + 31) & ~(size_t)31)) +
-              (size_t)wave * bv.odepth * 64;
-  Work work;
-  unsigned c_shadow = 0, c_reflect = 0;
-  const unsigned stride = nj * 256u;
-  for (unsigned base = j * 256u + wave * 64u; base < cnt; base += stride) {
-    const unsigned idx = base + lane;
-    const bool act = idx < cnt;
-    const RayRec r = rq[act ? idx : base];
-    int outcome = 0, nkey = 0;
-    D3 color = mk(0.0, 0.0, 0.0), no = mk(r.ox, r.oy, r.oz), nd = mk(r.dx, r.dy, r.dz);
-    double refl = 0.0;
-    bounce<kCull>(g, rad, a.mat, lights, a.n, a.nl, a.amb, bv, a.lg, act, mk(r.ox, r.oy, r.oz),
-                  mk(r.dx, r.dy, r.dz), r.key, r.dleft, work, c_shadow, outcome, color, refl, no, nd, nkey);
-    const bool spawn = act && outcome == kSpawned;
-    if (act && !spawn) {
-      a.term[r.pix] = Term{color.x, color.y, color.z};
-      a.nlev[r.pix] = (uint8_t)level;
-    }
-    if (spawn) {
-      a.stack[(size_t)level * a.npx + r.pix] = StackEnt{color.x, color.y, color.z, refl};
-      ++c_reflect;
-    }
-    const unsigned slot = wave_append(spawn, &a.ray_cnt[(level + 1) * kShards + shard]);
-    if (spawn) wq[slot] = RayRec{no.x, no.y, no.z, nd.x, nd.y, nd.z, r.pix, r.dleft - 1, nkey, 0};
-  }
-  const unsigned long long ss = wave_sum(c_shadow), sr = wave_sum(c_reflect);
-  if (lane == 0) {
-    unsigned long long *sc = counter_shard(a.counters);
-    if (ss) atomicAdd(&sc[1], ss);
-    if (sr) atomicAdd(&sc[2], sr);
-  }
-  flush_work(work, a.counters);
-}
-
-// Persistent variant: a resident grid whose waves take 8x8 tiles from 64
-// sharded tile counters (tiles in scanline order; a wave moves to the next
-// shard when its own is drained), so the scene is staged once per workgroup
-// and the reflection stack of any depth sits in global memory, one
-// [level][lane] slice per wave.
-constexpr int kTileShards = 64;
-#ifndef RT_PERSIST_WAVES_PER_EU
-#define RT_PERSIST_WAVES_PER_EU 3
-#endif
-template <bool kLdsGeo, bool kCull, int kSamples>
-__global__ __launch_bounds__(64 * kWaves, RT_PERSIST_WAVES_PER_EU) void render_persist(
-    const SphGeo *__restrict__ geo, const double *__restrict__ radius, const SphMat *__restrict__ mat,
-    const LightD *__restrict__ lights, int n, int nl, D3 amb, Cam cam, int W, int H, int depth, Rows rows,
-    BvhArgs bv_in, LgArgs lg, OutDesc od, unsigned long long *__restrict__ counters,
-    StackEnt *__restrict__ gstack, unsigned *__restrict__ tile_ctr, int ntx, int ntiles) {
-  extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
-  const SphGeo *g;
-  const double *rad;
-  const LightD *slight;
-  const SphMat *sm;
-  BvhArgs bv = bv_in;
-  stage_scene<kLdsGeo>(smem, geo, radius, mat, lights, n, nl, bv, g, rad, sm, slight);
-  // the ordered BVH walk's per-lane stacks, [wave][entry][lane], after the scene
-  if (bv.ordered)
-    bv.ostk = reinterpret_cast<int2 *>(smem + ((lds_layout(kLdsGeo, n, nl, bv_in.nnodes).end + 31) & ~(size_t)31)) +
-              (size_t)(threadIdx.x >> 6) * bv.odepth * 64;
-  const unsigned wave_id = blockIdx.x * kWaves + (threadIdx.x >> 6);
-  const int levels = depth > 1 ? depth - 1 : 1;
-  StackEnt *stk = gstack + (size_t)wave_id * levels * 64;
-  const int per = (ntiles + kTileShards - 1) / kTileShards;
-  int shard = (int)(wave_id % kTileShards);
-  Work work;
-  unsigned long long sums[4] = {0, 0, 0, 0};
-  RT_T0(t_wave);
-#ifdef RT_STAMPS
-  const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
-#endif
-  // The next tile index is requested before the current tile is traced, so
-  // the atomic's latency overlaps the work.
-  auto fetch = [&](int sh) -> unsigned {
-    unsigned t = 0;
-    if ((threadIdx.x & 63) == 0) t = atomicAdd(&tile_ctr[sh * 64], 1u);
-    return t;
-  };
-  unsigned pending = fetch(shard);
-  for (int tries = 0; tries < kTileShards;) {
-    const unsigned t = __builtin_amdgcn_readfirstlane(pending);
-    const long long tile = (long long)shard * per + t;
-    if ((int)t >= per || tile >= ntiles) {  // shard drained
-      shard = shard + 1 == kTileShards ? 0 : shard + 1;
-      ++tries;
-      if (tries < kTileShards) pending = fetch(shard);
-      continue;
-    }
-    pending = fetch(shard);
-    const int ty = (int)(tile / ntx), tx = (int)(tile % ntx);
-    trace_tile<kCull, kSamples, kStackLds>(g, rad, sm, slight, n, nl, amb, cam, W, H, depth, rows, bv, lg, od,
-                                           od.x0 + tx * 8, ty * 8, stk, CompactArgs{}, SplitArgs{}, work, sums);
-  }
-  RT_ACC(work, 5, t_wave);
-#ifdef RT_STAMPS
-  record_timeline(wave_id, t_real0, work);
-#endif
-  flush_counts(counters, sums, work);
-}
-
 // Reassemble rank-major shards into PPM row order (one workgroup per row).
 __global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                            int W, int H, int band, int G, int R) {
@@ -1140,6 +864,7 @@ struct rt_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
+  hipEvent_t switch_ev = nullptr;  // rt_set_stream: orders the new stream after the old one
   SphGeo *d_geo = nullptr;
   double *d_rad = nullptr;  // |radius|, for the conservative cull only
   SphMat *d_mat = nullptr;
@@ -1165,15 +890,10 @@ struct rt_ctx {
   // RT_HIP_BVH_LEAF; 0 = 4, or 2 above kBvhAlwaysAbove spheres (synth10k: with
   // the 256 grid 6.95 -> 6.46 ms; neither helps synth200)
   int bvh_leaf_opt = 0;
-  int lane_sweep = 0;  // RT_HIP_LANE_SWEEP: loose groups sweep all leaf slots per lane up to this many spheres
   // -1 (auto): every group walks the BVH when the scene has more than
   // kBvhAlwaysAbove spheres (a linear cull sweep is O(n) per group)
   int bvh_always = -1;
-  int pipeline = 0;  // 0 = megakernel (default), 1 = wavefront queues (knob RT_HIP_PIPELINE)
   int n_cu = 256;
-  // wavefront scratch: queues, per-pixel terminal colours / stack (grown on demand)
-  unsigned char *wf_buf = nullptr;
-  size_t wf_bytes = 0;
   LightD *d_lights = nullptr;
   int nsph = 0, nlight = 0;
   double amb[3] = {0, 0, 0};
@@ -1194,13 +914,8 @@ struct rt_ctx {
   long long launches = 0, hist_begin = 0;
   uint8_t *d_tmp = nullptr;
   size_t tmp_bytes = 0;
-  // persistent megakernel: tile counters + per-wave reflection stacks (grown on demand)
-  unsigned char *stack_buf = nullptr;
-  size_t stack_bytes = 0;
   int samples = 1;  // 4: the antialias mode (rt_set_antialias)
-  // RT_HIP_STACK: 0 LDS reflection stack (persistent kernel above depth 5),
-  // 1 global per-pixel stack, 2 global stack + workgroup-compacted levels
-  int stack_mode = 4;  // RT_HIP_STACK: 4 merged reflection levels (default), 1 per-pixel global stack, 0 LDS, 2 compacted
+  int stack_mode = 4;  // RT_HIP_STACK: 4 merged reflection levels (default), 1 per-pixel global stack (one tile per wave)
   bool defer = true;          // RT_HIP_DEFER: kStackMerge defers rays of level >= kDeferLevel to render_deferred
   int merge_q = 64;           // kStackMerge: the launch's LDS queue entries per wave (launch_render4 picks it)
   int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (16, 32 or 64)
@@ -1210,7 +925,6 @@ struct rt_ctx {
   // frames of the launch being enqueued (rt_render_frames_async; 1 otherwise) and their cameras
   int nframes = 1;
   const rt_camera *fcams = nullptr;
-  int xcd_map = 0;  // RT_HIP_XCD_MAP: visits per XCD (runs of ntiles/(8*visits) tiles); 0 = launch order
   unsigned char *cstack_buf = nullptr;
   size_t cstack_bytes = 0;
   // RT_HIP_LDS_SCENE=1: stage scenes that fit (<= kLdsBudget) in LDS, 4-wave
@@ -1227,7 +941,6 @@ struct rt_ctx {
   unsigned long long perm_gen = ~0ull;
   int *d_perm = nullptr, *h_perm = nullptr;  // h_perm pinned
   size_t perm_cap = 0;
-  int persist = 0;  // RT_HIP_PERSIST=1: persistent megakernel for every depth (always used above depth 5)
   std::string err;
 };
 
@@ -1303,7 +1016,6 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   b.pmargin = 4.0f * b.margin;
   if (!std::isfinite(b.diam)) b.diam = INFINITY;
   b.min_cands = c->bvh_min;
-  b.lane_sweep = c->lane_sweep;
   b.always = c->bvh_always >= 0 ? c->bvh_always : (c->nsph > kBvhAlwaysAbove ? 1 : 0);
   b.max_groups = c->bvh_groups;
   return b;
@@ -1364,40 +1076,37 @@ int tile_perm(rt_ctx *c, const Cam &cam, int W, int H, const Rows &rows, const O
 
 template <bool kLds, bool kCull, int kSamples, int kStack>
 int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                 const OutDesc &od, const SplitArgs &sa = SplitArgs{}, StackEnt *split_stack = nullptr) {
+                 const OutDesc &od) {
   BvhArgs bv = bvh_args(c, cam);
   const LgArgs lg = lg_args(c);
-  constexpr int kWg = wg_waves<kLds, kStack>(), kWx = kWg == 4 ? 2 : 1, kWy = kWg / kWx;
-  // the ordered walk's stacks follow the scene in LDS (render_kernel, kStackGlobal / kStackSplit / kStackMerge)
-  if ((kStack == kStackGlobal || kStack == kStackSplit || kStack == kStackMerge) && bv.ordered)
+  constexpr int kWg = wg_waves<kLds>(), kWx = kWg == 4 ? 2 : 1, kWy = kWg / kWx;
+  // the ordered walk's stacks follow the scene in LDS (render_kernel)
+  if (bv.ordered)
     bv.ostk_off = (int)((lds_layout(kLds, c->nsph, c->nlight, bv.nnodes).end + 31) & ~(size_t)31);
   const int ntx = (od.xw + 8 * kWx - 1) / (8 * kWx), nty = (rows.count + 8 * kWy - 1) / (8 * kWy);
   const long long ntiles = (long long)ntx * nty;
-  // frames of this launch (rt_render_frames_async): the global reflection stack only
+  // frames of this launch (rt_render_frames_async)
   const int nf = c->nframes;
-  if (nf < 1 || nf > RT_MAX_FRAMES || (nf > 1 && kStack != kStackGlobal && kStack != kStackMerge))
-    return RT_ERR_INVALID_ARG;
+  if (nf < 1 || nf > RT_MAX_FRAMES) return RT_ERR_INVALID_ARG;
   // kStackMerge: one wave per kMergeTiles consecutive tile slots
   const long long nslots = kStack == kStackMerge ? (ntiles + kMergeTiles - 1) / kMergeTiles : ntiles;
   if (ntiles * nf > (1LL << 30)) return RT_ERR_INVALID_ARG;
-  // runs of tiles per XCD visit (see render_kernel); grid rounded up to whole rounds
-  const int xcd_per = (c->xcd_map > 0 && nf == 1 && kStack != kStackMerge)
-                        ? (int)std::max(1LL, ntiles / (8LL * c->xcd_map)) : 0;
-  const long long rounds = xcd_per ? (ntiles + 8LL * xcd_per - 1) / (8LL * xcd_per) : 0;
-  const dim3 grid(xcd_per ? (unsigned)(rounds * 8 * xcd_per) : (unsigned)(nslots * nf));
+  const dim3 grid((unsigned)(nslots * nf));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
-  lds = ((lds + 31) & ~(size_t)31) +
-        (kStack == kStackCompact ? kLdsCompactBytes : kStack == kStackLds ? kLdsStackBytes : 0);
+  lds = (lds + 31) & ~(size_t)31;
   // the kernel places the ordered walk's stacks from these same arguments
-  if ((kStack == kStackGlobal || kStack == kStackSplit || kStack == kStackMerge) && bv.ordered)
+  if (bv.ordered)
     lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
   if (!kLds && kStack == kStackGlobal) lds += (size_t)kWg * 64 * sizeof(D3);  // parked colours (trace_wave)
   if (kStack == kStackMerge) lds += (size_t)c->merge_q * sizeof(QRay);         // the wave's ray queue (merge_tiles)
-  StackEnt *gstack = split_stack;
-  if (kStack != kStackLds && kStack != kStackSplit && depth > 1) {
+  StackEnt *gstack = nullptr;
+  if (depth > 1) {
     // the kernel indexes the stack with 32 bits: entry + level * npx < 2^32
     if ((unsigned long long)(depth - 1) * rows.count * od.xw * nf >= (1ull << 32)) return RT_ERR_INVALID_ARG;
-    const size_t need = (size_t)(depth - 1) * rows.count * od.xw * nf * sizeof(StackEnt);
+    // a multi-frame launch sizes the grow-only buffers for RT_MAX_FRAMES frames
+    // at once, so a frame sequence never re-allocates between launches of
+    // different batch sizes (bench warmup shorter than a batch, a last partial batch)
+    const size_t need = (size_t)(depth - 1) * rows.count * od.xw * (nf > 1 ? RT_MAX_FRAMES : 1) * sizeof(StackEnt);
     if (c->cstack_bytes < need) {
       RT_TRY(c, hipStreamSynchronize(c->stream));
       if (c->cstack_buf) (void)hipFree(c->cstack_buf);
@@ -1409,7 +1118,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     gstack = reinterpret_cast<StackEnt *>(c->cstack_buf);
   }
   const int *perm = nullptr;
-  if (c->sched && xcd_per == 0 && kStack != kStackSplit) {
+  if (c->sched) {
     int rc = tile_perm(c, cam, W, H, rows, od, 8 * kWx, 8 * kWy, ntiles, perm);
     if (rc != RT_OK) return rc;
   }
@@ -1435,8 +1144,6 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.counters = c->d_counters;
   ra.ntx = ntx;
   ra.ntiles = (int)ntiles;
-  ra.xcd_per = xcd_per;
-  ra.sa = sa;
   ra.perm = perm;
   // zero the other counter half for the next launch (enqueue's alternation)
   const int next = (int)((c->launches + 1) & 1);
@@ -1451,7 +1158,9 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     // that finds its shard segment full simply continues in its merge_tiles lane
     const size_t npx = (size_t)rows.count * od.xw * nf;
     const size_t cap = std::max<size_t>(64, ((npx / kShards / RT_DEFER_CAP_DIV) + 63) & ~(size_t)63);
-    const size_t need = cap * kShards * sizeof(QRay);
+    const size_t npx_alloc = (size_t)rows.count * od.xw * (nf > 1 ? RT_MAX_FRAMES : 1);
+    const size_t cap_alloc = std::max<size_t>(64, ((npx_alloc / kShards / RT_DEFER_CAP_DIV) + 63) & ~(size_t)63);
+    const size_t need = std::max(cap, cap_alloc) * kShards * sizeof(QRay);
     if (c->dq_bytes < need) {
       RT_TRY(c, hipStreamSynchronize(c->stream));
       if (c->dq_buf) (void)hipFree(c->dq_buf);
@@ -1474,47 +1183,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
 }
 
 template <bool kLds, bool kCull, int kSamples>
-int launch_persist3(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
-                    const OutDesc &od) {
-  const BvhArgs bv = bvh_args(c, cam);
-  const LgArgs lg = lg_args(c);
-  D3 amb{c->amb[0], c->amb[1], c->amb[2]};
-  lds = (lds + 31) & ~(size_t)31;
-  if (bv.ordered) lds += (size_t)kWaves * bv.odepth * 64 * sizeof(int2);  // the kernel places them from bv
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_persist<kLds, kCull, kSamples>, 64 * kWaves, lds) !=
-          hipSuccess ||
-      nb < 1)
-    nb = 1;
-  const int ntx = (od.xw + 7) / 8, nty = (rows.count + 7) / 8;
-  const long long ntiles = (long long)ntx * nty;
-  if (ntiles > (1LL << 31) - 1) return RT_ERR_INVALID_ARG;
-  const long long want = (ntiles + kWaves - 1) / kWaves;
-  const int grid = (int)std::max(1LL, std::min(want, (long long)c->n_cu * nb));
-  const size_t levels = depth > 1 ? (size_t)depth - 1 : 1;
-  const size_t need = (size_t)grid * kWaves * levels * 64 * sizeof(StackEnt) + kTileShards * 64 * sizeof(unsigned);
-  if (c->stack_bytes < need) {
-    RT_TRY(c, hipStreamSynchronize(c->stream));
-    if (c->stack_buf) (void)hipFree(c->stack_buf);
-    c->stack_buf = nullptr;
-    c->stack_bytes = 0;
-    RT_TRY(c, hipMalloc(&c->stack_buf, need));
-    c->stack_bytes = need;
-  }
-  unsigned *ctr = reinterpret_cast<unsigned *>(c->stack_buf);
-  StackEnt *gstack = reinterpret_cast<StackEnt *>(c->stack_buf + kTileShards * 64 * sizeof(unsigned));
-  RT_TRY(c, hipMemsetAsync(ctr, 0, kTileShards * 64 * sizeof(unsigned), c->stream));
-  hipLaunchKernelGGL((render_persist<kLds, kCull, kSamples>), dim3(grid), dim3(64 * kWaves), lds, c->stream,
-                     c->d_geo, c->d_rad, c->d_mat, c->d_lights, c->nsph, c->nlight, amb, cam, W, H, depth, rows, bv,
-                     lg, od, c->d_counters, gstack, ctr, ntx, (int)ntiles);
-  return RT_OK;
-}
-
-template <bool kLds, bool kCull, int kSamples>
 int launch_render4(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
                    const OutDesc &od) {
-  if (c->stack_mode == kStackCompact)
-    return launch_tiles<kLds, kCull, kSamples, kStackCompact>(c, lds, cam, W, H, depth, rows, od);
   if (c->stack_mode == kStackMerge) {
     // merged reflection levels: RGB8 row-compact output, one sample, scene through L2,
     // and only while the wave's LDS (BVH stacks + ray queue) still allows the
@@ -1532,11 +1202,7 @@ int launch_render4(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dept
     }
     return launch_tiles<kLds, kCull, kSamples, kStackGlobal>(c, lds, cam, W, H, depth, rows, od);
   }
-  if (c->stack_mode == kStackGlobal)
-    return launch_tiles<kLds, kCull, kSamples, kStackGlobal>(c, lds, cam, W, H, depth, rows, od);
-  if (c->persist || depth - 1 > kMaxLdsStack) return launch_persist3<kLds, kCull, kSamples>(c, lds, cam, W, H, depth,
-                                                                                           rows, od);
-  return launch_tiles<kLds, kCull, kSamples, kStackLds>(c, lds, cam, W, H, depth, rows, od);
+  return launch_tiles<kLds, kCull, kSamples, kStackGlobal>(c, lds, cam, W, H, depth, rows, od);
 }
 
 int launch_render(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
@@ -1554,140 +1220,6 @@ int launch_render(rt_ctx *c, bool lds_geo, size_t lds, const Cam &cam, int W, in
             : launch_render4<false, false, 1>(c, lds, cam, W, H, depth, rows, od);
 }
 
-size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
-
-// Carve the wavefront scratch for npx pixels at this depth (grow-only).
-int ensure_wf(rt_ctx *c, size_t npx, int depth, size_t seg_cap, WfArgs &a) {
-  const size_t levels = (size_t)(depth > 0 ? depth : 1);
-  const size_t qn = seg_cap * kShards;
-  const size_t b_hit = align_up(qn * sizeof(HitRec)), b_ray = align_up(qn * sizeof(RayRec)),
-               b_cnt = align_up(2 * (levels + 1) * kShards * sizeof(unsigned)),
-               b_term = align_up(npx * sizeof(Term)), b_nlev = align_up(npx),
-               b_stack = align_up((levels - 1) * npx * sizeof(StackEnt));
-  const size_t need = b_hit + b_ray + b_cnt + b_term + b_nlev + b_stack;
-  if (c->wf_bytes < need) {
-    RT_TRY(c, hipStreamSynchronize(c->stream));
-    if (c->wf_buf) (void)hipFree(c->wf_buf);
-    c->wf_buf = nullptr;
-    c->wf_bytes = 0;
-    RT_TRY(c, hipMalloc(&c->wf_buf, need));
-    c->wf_bytes = need;
-  }
-  unsigned char *p = c->wf_buf;
-  a.seg_cap = (int)seg_cap;
-  a.hitq = reinterpret_cast<HitRec *>(p);
-  p += b_hit;
-  a.rayq = reinterpret_cast<RayRec *>(p);
-  p += b_ray;
-  a.hit_cnt = reinterpret_cast<unsigned *>(p);
-  a.ray_cnt = a.hit_cnt + (levels + 1) * kShards;
-  p += b_cnt;
-  a.term = reinterpret_cast<Term *>(p);
-  p += b_term;
-  a.nlev = p;
-  p += b_nlev;
-  a.stack = reinterpret_cast<StackEnt *>(p);
-  RT_TRY(c, hipMemsetAsync(a.hit_cnt, 0, 2 * (levels + 1) * kShards * sizeof(unsigned), c->stream));
-  return RT_OK;
-}
-
-template <bool kLds, bool kCull>
-int launch_wavefront2(rt_ctx *c, WfArgs &a, size_t lds) {
-  const int W = a.W;
-  const size_t npx = (size_t)a.npx;
-  static int blocks_per_cu = 0;  // resident 256-thread workgroups per CU for wf_shade
-  if (blocks_per_cu == 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, wf_shade<kLds, kCull>, 256, lds) != hipSuccess || nb < 1)
-      nb = 2;
-    blocks_per_cu = nb;
-  }
-  // persistent grid: a multiple of kShards, about one resident wave of workgroups
-  const size_t want = (npx + 255) / 256, resident = (size_t)c->n_cu * blocks_per_cu;
-  const size_t per_shard = std::max<size_t>(1, (std::min(want, resident) + kShards - 1) / kShards);
-  const unsigned persist = (unsigned)(per_shard * kShards);
-  if (c->pipeline == 2) {  // hybrid: fused coherent level 0, queues from level 1 on
-    hipLaunchKernelGGL((wf_level0<kLds, kCull>), dim3((W + 7) / 8, (a.rows.count + 7) / 8), dim3(64), lds,
-                       c->stream, a);
-  } else {
-    hipLaunchKernelGGL((wf_primary<kLds, kCull>), dim3((W + 15) / 16, (a.rows.count + 15) / 16), dim3(256), lds,
-                       c->stream, a);
-  }
-  for (int level = 0; level < a.depth; ++level) {
-    if (level > 0) hipLaunchKernelGGL((wf_reflect<kLds, kCull>), dim3(persist), dim3(256), lds, c->stream, a, level);
-    if (level > 0 || c->pipeline != 2)
-      hipLaunchKernelGGL((wf_shade<kLds, kCull>), dim3(persist), dim3(256), lds, c->stream, a, level);
-  }
-  hipLaunchKernelGGL(wf_resolve, dim3((W + 63) / 64, (a.rows.count + 3) / 4), dim3(256), 0, c->stream, a);
-  return RT_OK;
-}
-
-// RT_HIP_PIPELINE=3: level 0 in the megakernel (coherent tiles), reflection
-// levels through the ray queues with wf_bounce, the unwind in wf_resolve.
-template <bool kLds, bool kCull>
-int launch_split(rt_ctx *c, WfArgs &a, const Cam &cam, size_t lds) {
-  SplitArgs sa;
-  sa.rayq = reinterpret_cast<RayRec *>(a.hitq);  // level 1 reads buffer 1
-  sa.ray_cnt = a.ray_cnt;
-  sa.seg_cap = a.seg_cap;
-  sa.term = a.term;
-  sa.nlev = a.nlev;
-  int rc = launch_tiles<kLds, kCull, 1, kStackSplit>(c, lds, cam, a.W, a.H, a.depth, a.rows,
-                                                     OutDesc{a.out, RT_FB_RGB8, 0, 0, a.W}, sa, a.stack);
-  if (rc != RT_OK) return rc;
-  static int blocks_per_cu = 0;
-  size_t blds = ((lds + 31) & ~(size_t)31);
-  if (a.bv.ordered) blds += (size_t)4 * a.bv.odepth * 64 * sizeof(int2);
-  if (blocks_per_cu == 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, wf_bounce<kLds, kCull>, 256, blds) != hipSuccess || nb < 1)
-      nb = 2;
-    blocks_per_cu = nb;
-  }
-  const size_t want = ((size_t)a.npx + 255) / 256, resident = (size_t)c->n_cu * blocks_per_cu;
-  const size_t per_shard = std::max<size_t>(1, (std::min(want, resident) + kShards - 1) / kShards);
-  for (int level = 1; level < a.depth; ++level)
-    hipLaunchKernelGGL((wf_bounce<kLds, kCull>), dim3((unsigned)(per_shard * kShards)), dim3(256), blds, c->stream, a,
-                       level);
-  hipLaunchKernelGGL(wf_resolve, dim3((a.W + 63) / 64, (a.rows.count + 3) / 4), dim3(256), 0, c->stream, a);
-  return RT_OK;
-}
-
-int launch_wavefront(rt_ctx *c, const Cam &cam, int W, int H, int depth, const Rows &r, uint8_t *dst, bool lds_geo,
-                     size_t lds) {
-  WfArgs a{};
-  a.geo = c->d_geo;
-  a.rad = c->d_rad;
-  a.mat = c->d_mat;
-  a.lights = c->d_lights;
-  a.n = c->nsph;
-  a.nl = c->nlight;
-  a.amb = D3{c->amb[0], c->amb[1], c->amb[2]};
-  a.cam = cam;
-  a.W = W;
-  a.H = H;
-  a.depth = depth;
-  a.rows = r;
-  a.npx = r.count * W;
-  a.out = dst;
-  a.counters = c->d_counters;
-  a.bv = bvh_args(c, cam);
-  a.lg = lg_args(c);
-  // queue segment capacity: a segment receives at most one entry per pixel of
-  // the workgroups mapped to it (16x16 workgroups of wf_primary, 8x8 of wf_level0)
-  const size_t wgs16 = (size_t)((W + 15) / 16) * (size_t)((r.count + 15) / 16);
-  const size_t wgs8 = (size_t)((W + 7) / 8) * (size_t)((r.count + 7) / 8);
-  const size_t seg_cap = std::max((wgs16 + kShards - 1) / kShards * 256, (wgs8 + kShards - 1) / kShards * 64);
-  int rc = ensure_wf(c, (size_t)a.npx, depth, seg_cap, a);
-  if (rc != RT_OK) return rc;
-  if (c->pipeline == 3) {
-    if (lds_geo) return c->cull ? launch_split<true, true>(c, a, cam, lds) : launch_split<true, false>(c, a, cam, lds);
-    return c->cull ? launch_split<false, true>(c, a, cam, lds) : launch_split<false, false>(c, a, cam, lds);
-  }
-  if (lds_geo) return c->cull ? launch_wavefront2<true, true>(c, a, lds) : launch_wavefront2<true, false>(c, a, lds);
-  return c->cull ? launch_wavefront2<false, true>(c, a, lds) : launch_wavefront2<false, false>(c, a, lds);
-}
-
 int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_rows *rows, const void *out,
              Rows &r) {
   if (!c || !cam || !out || W <= 0 || H <= 0) return RT_ERR_INVALID_ARG;
@@ -1700,8 +1232,6 @@ int validate(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_
 }
 
 int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows &r, const OutDesc &od) {
-  if (c->nframes > 1 && (c->pipeline != 0 || (c->stack_mode != kStackGlobal && c->stack_mode != kStackMerge)))
-    return RT_ERR_INVALID_ARG;
   RT_TRY(c, hipSetDevice(c->device));
   const int half = (int)(c->launches & 1);
   c->d_counters = c->d_ctr_base + (size_t)half * kShards * kShardStride;
@@ -1721,15 +1251,8 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
       c->err = "light list does not fit in LDS";
       return RT_ERR_INVALID_ARG;
     }
-    // the queue pipelines write row-compact RGB8 of single-sample renders only
-    if (c->pipeline >= 1 && od.fmt == RT_FB_RGB8 && !od.full && od.x0 == 0 && od.xw == W && c->samples == 1) {
-      if ((long long)r.count * W > (1LL << 31) - 1) return RT_ERR_INVALID_ARG;
-      int rc = launch_wavefront(c, cam, W, H, depth, r, static_cast<uint8_t *>(od.ptr), lds_geo, lds);
-      if (rc != RT_OK) return rc;
-    } else {
-      int rc = launch_render(c, lds_geo, lds, cam, W, H, depth, r, od);
-      if (rc != RT_OK) return rc;
-    }
+    int rc = launch_render(c, lds_geo, lds, cam, W, H, depth, r, od);
+    if (rc != RT_OK) return rc;
     RT_TRY(c, hipGetLastError());
   }
   RT_TRY(c, hipEventRecord(c->ev1[slot], c->stream));
@@ -1759,21 +1282,14 @@ int rt_create(int device, rt_ctx **out) {
   if (device < 0 || device >= n) return RT_ERR_INVALID_ARG;
   rt_ctx *c = new rt_ctx();
   c->device = device;
-  if (const char *e = std::getenv("RT_HIP_PIPELINE")) c->pipeline = std::max(0, std::min(3, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_BVH")) c->bvh_on = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_MIN")) c->bvh_min = std::atoi(e);
-  if (const char *e = std::getenv("RT_HIP_LANE_SWEEP")) c->lane_sweep = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_BVH_ALWAYS")) c->bvh_always = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_GROUPS")) c->bvh_groups = std::max(1, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID")) c->lg_on = std::atoi(e) != 0;
-  if (const char *e = std::getenv("RT_HIP_PERSIST")) c->persist = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_LDS_SCENE")) c->lds_scene = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_SCHED")) c->sched = std::atoi(e) != 0;
-  if (const char *e = std::getenv("RT_HIP_STACK")) {
-    const int m = std::max(0, std::min(4, std::atoi(e)));
-    c->stack_mode = m == kStackSplit ? kStackGlobal : m;  // 3 is the split pipeline's own mode
-  }
-  if (const char *e = std::getenv("RT_HIP_XCD_MAP")) c->xcd_map = std::max(0, std::atoi(e));
+  if (const char *e = std::getenv("RT_HIP_STACK")) c->stack_mode = std::atoi(e) == kStackGlobal ? kStackGlobal : kStackMerge;
   if (const char *e = std::getenv("RT_HIP_BVH_ORDERED")) c->bvh_ordered = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH4")) c->bvh_wide = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
@@ -1791,7 +1307,12 @@ int rt_create(int device, rt_ctx **out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
       c->n_cu = prop.multiProcessorCount;
   }
-  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(RT_ERR_HIP);
+  // A blocking stream: it is ordered with the legacy NULL stream (torch's
+  // default stream), so buffers a caller fills there are ready before a
+  // render on the context's own stream reads or overwrites them, and the
+  // caller's later NULL-stream work sees the render's output.
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault) != hipSuccess) return bail(RT_ERR_HIP);
+  if (hipEventCreateWithFlags(&c->switch_ev, hipEventDisableTiming) != hipSuccess) return bail(RT_ERR_HIP);
   c->stream = c->own_stream;
   if (hipMalloc(&c->d_ctr_base, 2 * kShards * kShardStride * sizeof(unsigned long long)) != hipSuccess)
     return bail(RT_ERR_OUT_OF_MEMORY);
@@ -1816,8 +1337,6 @@ void rt_destroy(rt_ctx *c) {
   if (c->d_ctr_base) (void)hipFree(c->d_ctr_base);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->d_tmp) (void)hipFree(c->d_tmp);
-  if (c->wf_buf) (void)hipFree(c->wf_buf);
-  if (c->stack_buf) (void)hipFree(c->stack_buf);
   if (c->cstack_buf) (void)hipFree(c->cstack_buf);
   if (c->dq_buf) (void)hipFree(c->dq_buf);
   if (c->d_perm) (void)hipFree(c->d_perm);
@@ -1826,6 +1345,7 @@ void rt_destroy(rt_ctx *c) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
   }
+  if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -1834,7 +1354,16 @@ const char *rt_last_error(const rt_ctx *c) { return c ? c->err.c_str() : "null c
 
 int rt_set_stream(rt_ctx *c, void *s) {
   if (!c) return RT_ERR_INVALID_ARG;
-  c->stream = s ? (hipStream_t)s : c->own_stream;
+  hipStream_t next = s ? (hipStream_t)s : c->own_stream;
+  if (next != c->stream) {
+    // The context's scratch (reflection stack, deferred queue, counters, tile
+    // order) is shared by every launch: work enqueued on the new stream waits
+    // for everything already enqueued on the old one.
+    RT_TRY(c, hipSetDevice(c->device));
+    RT_TRY(c, hipEventRecord(c->switch_ev, c->stream));
+    RT_TRY(c, hipStreamWaitEvent(next, c->switch_ev, 0));
+    c->stream = next;
+  }
   return RT_OK;
 }
 

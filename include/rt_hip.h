@@ -29,6 +29,13 @@
  * (the reference's CUDA_CHECK -> exit(1), src/main_gpu.cu:27-35, is not kept).
  * Threading: one rt_ctx per device per host thread; distinct contexts are
  * independent and may be used concurrently.
+ * Streams: all device work of a context (renders, rt_unpermute_rows) is
+ * enqueued on ONE stream, the context's current stream, and is ordered only
+ * on it.  The context's own stream (the default) is a BLOCKING stream: it is
+ * ordered with the legacy NULL stream, so device buffers a caller fills or
+ * reads on the NULL stream are ordered with the context's work.  A caller
+ * that uses another stream of its own either passes it to rt_set_stream or
+ * orders it against the context's stream itself.
  */
 #ifndef RT_HIP_H
 #define RT_HIP_H
@@ -139,8 +146,11 @@ int rt_device_count(int *count);
 int rt_create(int device, rt_ctx **out);
 void rt_destroy(rt_ctx *ctx);
 const char *rt_last_error(const rt_ctx *ctx);
-/* Use an external stream (hipStream_t) for all work of this context; NULL
- * restores the context's own stream. */
+/* Use an external stream (hipStream_t) for all later work of this context;
+ * NULL restores the context's own (blocking) stream.  The switch is ordered:
+ * work enqueued after it on the new stream waits for all work already
+ * enqueued on the previous stream (the context's scratch buffers are shared
+ * by every launch). */
 int rt_set_stream(rt_ctx *ctx, void *hip_stream);
 /* Per-wave conservative sphere culling (default on).  Off = every ray tests
  * every sphere (the reference's brute-force sweep, scene.h:47-58).  Output
@@ -173,8 +183,9 @@ int rt_render_stats(rt_ctx *ctx, rt_stats *stats);
  * bytes).  The tiles of all frames share one launch, so the long reflection
  * chains of one frame overlap the others' work instead of each frame ending
  * on its slowest tiles.  Counts as ONE launch for rt_kernel_times; the stats
- * of rt_render_stats are the sums over its frames.  Requires the default
- * render path (no RT_HIP_PIPELINE / RT_HIP_PERSIST / RT_HIP_STACK != 1). */
+ * of rt_render_stats are the sums over its frames.  The first multi-frame
+ * launch sizes the context's scratch for RT_MAX_FRAMES frames of this shape,
+ * so later launches of any frame count do not re-allocate. */
 int rt_render_frames_async(rt_ctx *ctx, const rt_camera *cams, int nframes, int width, int height, int depth,
                            const rt_rows *rows, uint8_t *rgb_out_device, size_t frame_stride);
 

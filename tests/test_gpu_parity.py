@@ -91,6 +91,7 @@ def test_unpermute_kernel(gpu_renderer):
     gpu_renderer.upload(sc)
     R = rt_hip.rows_for_shard(H, band, 0, G).count
     gathered = torch.zeros((G, R, W, 3), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()  # the zero-fill (torch's stream) lands before the renders
     for r in range(G):
         gpu_renderer.render(sc.camera(), W, H, m["depth"], rows=rt_hip.rows_for_shard(H, band, r, G),
                             out=gathered[r], out_on_device=True)
@@ -111,6 +112,7 @@ def test_unpermute_copy_widths(gpu_renderer, W, G, band, off):
     R = -(-(-(-H // band)) // G) * band
     src = torch.randint(0, 256, (off + G * R * W * 3,), dtype=torch.uint8, device="cuda:0")
     dst = torch.zeros((off + H * W * 3,), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()  # both fills (torch's stream) land before the unpermute
     gpu_renderer.unpermute(src.data_ptr() + off, dst.data_ptr() + off, W, H, band, G, R)
     gpu_renderer.stats()
     s = src[off:].cpu().numpy().reshape(G, R, W * 3)
@@ -291,9 +293,8 @@ def test_cull_equals_bruteforce_at_4k(gpu_renderer):
 
 
 @pytest.fixture(params=[{"RT_HIP_BVH_ALWAYS": "1"}, {"RT_HIP_BVH_MIN": "0"}, {"RT_HIP_BVH": "0"},
-                        {"RT_HIP_BVH_MIN": "0", "RT_HIP_LANE_SWEEP": "100000"},
                         {"RT_HIP_BVH_ALWAYS": "1", "RT_HIP_BVH4": "0"}, {"RT_HIP_BVH_LEAF": "4"}],
-                ids=["bvh-always", "bvh-min0", "bvh-off", "lane-sweep", "bvh-always-two-child", "leaf-4"])
+                ids=["bvh-always", "bvh-min0", "bvh-off", "bvh-always-two-child", "leaf-4"])
 def bvh_renderer(request, monkeypatch):
     """A fresh context per BVH policy (the knobs are read at rt_create)."""
     import rt_hip
@@ -346,94 +347,19 @@ def test_bvh_far_from_origin(bvh_renderer):
     assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
 
 
-@pytest.fixture(params=["1", "2", "3"], ids=["queues", "hybrid", "split"])
-def pipeline_renderer(request, monkeypatch):
-    """The queue-based pipelines (RT_HIP_PIPELINE=1: every level through the
-    ray/hit queues; 2: fused coherent level 0, queues from level 1 on; 3: the
-    megakernel's level 0, then wf_bounce per level over the ray queues)."""
-    import rt_hip
-
-    monkeypatch.setenv("RT_HIP_PIPELINE", request.param)
-    r = rt_hip.Renderer(0)
-    yield r
-    r.close()
-
-
-@pytest.mark.parametrize("name", ["complex_97x61_d4", "medium_1280x720_d10", "synth200_1920x1080_d4",
-                                  "synth10k_384x216_d6", "simple_2x2_d10", "simple_1x1_d10"])
-def test_pipelines_golden(pipeline_renderer, name):
-    for cull in (True, False):
-        pipeline_renderer.set_culling(cull)
-        rgb, st, m = _render(pipeline_renderer, name)
-        assert rgb == golden_rgb(name), (cull, diff_summary(rgb, golden_rgb(name)))
-        assert {"primary": st.rays_primary, "shadow": st.rays_shadow, "reflect": st.rays_reflect} == m["rays"]
-
-
-@pytest.mark.parametrize("depth", [0, 1, 2, 5, 64])
-def test_pipelines_depth_edges(pipeline_renderer, depth):
-    import orc
-    import rt_hip
-
-    W, H = 67, 45
-    sc = rt_hip.Scene.load(scene_path("medium"))
-    pipeline_renderer.upload(sc)
-    rgb, st = pipeline_renderer.render(sc.camera(), W, H, depth)
-    ref, counts, _ = orc.OracleScene(scene_path("medium")).render(W, H, depth, threads=4)
-    assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
-    assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
-                                                                   counts["reflect"])
-
-
-@pytest.mark.parametrize("G,band", [(3, 8), (5, 1)])
-def test_pipelines_row_shards(pipeline_renderer, G, band):
-    import rt_hip
-
-    name = "complex_97x61_d4"
-    m = manifest()[name]
-    W, H = m["width"], m["height"]
-    want = np.frombuffer(golden_rgb(name), np.uint8).reshape(H, W, 3)
-    for r in range(G):
-        rows = rt_hip.rows_for_shard(H, band, r, G)
-        rgb, _, _ = _render(pipeline_renderer, name, rows)
-        got = np.frombuffer(rgb, np.uint8).reshape(rows.count, W, 3)
-        for k in range(rows.count):
-            y = (k // band) * band * G + r * band + k % band
-            if y < H:
-                assert np.array_equal(got[k], want[y]), (r, k, y)
-            else:
-                assert not got[k].any()
-
-
-@pytest.mark.parametrize("seed", range(0, 12, 4))
-def test_pipelines_random_scenes(pipeline_renderer, seed):
-    import orc
-    import rt_hip
-
-    text = _random_scene(seed, 60 + 40 * seed)
-    W, H, D = 96, 64, 5
-    sc = rt_hip.Scene.parse(text)
-    pipeline_renderer.upload(sc)
-    ref, _, _ = orc.OracleScene(text=text).render(W, H, D, threads=4)
-    rgb, _ = pipeline_renderer.render(sc.camera(), W, H, D)
-    assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
-
-
-@pytest.fixture(params=[{"RT_HIP_STACK": "0"}, {"RT_HIP_STACK": "2"}, {"RT_HIP_XCD_MAP": "0"},
-                        {"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_LDS_SCENE": "1", "RT_HIP_STACK": "0"},
-                        {"RT_HIP_PERSIST": "1", "RT_HIP_STACK": "0"}, {"RT_HIP_SCHED": "0"},
-                        {"RT_HIP_STACK": "1"}, {"RT_HIP_STACK": "4"}, {"RT_HIP_STACK": "4", "RT_HIP_SCHED": "0"},
-                        {"RT_HIP_STACK": "4", "RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_MERGE_Q": "16"},
-                        {"RT_HIP_DEFER": "0"}, {"RT_HIP_DEFER_LEVEL": "1"}, {"RT_HIP_DEFER_LEVEL": "3"}],
-                ids=["lds-stack", "compact", "no-xcd-map", "lds-scene", "lds-scene-lds-stack", "persist",
-                     "scanline-order", "global-stack", "merge", "merge-scanline", "merge-lds-scene", "merge-queue-16",
-                     "no-defer", "defer-level-1", "defer-level-3"])
+@pytest.fixture(params=[{"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_SCHED": "0"}, {"RT_HIP_STACK": "1"},
+                        {"RT_HIP_STACK": "1", "RT_HIP_SCHED": "0"}, {"RT_HIP_STACK": "4", "RT_HIP_LDS_SCENE": "1"},
+                        {"RT_HIP_MERGE_Q": "16"}, {"RT_HIP_DEFER": "0"}, {"RT_HIP_DEFER_LEVEL": "1"},
+                        {"RT_HIP_DEFER_LEVEL": "3"}],
+                ids=["lds-scene", "scanline-order", "global-stack", "global-stack-scanline", "merge-lds-scene",
+                     "merge-queue-16", "no-defer", "defer-level-1", "defer-level-3"])
 def stack_renderer(request, monkeypatch):
-    """Non-default kernel layouts (RT_HIP_STACK=0: LDS reflection stack, the
-    persistent kernel above depth 5; 2: workgroup-compacted reflection levels;
-    RT_HIP_XCD_MAP=0: workgroup tiles in launch order; RT_HIP_LDS_SCENE=1:
-    scenes that fit staged in LDS with 4-wave workgroups; RT_HIP_PERSIST=1:
-    the persistent tile-queue kernel at every depth; RT_HIP_SCHED=0: tiles
-    launched in scanline order instead of heaviest-predicted first)."""
+    """Non-default kernel layouts (RT_HIP_STACK=1: one tile per wave with the
+    per-pixel global stack instead of merged levels; RT_HIP_LDS_SCENE=1:
+    scenes that fit staged in LDS with 4-wave workgroups; RT_HIP_SCHED=0: tiles
+    launched in scanline order instead of heaviest-predicted first;
+    RT_HIP_MERGE_Q / RT_HIP_DEFER / RT_HIP_DEFER_LEVEL: merge-queue size and
+    the deferred-ray kernel)."""
     import rt_hip
 
     for k, v in request.param.items():

@@ -57,6 +57,7 @@ def test_tiles_f64_match_oracle_framebuffer(gpu_renderer, tw, th):
     sc = rt_hip.Scene.load(scene_path(m["scene"]))
     gpu_renderer.upload(sc)
     fb = torch.full((H * W * 3,), float("nan"), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # the fill (torch's stream) lands before the tiles
     total = 0
     for tx, ty, w, h in _tiles(W, H, tw, th):
         gpu_renderer.render_tile(sc.camera(), W, H, D, tx, ty, w, h, rt_hip.RT_FB_F64X3, fb.data_ptr())
@@ -84,6 +85,7 @@ def test_tiles_f32_and_rgb8(gpu_renderer):
     gpu_renderer.upload(sc)
     f32 = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
     rgb = torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill (torch's stream) lands before the tiles
     for tx, ty, w, h in _tiles(W, H, 200, 150):  # ragged right and top edges
         gpu_renderer.render_tile(sc.camera(), W, H, D, tx, ty, w, h, rt_hip.RT_FB_F32X3, f32.data_ptr())
         gpu_renderer.render_tile(sc.camera(), W, H, D, tx, ty, w, h, rt_hip.RT_FB_RGB8, rgb.data_ptr())
@@ -105,6 +107,7 @@ def test_tile_leaves_other_pixels_alone(gpu_renderer):
     sc = rt_hip.Scene.load(scene_path("complex"))
     gpu_renderer.upload(sc)
     fb = torch.full((H * W * 3,), 7, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill (torch's stream) lands before the tiles
     gpu_renderer.render_tile(sc.camera(), W, H, D, 10, 5, 20, 9, rt_hip.RT_FB_RGB8, fb.data_ptr())
     st = gpu_renderer.stats()
     assert st.rays_primary == 20 * 9
@@ -153,6 +156,7 @@ def test_antialias_tiles_and_deep_depth(aa_renderer):
     sc = rt_hip.Scene.load(scene_path("complex"))
     aa_renderer.upload(sc)
     fb = torch.zeros(H * W * 3, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # the fill (torch's stream) lands before the tiles
     for tx, ty, w, h in _tiles(W, H, 16, 16):
         aa_renderer.render_tile(sc.camera(), W, H, D, tx, ty, w, h, rt_hip.RT_FB_F64X3, fb.data_ptr())
     aa_renderer.stats()

@@ -94,12 +94,13 @@ def test_grid_scenes_vs_oracle(grid_renderer, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pipeline", ["1", "2"])
-def test_grid_in_queue_pipelines(monkeypatch, pipeline):
+@pytest.mark.parametrize("env", [{"RT_HIP_STACK": "1"}, {"RT_HIP_LDS_SCENE": "1"}], ids=["global-stack", "lds-scene"])
+def test_grid_in_other_layouts(monkeypatch, env):
     import orc
     import rt_hip
 
-    monkeypatch.setenv("RT_HIP_PIPELINE", pipeline)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     r = rt_hip.Renderer(0)
     try:
         for name in ("lights_in_cluster", "axis_tangent"):
