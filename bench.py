@@ -186,11 +186,8 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
             rt_frames.run_frames(dist, n, rank, render, shards, gathered, unpermute if rank == 0 else None, F,
                                  render_batch, side)
         else:
-            done, b = 0, 0
-            while done < n:
-                m = min(F, n - done)
+            for b, m in enumerate(rt_frames.batch_sizes(n, F)):
                 render_batch(shards[b & 1][:m])
-                done, b = done + m, b + 1
 
     # at least one full batch: the launch shape of the timed region has run
     # once (scratch sized, tile order built) before the clock starts
@@ -257,7 +254,7 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
             "launches_timed": len(ktimes), "rows_per_rank": R, "tests_exact": tests_exact,
             "tests_cull": tests_cull, "cull": cull, "gather_ms_per_batch": gather_ms,
             "rank_kernel_ms_per_frame": rank_kernel_ms, "world_size_seen": seen_world,
-            "warmup_frames_rendered": max(warmup, F)}
+            "warmup_frames_rendered": max(warmup, F), "launch_frames": rt_frames.batch_sizes(steps, F)}
 
 
 def main():
@@ -312,16 +309,26 @@ def main():
         k_s = m["kernel_ms_per_frame"] * 1e-3  # launch time / frames per launch
         # executed work of one frame (device counters), not the brute-force count
         flops = FLOP_PER_TEST * m["tests_exact"] + FLOP_PER_CULL * m["tests_cull"]
-        achieved = flops / k_s / 1e12
+        test_tflops = flops / k_s / 1e12
         brute = FLOP_PER_TEST * m["spheres"] * m["rank_rays"] / k_s / 1e12
-        traffic, pmc_rec = None, {}
+        pmc_rec = {}
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 pmc_rec = json.load(f).get(args.workload, {})
-            traffic = pmc_rec.get("hbm_bytes_per_frame")
-            if traffic is not None:
-                traffic *= batch  # per launch, like algorithmic_flops_per_launch
+        # the PMC record is per frame of THIS workload at N = 1; it describes the
+        # measured kernel only if it was taken with the same kernel sources
+        src_sha = kernel_source_sha()
+        pmc_ok = bool(pmc_rec) and pmc_rec.get("kernel_src_sha") == src_sha and world == 1
+        fp64_pf = pmc_rec.get("fp64_flops_per_frame") if pmc_ok else None
+        if fp64_pf is not None:
+            achieved, flops_source = fp64_pf / k_s / 1e12, "pmc"
+        else:  # no current PMC record: the exact/cull tests the device counters saw
+            achieved, flops_source = test_tflops, "device work counters (exact + cull tests)"
+        traffic = None
+        if pmc_ok and "fetch_bytes" in pmc_rec and "write_bytes" in pmc_rec:
+            # FETCH_SIZE x 2: MI355X_MICROARCH.md's gfx950 correction; per launch of `batch` frames
+            traffic = int((2 * pmc_rec["fetch_bytes"] + pmc_rec["write_bytes"]) * batch)
         out_bytes = m["W"] * m["rows_per_rank"] * 3
         line = {
             "metric": METRIC,
@@ -346,6 +353,12 @@ def main():
                        # one batch's gather to rank 0 measured alone (overlapped with rendering
                        # in the timed loop)
                        "kernel_ms_per_frame_max_rank": round(m["kernel_ms_per_frame_max_rank"], 4),
+                       # what torch.distributed saw: the process group's size and every rank's
+                       # kernel time per frame of its shard (rank order)
+                       "world_size_seen": m["world_size_seen"],
+                       "rank_kernel_ms_per_frame": m["rank_kernel_ms_per_frame"],
+                       "launch_frames": m["launch_frames"],
+                       "warmup_frames_rendered": m["warmup_frames_rendered"],
                        "kernel_only_mrays_per_s": round(m["frame_rays"] / m["kernel_ms_per_frame_max_rank"] / 1e3,
                                                         1),
                        **({"gather_ms_per_batch": round(m["gather_ms_per_batch"], 4),
@@ -353,34 +366,41 @@ def main():
                           if m.get("gather_ms_per_batch") is not None else {}),
                        "parallelism": f"rows cyclic {BAND}-row bands x {world} GPU, {batch} frames per launch" +
                                       (f" + RCCL gather to rank 0 every {batch} frames" if dist_on else "")},
-            # achieved = SURVEY 8(d)'s algorithmic FLOPs (25 per ray-sphere pair, every
-            # ray against every sphere) over the measured kernel time.  The kernel
-            # prunes pairs exactly (cull bounds, BVH, shadow grids), so this
-            # brute-force-equivalent rate can exceed the VALU peak; the executed
-            # work and the PMC-measured VALU use are listed beside it.  One
-            # launch renders `batch` frames; rates are per launch = per frame.
-            "roofline": {"bound": "valu", "achieved": round(brute, 3), "peak": FP64_VALU_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(brute / FP64_VALU_PEAK_TFLOPS, 4),
+            # achieved = the fp64 FLOPs the render kernels EXECUTE per frame
+            # (rocprofv3 PMC, 64 x (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions,
+            # profiles/pmc_traffic.json taken with these kernel sources) over the
+            # in-stream kernel time per frame: a hardware fraction of the fp64
+            # VALU peak.  One launch renders `batch` frames; rates per launch =
+            # per frame.  SURVEY 8(d)'s brute-force count is algorithmic_equivalent.
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 4),
                          "traffic": traffic,
-                         "kernel": "rtk::render_kernel (fp64 VALU; no dense contraction, so no MFMA roof)",
-                         "per_unit": f"{FLOP_PER_TEST} FLOP per ray-sphere pair x {m['spheres']} spheres x "
-                                     f"{m['rank_rays']} rays per frame x {batch} frames per launch (SURVEY 8(d))",
-                         "algorithmic_flops_per_launch": FLOP_PER_TEST * m["spheres"] * m["rank_rays"] * batch,
-                         "algorithmic_flops_per_frame": FLOP_PER_TEST * m["spheres"] * m["rank_rays"],
+                         "kernel": "rtk::render_kernel + rtk::render_deferred (fp64 VALU; no dense contraction, "
+                                   "so no MFMA roof)",
+                         "flops_source": flops_source,
+                         "fp64_flops_per_frame": fp64_pf,
+                         "fp64_flops_per_launch": fp64_pf * batch if fp64_pf is not None else None,
+                         "per_unit": "executed fp64 FLOPs per frame (PMC) x frames per launch",
+                         "valu_busy": pmc_rec.get("valu_busy") if pmc_ok else None,
+                         "fp64_share_of_valu_insts": pmc_rec.get("fp64_share_of_valu_insts") if pmc_ok else None,
+                         "valu_lane_utilization": pmc_rec.get("valu_lane_utilization") if pmc_ok else None,
+                         "kernel_src_sha": src_sha,
+                         "pmc_matches_kernel_src": pmc_ok,
+                         # PMC counters per FRAME (scripts/make_pmc_json.py); bytes: fetch (raw) / write per frame
+                         "pmc": {k: pmc_rec[k] for k in ("valu_busy", "fp64_flops_per_frame", "fetch_bytes",
+                                                         "write_bytes", "hbm_bytes_per_frame", "source",
+                                                         "kernel_src_sha") if k in pmc_rec},
+                         "algorithmic_equivalent": {
+                             "achieved": round(brute, 3), "frac": round(brute / FP64_VALU_PEAK_TFLOPS, 4),
+                             "per_unit": f"{FLOP_PER_TEST} FLOP per ray-sphere pair x {m['spheres']} spheres x "
+                                         f"{m['rank_rays']} rays per frame (SURVEY 8(d), every ray against every "
+                                         f"sphere; the kernel prunes pairs exactly, so this exceeds the peak)",
+                             "flops_per_frame": FLOP_PER_TEST * m["spheres"] * m["rank_rays"],
+                             "flops_per_launch": FLOP_PER_TEST * m["spheres"] * m["rank_rays"] * batch},
                          "executed": {"exact_tests": m["tests_exact"], "cull_tests": m["tests_cull"],
-                                      "test_tflops": round(achieved, 3),
+                                      "test_tflops": round(test_tflops, 3),
                                       "frac_of_brute_force_tests": round(
                                           m["tests_exact"] / max(1, m["spheres"] * m["rank_rays"]), 6)},
-                         # PMC counters per FRAME (scripts/make_pmc_json.py); bytes: fetch/write per frame
-                         "pmc": {k: pmc_rec[k] for k in ("valu_busy", "fp64_flops_per_frame", "fetch_bytes",
-                                                         "write_bytes", "hbm_bytes_per_frame", "source")
-                                 if k in pmc_rec},
-                         "pmc_fp64_tflops": (round(pmc_rec["fp64_flops_per_frame"] / k_s / 1e12, 3)
-                                             if "fp64_flops_per_frame" in pmc_rec else None),
-                         # the hardware's side of the same roof: the fraction of SIMD cycles
-                         # issuing VALU instructions (rocprofv3 PMC, per frame); `frac`
-                         # above counts brute-force-equivalent work and so exceeds 1
-                         "valu_busy_frac": pmc_rec.get("valu_busy"),
                          "culling": m["cull"],
                          "kernel_ms_mean": round(m["kernel_ms_mean"], 4),
                          "kernel_ms_min": round(m["kernel_ms_min"], 4),

@@ -26,6 +26,17 @@ from __future__ import annotations
 from typing import Callable, Sequence
 
 
+def batch_sizes(steps: int, batch: int) -> list[int]:
+    """`steps` frames in ceil(steps / batch) launches of near-equal size (the
+    larger ones first): 20 frames at batch 16 are two launches of 10, not 16 + 4,
+    whose short tail launch would run at a lower per-frame rate."""
+    if steps <= 0:
+        return []
+    k = -(-steps // batch)
+    q, r = divmod(steps, k)
+    return [q + 1] * r + [q] * (k - r)
+
+
 def run_frames(dist, steps: int, rank: int, render: Callable[[object], None], shards: Sequence,
                gathered: Sequence | None, unpermute: Callable[[Sequence, int], None] | None,
                batch: int = 1, render_batch: Callable[[object], None] | None = None, side=None) -> None:
@@ -33,7 +44,8 @@ def run_frames(dist, steps: int, rank: int, render: Callable[[object], None], sh
     shard buffer); shards[k] is buffer k ([batch, R, W, 3]); on rank 0,
     gathered[k] is the list of per-rank receive tensors ([batch, R, W, 3]) for
     buffer k and unpermute(gathered[k], j) enqueues the reassembly of frame j
-    of that buffer.  `steps` frames are rendered in batches of `batch`;
+    of that buffer.  `steps` frames are rendered in batches of at most `batch`
+    (batch_sizes: near-equal launches);
     render_batch(view), if given, enqueues all frames of a [n, R, W, 3] view
     at once instead of n render() calls."""
     works = [None, None]
@@ -51,11 +63,10 @@ def run_frames(dist, steps: int, rank: int, render: Callable[[object], None], sh
                 side.end(k)
 
     done, b = 0, 0
-    while done < steps:
+    for n in batch_sizes(steps, batch):
         k = b & 1
         if works[k] is not None:
             retire(k)  # batch b-2: its shard buffer is free, rank 0 reassembles it
-        n = min(batch, steps - done)
         if render_batch is not None:
             render_batch(shards[k][:n])
         else:

@@ -9,10 +9,15 @@ multi-frame launches are rt_render_frames_async), and every counter is summed
 over the render dispatches -- each with the render_deferred dispatch that
 follows it (the launch's deep reflection rays) -- and divided by the frames
 they rendered:
-  hbm_bytes_per_frame = (FETCH_SIZE + WRITE_SIZE) * 1024  (rocprofv3 reports KiB;
-      the gfx950 x2 FETCH_SIZE correction of MI355X_MICROARCH.md applies to wide
-      16-B/lane streaming reads, which this kernel does not issue, so the raw
-      value is used; fetch and write are also listed separately)
+  hbm_bytes_per_frame = (2 * FETCH_SIZE + WRITE_SIZE) * 1024  (rocprofv3 reports
+      KiB; FETCH_SIZE doubled: MI355X_MICROARCH.md's gfx950 correction -- it
+      reports half the bytes of 128-B requests; fetch_bytes / write_bytes are
+      the raw per-frame values)
+  fp64_share_of_valu_insts = (ADD + MUL + FMA + TRANS)_F64 / SQ_INSTS_VALU
+  valu_lane_utilization = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)
+      (rocprofv3's VALUUtilization: the mean fraction of a wave's lanes active
+      per VALU cycle)
+  kernel_src_sha = bench.kernel_source_sha() of the tree the passes ran on
   valu_busy = SQ_ACTIVE_INST_VALU * 4 / (SIMDs * GRBM_GUI_ACTIVE / XCDs)
   fp64_flops_per_frame = 64 * (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions
       (an upper bound: it assumes every lane of the wave is active)
@@ -52,7 +57,7 @@ def main():
     if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
         out["fetch_bytes"] = round(vals["FETCH_SIZE"] * 1024)
         out["write_bytes"] = round(vals["WRITE_SIZE"] * 1024)
-        out["hbm_bytes_per_frame"] = out["fetch_bytes"] + out["write_bytes"]
+        out["hbm_bytes_per_frame"] = 2 * out["fetch_bytes"] + out["write_bytes"]
     if "SQ_ACTIVE_INST_VALU" in vals and "GRBM_GUI_ACTIVE" in vals:
         cycles = vals["GRBM_GUI_ACTIVE"] / XCDS
         out["kernel_cycles_per_frame"] = round(cycles)
@@ -61,6 +66,14 @@ def main():
     if None not in f64:
         out["fp64_flops_per_frame"] = round(64 * (f64[0] + f64[1] + 2 * f64[2] + f64[3]))
         out["valu_insts_per_frame"] = round(vals.get("SQ_INSTS_VALU", 0))
+        if vals.get("SQ_INSTS_VALU"):
+            out["fp64_share_of_valu_insts"] = round(sum(f64) / vals["SQ_INSTS_VALU"], 4)
+    if vals.get("SQ_THREAD_CYCLES_VALU") and vals.get("SQ_ACTIVE_INST_VALU"):
+        out["valu_lane_utilization"] = round(vals["SQ_THREAD_CYCLES_VALU"] / (64 * vals["SQ_ACTIVE_INST_VALU"]), 4)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench  # noqa: E402  (the source hash bench.py checks)
+
+    out["kernel_src_sha"] = bench.kernel_source_sha()
     out["source"] = os.path.relpath(base, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     out["counters"] = {k: round(v, 1) for k, v in sorted(vals.items())}
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
