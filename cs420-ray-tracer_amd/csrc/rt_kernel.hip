@@ -27,6 +27,12 @@
 
 #pragma clang fp contract(off)
 
+// RT_ABL=k: ablation builds for cost attribution only (scripts/build_rev.sh
+// ... -DRT_ABL=k); they render WRONG images and are never the product.
+#ifndef RT_ABL
+#define RT_ABL 0
+#endif
+
 #include "rt_device.h"
 #include "rt_sched.h"
 
@@ -168,7 +174,11 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
         const LgArgs &lg0 = kernarg_late<kArgMem, offsetof(RenderArgs, lg)>(lg_arg);
         if (lg0.on && nl > 0) next = lg_range(lg0, 0, hp, mk(slight[0].px, slight[0].py, slight[0].pz), hit);
       }
+#if RT_ABL == 1  // ablation (diagnostic builds only, wrong images): no lights
+      for (int l = 0; l < 0; ++l) {
+#else
       for (int l = 0; l < nl; ++l) {
+#endif
         const LgArgs &lg = kernarg_late<kArgMem, offsetof(RenderArgs, lg)>(lg_arg);
         RT_T0(t_setup);
         // this light's first list id, and the next light's cell range, are
@@ -181,12 +191,28 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
         const D3 to_light = sub(lp, hp);
         const double dist = length(to_light);
         const D3 ldir = normalized(to_light);
-        const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
+        // A lane whose light-grid cell and global list are both empty has no
+        // sphere that can occlude it (shadow_quiet), so its shadow ray is not
+        // even built; the wave builds the rays (the second normalisation is
+        // most of the setup) only when some lane still needs the exact test.
+        const bool need = hit && !(lg.on && shadow_quiet(lg, l, cell, hp, lp, dist));
         RT_ACC(work, 3, t_setup);
         RT_T0(t_sh);
-        const bool occ = lg.on ? shadow_cells(g, n, hit, so, sd, lp, dist, lg, l, cell, id0, work)
-                               : sweep_shadow<kCull>(g, rad, n, hit, so, sd, lp, hi, dist,
-                                                     kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), work);
+        bool occ = false;
+#if RT_ABL == 2  // ablation: no shadow queries
+        if (false) {
+#else
+        if (__ballot(need)) {
+#endif
+#if RT_ABL == 4  // ablation: shadow rays without the second normalisation / offset
+          const D3 so = hp, sd = ldir;
+#else
+          const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
+#endif
+          occ = lg.on ? shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work)
+                      : sweep_shadow<kCull>(g, rad, n, need, so, sd, lp, hi, dist,
+                                            kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), work);
+        }
         RT_ACC(work, 9, t_sh);
         RT_T0(t_shade);
         if (hit && !occ) {
@@ -198,8 +224,13 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
           // pow(+0, y > 0) is +0 exactly (C99 F.10.4.4), so most lanes skip ocml's pow.
           double spec = 0.0;
           int ipow = 0;
+#if RT_ABL == 3  // ablation: no pow
+          spec = rdv;
+          (void)ipow;
+#else
           if (!(rdv == 0.0 && m.shin > 0.0))
             spec = int_pow_ok(rdv, m.shin, ipow) ? int_pow(rdv, ipow) : pow_call(rdv, m.shin);
+#endif
           const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
           col = add(add(specular, diffuse), col);                  // scene.h:117
         }
