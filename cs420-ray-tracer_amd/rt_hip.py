@@ -22,7 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(HERE, "librt_hip.so")
 
 RT_MAX_DEPTH = 64
-ABI_VERSION = 3  # RT_HIP_ABI_VERSION in include/rt_hip.h
+ABI_VERSION = 4  # RT_HIP_ABI_VERSION in include/rt_hip.h
 MAX_FRAMES = 16  # RT_MAX_FRAMES
 
 
@@ -103,6 +103,38 @@ SIGNATURES = {
     "rt_set_antialias": (C.c_int, [_P, C.c_int]),
 }
 
+# include/rt_hip_compat.h: the reference's hybrid interface (src/kernel.cu:185-207),
+# struct layouts of include/gpu_shared.h:84-171
+class rt_float3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class rt_gpu_material(C.Structure):
+    _fields_ = [("albedo", rt_float3), ("metallic", C.c_float), ("shininess", C.c_float)]
+
+
+class rt_gpu_sphere(C.Structure):
+    _fields_ = [("center", rt_float3), ("radius", C.c_float), ("material", rt_gpu_material)]
+
+
+class rt_gpu_light(C.Structure):
+    _fields_ = [("position", rt_float3), ("color", rt_float3), ("intensity", C.c_float)]
+
+
+class rt_gpu_camera(C.Structure):
+    _fields_ = [("origin", rt_float3), ("lower_left", rt_float3), ("horizontal", rt_float3),
+                ("vertical", rt_float3), ("forward", rt_float3), ("right", rt_float3), ("up", rt_float3),
+                ("fov", C.c_float)]
+
+
+COMPAT_SIGNATURES = {
+    "launch_gpu_kernel": (None, [C.POINTER(rt_float3), C.POINTER(rt_gpu_sphere), C.c_int, C.c_int,
+                                 C.POINTER(rt_gpu_camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.c_int, _P]),
+    "upload_lights_and_ambience": (None, [C.POINTER(rt_gpu_light), C.c_int, rt_float3]),
+    "rt_compat_status": (C.c_int, []),
+}
+
 # framebuffer formats of rt_render_tile (rt_hip.h)
 RT_FB_RGB8, RT_FB_F32X3, RT_FB_F64X3 = 0, 1, 2
 
@@ -124,7 +156,7 @@ def lib(path: str = LIB_PATH):
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} missing: run __graft_entry__.build() (no CPU fallback exists)")
         L = C.CDLL(path)
-        for name, (res, args) in SIGNATURES.items():
+        for name, (res, args) in list(SIGNATURES.items()) + list(COMPAT_SIGNATURES.items()):
             if os.environ.get("RT_HIP_LIB") and not hasattr(L, name):
                 continue  # an older diagnostic build (RT_HIP_LIB) may predate an entry point
             fn = getattr(L, name)

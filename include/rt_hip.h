@@ -24,6 +24,8 @@
  *                                      y = tile_y + ..., fb[y*W + x], kernel.cu:99-112), as main_hybrid.cpp:457-470
  *                                      calls it; float3 / Vec3 / RGB8 framebuffers
  *   rt_set_antialias                <- the `-a` flag of ray_gpu, src/main_gpu.cu:249-333, 363-370
+ *   launch_gpu_kernel, upload_lights_and_ambience (include/rt_hip_compat.h)
+ *                                   <- the same symbols of src/kernel.cu:185-207, link-compatible
  *
  * Errors: every call returns an rt_status (0 = ok); the library never exits
  * (the reference's CUDA_CHECK -> exit(1), src/main_gpu.cu:27-35, is not kept).
@@ -47,7 +49,7 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 3
+#define RT_HIP_ABI_VERSION 4  /* 4: the reference hybrid interface (rt_hip_compat.h) */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 

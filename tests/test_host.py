@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     lib = rt_hip.lib()
     for n in names:
         getattr(lib, n)
-    assert lib.rt_abi_version() == rt_hip.ABI_VERSION == 3
+    assert lib.rt_abi_version() == rt_hip.ABI_VERSION == 4
 
 
 def test_error_strings():
@@ -177,3 +177,23 @@ def test_rows_for_shard_covers_every_row_once():
 def test_cli_usage_exits_cleanly():
     r = subprocess.run([os.path.join(PKG, "ray_hip"), "--help"], capture_output=True, text=True)
     assert r.returncode == 2 and "usage" in r.stderr
+
+
+def test_compat_interface_exported_with_reference_layouts():
+    """include/rt_hip_compat.h: launch_gpu_kernel / upload_lights_and_ambience are
+    exported by librt_hip.so, and the structs have the reference's layouts
+    (float3 12 B, GPUMaterial 20 B, GPUSphere 36 B, GPULight 28 B, GPUCamera 88 B,
+    include/gpu_shared.h:84-171)."""
+    import ctypes as C
+
+    text = open(os.path.join(REPO, "include", "rt_hip_compat.h")).read()
+    names = sorted(set(re.findall(r"^\s*(?:void|int)\s+(\w+)\s*\(", text, re.M)))
+    assert names == sorted(rt_hip.COMPAT_SIGNATURES), names
+    out = subprocess.check_output(["nm", "-D", "--defined-only", rt_hip.LIB_PATH], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    assert set(names) <= exported
+    sizes = {rt_hip.rt_float3: 12, rt_hip.rt_gpu_material: 20, rt_hip.rt_gpu_sphere: 36, rt_hip.rt_gpu_light: 28,
+             rt_hip.rt_gpu_camera: 88}
+    for t, n in sizes.items():
+        assert C.sizeof(t) == n, (t.__name__, C.sizeof(t))
+    assert rt_hip.lib().rt_compat_status() == 0
