@@ -10,7 +10,9 @@ mkdir -p "$TMP/csrc" "$TMP/include" "$ROOT/build_variants"
 for f in $(git -C "$ROOT" ls-tree --name-only "$REV" cs420-ray-tracer_amd/csrc/); do
   git -C "$ROOT" show "$REV:$f" > "$TMP/csrc/$(basename "$f")"
 done
-git -C "$ROOT" show "$REV:include/rt_hip.h" > "$TMP/include/rt_hip.h"
+for f in $(git -C "$ROOT" ls-tree --name-only "$REV" include/); do
+  git -C "$ROOT" show "$REV:$f" > "$TMP/include/$(basename "$f")"
+done
 cd "$TMP/csrc"
 SRCS=$(ls rt_kernel.hip rt_bvh.cpp rt_lightgrid.cpp rt_sched.cpp rt_host.cpp rt_compat.cpp 2>/dev/null)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -I../include "$@" -shared \
