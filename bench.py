@@ -8,7 +8,7 @@ bands through librt_hip.so (on torch's current stream, output resident in
 HBM), then the shards are gathered to rank 0 with RCCL (torch.distributed
 "nccl" = RCCL over xGMI) and unpermuted into the final PPM-ordered
 framebuffer on device.  Frames are rendered in batches of
---frames-per-launch (default 16), one rt_render_frames_async launch per batch,
+--frames-per-launch (default 32), one rt_render_frames_async launch per batch,
 so the slowest tiles of one frame overlap the other frames' work; for N > 1
 a batch renders while the previous batch's shards travel to rank 0 in one
 gather.  Every frame is rendered and delivered in full.  Total work per step is fixed
@@ -265,8 +265,8 @@ def main():
     ap.add_argument("--workload", default="synth200_1920x1080_d4", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-also", action="store_true", help="skip the complex.txt north-star line item")
-    ap.add_argument("--frames-per-launch", "--frames-per-gather", dest="frames_per_launch", type=int, default=16,
-                    help="frames rendered by one kernel launch (rt_render_frames_async, 1..16); for N > 1 also "
+    ap.add_argument("--frames-per-launch", "--frames-per-gather", dest="frames_per_launch", type=int, default=32,
+                    help="frames rendered by one kernel launch (rt_render_frames_async, 1..32); for N > 1 also "
                          "the frames per RCCL gather to rank 0 (one collective per batch)")
     ap.add_argument("--force-dist", action="store_true",
                     help="rehearsal: run the N > 1 data path (RCCL process group, shard gather, unpermute) at N = 1")
@@ -292,7 +292,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world)
 
     cull = not args.brute_force
-    batch = max(1, min(16, args.frames_per_launch))  # RT_MAX_FRAMES
+    batch = max(1, min(rt_hip.MAX_FRAMES, args.frames_per_launch))
     m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local, cull, batch, dist_on)
     also = {}
     if not args.no_also and args.workload != "complex_1920x1080_d4":

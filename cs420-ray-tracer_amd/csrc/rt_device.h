@@ -963,28 +963,6 @@ __device__ __forceinline__ int lg_first(const LgArgs &lg, LgRange r) {
   return (r.cb >= 0 && r.ce > r.cb) ? lg.ids[r.cb] : 0;
 }
 
-// True when this lane's shadow query of light l provably finds no occluder
-// without building the ray: its cell list (`cell`, from the direction hp - L)
-// and the light's global list are both empty, and the shadow line the
-// reference would build -- o = hp + ldir*EPS, d = normalized(ldir),
-// scene.h:65-86 -- passes within max_off of L, so shadow_cells would take its
-// list path and test nothing.  The line's distance from L is a few roundings
-// of its coordinates: every term of off = |(L - o) x d|_1 is bounded by
-// ~8 * 2^-53 * (|L - hp|_1 + |hp|_1 + EPS) (to_light, ldir, o and d each round
-// once or twice per component, |d| = 1 +- 2^-51), so reach * 2^-45 <= max_off,
-// reach = dist + |hp|_1 + |L|_1 + 1, covers it with a 2^5 margin; NaN or
-// infinite values fail the comparison and keep the exact test
-// (tests/native/quiet_check.cpp checks the bound on 10^7 random rays).
-__device__ __forceinline__ bool shadow_quiet(const LgArgs &lg, int l, LgRange cell, D3 hp, D3 lp, double dist) {
-  if (cell.cb < 0 || cell.ce != cell.cb) return false;
-  const int cells = 6 * lg.N * lg.N;
-  const int32_t *st = lg.start + (size_t)l * (size_t)(cells + 2);
-  if (st[cells + 1] != st[cells]) return false;  // spheres at the light: always tested
-  const double reach = dist + (__builtin_fabs(hp.x) + __builtin_fabs(hp.y) + __builtin_fabs(hp.z)) +
-                       (__builtin_fabs(lp.x) + __builtin_fabs(lp.y) + __builtin_fabs(lp.z)) + 1.0;
-  return reach * 0x1p-45 <= lg.max_off;
-}
-
 __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d, D3 lp,
                                              double dist, const LgArgs &lg, int l, LgRange cell, int id0,
                                              Work &work) {

@@ -96,6 +96,8 @@ struct RenderArgs {
   int merge_q;                    // kStackMerge: LDS ray-queue entries per wave (16..64)
   int defer_level;                // kStackMerge: rays of this reflection level and deeper are deferred
 };
+// the whole struct is the kernel's argument block (kernarg segment, at most 4 KiB)
+static_assert(sizeof(RenderArgs) <= 4096, "RenderArgs exceeds the kernel-argument segment");
 
 // Member `x` (at offset kOff of RenderArgs) re-read from the kernarg segment
 // here.  Kernel arguments are otherwise loaded into SGPRs at entry and live
@@ -191,11 +193,7 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
         const D3 to_light = sub(lp, hp);
         const double dist = length(to_light);
         const D3 ldir = normalized(to_light);
-        // A lane whose light-grid cell and global list are both empty has no
-        // sphere that can occlude it (shadow_quiet), so its shadow ray is not
-        // even built; the wave builds the rays (the second normalisation is
-        // most of the setup) only when some lane still needs the exact test.
-        const bool need = hit && !(lg.on && shadow_quiet(lg, l, cell, hp, lp, dist));
+        const bool need = hit;
         RT_ACC(work, 3, t_setup);
         RT_T0(t_sh);
         bool occ = false;
@@ -1134,10 +1132,9 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   if (depth > 1) {
     // the kernel indexes the stack with 32 bits: entry + level * npx < 2^32
     if ((unsigned long long)(depth - 1) * rows.count * od.xw * nf >= (1ull << 32)) return RT_ERR_INVALID_ARG;
-    // a multi-frame launch sizes the grow-only buffers for RT_MAX_FRAMES frames
-    // at once, so a frame sequence never re-allocates between launches of
-    // different batch sizes (bench warmup shorter than a batch, a last partial batch)
-    const size_t need = (size_t)(depth - 1) * rows.count * od.xw * (nf > 1 ? RT_MAX_FRAMES : 1) * sizeof(StackEnt);
+    // grow-only: sized for this launch's frames; a later launch of as many
+    // frames or fewer (a last partial batch) reuses it
+    const size_t need = (size_t)(depth - 1) * rows.count * od.xw * nf * sizeof(StackEnt);
     if (c->cstack_bytes < need) {
       RT_TRY(c, hipStreamSynchronize(c->stream));
       if (c->cstack_buf) (void)hipFree(c->cstack_buf);
@@ -1189,9 +1186,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     // that finds its shard segment full simply continues in its merge_tiles lane
     const size_t npx = (size_t)rows.count * od.xw * nf;
     const size_t cap = std::max<size_t>(64, ((npx / kShards / RT_DEFER_CAP_DIV) + 63) & ~(size_t)63);
-    const size_t npx_alloc = (size_t)rows.count * od.xw * (nf > 1 ? RT_MAX_FRAMES : 1);
-    const size_t cap_alloc = std::max<size_t>(64, ((npx_alloc / kShards / RT_DEFER_CAP_DIV) + 63) & ~(size_t)63);
-    const size_t need = std::max(cap, cap_alloc) * kShards * sizeof(QRay);
+    const size_t need = cap * kShards * sizeof(QRay);
     if (c->dq_bytes < need) {
       RT_TRY(c, hipStreamSynchronize(c->stream));
       if (c->dq_buf) (void)hipFree(c->dq_buf);

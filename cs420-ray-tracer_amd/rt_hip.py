@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(HERE, "librt_hip.so")
 
 RT_MAX_DEPTH = 64
 ABI_VERSION = 4  # RT_HIP_ABI_VERSION in include/rt_hip.h
-MAX_FRAMES = 16  # RT_MAX_FRAMES
+MAX_FRAMES = 32  # RT_MAX_FRAMES
 
 
 class RtError(RuntimeError):

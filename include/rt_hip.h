@@ -176,7 +176,7 @@ int rt_render_async(rt_ctx *ctx, const rt_camera *cam, int width, int height, in
 int rt_render_stats(rt_ctx *ctx, rt_stats *stats);
 
 /* Most frames one rt_render_frames_async launch renders. */
-#define RT_MAX_FRAMES 16
+#define RT_MAX_FRAMES 32
 /* Asynchronous render of `nframes` frames (1..RT_MAX_FRAMES) of the uploaded
  * scene in ONE kernel launch, frame f seen through cams[f]: a frame sequence
  * of the per-frame pixel loop src/main.cpp:146-157, each frame exactly what
@@ -185,9 +185,10 @@ int rt_render_stats(rt_ctx *ctx, rt_stats *stats);
  * bytes).  The tiles of all frames share one launch, so the long reflection
  * chains of one frame overlap the others' work instead of each frame ending
  * on its slowest tiles.  Counts as ONE launch for rt_kernel_times; the stats
- * of rt_render_stats are the sums over its frames.  The first multi-frame
- * launch sizes the context's scratch for RT_MAX_FRAMES frames of this shape,
- * so later launches of any frame count do not re-allocate. */
+ * of rt_render_stats are the sums over its frames.  The context's scratch
+ * (reflection stack, deferred-ray queue) grows to the largest launch seen, so
+ * launches of as many frames or fewer do not re-allocate: render the largest
+ * batch once before timing a sequence. */
 int rt_render_frames_async(rt_ctx *ctx, const rt_camera *cams, int nframes, int width, int height, int depth,
                            const rt_rows *rows, uint8_t *rgb_out_device, size_t frame_stride);
 

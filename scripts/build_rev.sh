@@ -14,7 +14,7 @@ for f in $(git -C "$ROOT" ls-tree --name-only "$REV" include/); do
   git -C "$ROOT" show "$REV:$f" > "$TMP/include/$(basename "$f")"
 done
 cd "$TMP/csrc"
-SRCS=$(ls rt_kernel.hip rt_bvh.cpp rt_lightgrid.cpp rt_sched.cpp rt_host.cpp rt_compat.cpp 2>/dev/null)
+SRCS=$(ls rt_kernel.hip rt_bvh.cpp rt_lightgrid.cpp rt_sched.cpp rt_host.cpp rt_compat.cpp 2>/dev/null || true)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -I../include "$@" -shared \
   -o "$ROOT/build_variants/librt_hip_$NAME.so" $SRCS
 rm -rf "$TMP"

@@ -52,7 +52,7 @@ def _moved(cam, k):
     return c
 
 
-@pytest.mark.parametrize("name,F", [("complex_97x61_d4", 2), ("complex_97x61_d4", 16), ("medium_1280x720_d10", 3),
+@pytest.mark.parametrize("name,F", [("complex_97x61_d4", 2), ("complex_97x61_d4", 32), ("medium_1280x720_d10", 3),
                                     ("synth200_1920x1080_d4", 8), ("synth10k_384x216_d6", 5)])
 def test_frames_equal_golden(gpu_renderer, name, F):
     sc, m = _load(gpu_renderer, name)
@@ -145,9 +145,10 @@ def test_frames_argument_errors(gpu_renderer):
 
     sc, m = _load(gpu_renderer, "complex_97x61_d4")
     W, H, D = m["width"], m["height"], m["depth"]
-    buf = torch.empty((17 * H * W * 3,), dtype=torch.uint8, device="cuda:0")
+    over = rt_hip.MAX_FRAMES + 1
+    buf = torch.empty((over * H * W * 3,), dtype=torch.uint8, device="cuda:0")
     cam = sc.camera()
-    for cams, stride in (([], H * W * 3), ([cam] * 17, H * W * 3), ([cam] * 2, H * W * 3 - 1)):
+    for cams, stride in (([], H * W * 3), ([cam] * over, H * W * 3), ([cam] * 2, H * W * 3 - 1)):
         with pytest.raises(rt_hip.RtError):
             gpu_renderer.render_frames_async(cams, W, H, D, None, buf.data_ptr(), stride)
     # one frame ignores the stride, like rt_render_async

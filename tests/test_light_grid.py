@@ -33,20 +33,6 @@ def test_grid_lists_are_conservative(tmp_path):
     assert words[-1] == "0"
 
 
-def test_shadow_quiet_bound(tmp_path):
-    """rtk::shadow_quiet skips building a shadow ray when its cell is empty and
-    reach * 2^-45 <= max_off; that bound must cover the built line's distance
-    from the light (tests/native/quiet_check.cpp, 4M random rays, 10^-3..10^4
-    scales, up to 10^6 from the origin)."""
-    exe = tmp_path / "quiet_check"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe),
-                    os.path.join(REPO, "tests", "native", "quiet_check.cpp")], check=True)
-    out = subprocess.run([str(exe), "4000000"], capture_output=True, text=True, timeout=120)
-    assert out.returncode == 0, out.stdout + out.stderr
-    words = out.stdout.split()
-    assert words[1] == "4000000" and float(words[3]) < 0.1 and words[-1] == "0", out.stdout
-
-
 GRID_SCENES = {
     # the light sits exactly on a sphere's surface and inside another one
     "light_on_surface": "sphere 0 0 -5 1 0.8 0.2 0.2 0.3 1 10\nsphere 0 5 -5 2 0.2 0.8 0.2 0 1 10\n"
