@@ -68,6 +68,7 @@ def lib():
         L.orc_render_aa.argtypes = [C.POINTER(orc_scene), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                     C.c_void_p, C.POINTER(orc_counts), C.c_int]
         L.orc_quantize.argtypes = [C.c_double]
+        L.orc_tile_complexity.argtypes = [C.POINTER(orc_scene)] + [C.c_int] * 6
         _lib = L
     return _lib
 
@@ -126,6 +127,19 @@ class OracleScene:
             raise ValueError("orc_render_aa rejected its arguments")
         out = (bytes(rgb), cnt.as_dict(), dt)
         return out + (list(fb),) if want_fb else out
+
+
+def hybrid_tiles(scene: "OracleScene", W: int, H: int, tile: int, threshold: int):
+    """The hybrid driver's tile split (src/main_hybrid.cpp:351-395 / :487-527):
+    tiles in scanline order of tile rows, (x0, y0, x1, y1, complexity, to_cpu)
+    with to_cpu = complexity > threshold."""
+    out = []
+    for y in range(0, H, tile):
+        for x in range(0, W, tile):
+            x1, y1 = min(x + tile, W), min(y + tile, H)
+            c = lib().orc_tile_complexity(C.byref(scene.s), x, y, x1, y1, W, H)
+            out.append((x, y, x1, y1, c, c > threshold))
+    return out
 
 
 def intersect(center, radius, origin, direction):

@@ -168,6 +168,28 @@ static orc_ray get_ray(const orc_camera *c, double u, double v) {
     return make_ray(c->position, vnorm(dir)); /* normalized, then normalized again by Ray() */
 }
 
+/* estimate_tile_complexity, src/main_hybrid.cpp:323-347: five camera rays at
+ * the tile's corners and centre, u = x / img_w and v = y / img_h (the
+ * reference divides by float(IMG_WIDTH) / float(IMG_HEIGHT), not W - 1), the
+ * centre weighted 2, summed over every sphere whose intersect() reports a hit
+ * (sphere.h:26-59; t itself is unused).  Tile = [x0, x1) x [y0, y1). */
+int orc_tile_complexity(const orc_scene *s, int x0, int y0, int x1, int y1, int img_w, int img_h) {
+    orc_camera cam;
+    orc_make_camera(s, &cam);
+    const int sx[5] = {x0, x1 - 1, (x0 + x1) / 2, x0, x1 - 1};
+    const int sy[5] = {y0, y0, (y0 + y1) / 2, y1 - 1, y1 - 1};
+    const int w[5] = {1, 1, 2, 1, 1};
+    int cplx = 0;
+    for (int i = 0; i < 5; i++) {
+        orc_ray r = get_ray(&cam, (double)sx[i] / (float)img_w, (double)sy[i] / (float)img_h);
+        for (int k = 0; k < s->num_spheres; k++) {
+            double t;
+            if (orc_intersect(&s->spheres[k], r.o, r.d, &t)) cplx += w[i];
+        }
+    }
+    return cplx;
+}
+
 int orc_quantize(double c) {
     double m = 255.99 * min1(c); /* main.cpp:85 */
     if (m <= -2147483648.0) return -2147483647 - 1;

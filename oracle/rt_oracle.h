@@ -97,6 +97,9 @@ int orc_render(const orc_scene *s, int W, int H, int depth,
 int orc_render_aa(const orc_scene *s, int W, int H, int depth, int samples, uint8_t *rgb, double *fb,
                   orc_counts *counts, int nthreads);
 
+/* estimate_tile_complexity of the hybrid driver, src/main_hybrid.cpp:323-347. */
+int orc_tile_complexity(const orc_scene *s, int x0, int y0, int x1, int y1, int img_w, int img_h);
+
 /* Quantiser of main.cpp:85-87: int(255.99 * std::min(1.0, c)). */
 int orc_quantize(double c);
 

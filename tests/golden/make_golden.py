@@ -40,6 +40,10 @@ CONFIGS = [
     ("complex_97x61_d4", "complex", 97, 61, 4, "ref_render"),          # ragged small case
     ("simple_2x2_d10", "simple", 2, 2, 10, "ref_render"),              # tiny case
     ("simple_1x1_d10", "simple", 1, 1, 10, "ref_render"),              # W-1 = 0: NaN camera ray
+    # the hybrid driver's fixed size (src/main_hybrid.cpp:41-42, max_depth 3 at :736)
+    ("simple_1080x720_d3", "simple", 1080, 720, 3, "ref_render"),
+    ("medium_1080x720_d3", "medium", 1080, 720, 3, "ref_render"),
+    ("complex_1080x720_d3", "complex", 1080, 720, 3, "ref_render"),
 ]
 
 
