@@ -1,0 +1,37 @@
+"""Host ASan + UBSan build: the C++ host side of librt_hip.so --
+scene parser and PPM writer (rt_host.cpp), BVH builders (rt_bvh.cpp), light
+direction grids (rt_lightgrid.cpp), tile scheduler (rt_sched.cpp) -- plus
+ray_hybrid's CPU tile worker (rt_cpu.cpp) and the oracle (oracle/rt_oracle.c),
+compiled with -fsanitize=address,undefined -fno-sanitize-recover=all and
+driven by tests/native/host_sanitize.cpp over the committed scenes and random,
+hostile inputs (NaN/inf tokens, malformed records, degenerate sphere sets,
+lights on sphere surfaces, random shard views).  These builders decide which
+spheres the GPU may skip and which memory it reads, so a memory bug there is
+a parity bug.  No GPU is involved."""
+import os
+import subprocess
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "cs420-ray-tracer_amd", "csrc")
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-g", "-O1",
+       "-ffp-contract=off"]
+
+
+def test_host_builders_under_asan_ubsan(tmp_path):
+    orc_o = tmp_path / "rt_oracle.o"
+    subprocess.run(["gcc", *SAN, "-std=c11", "-c", "-o", str(orc_o), os.path.join(REPO, "oracle", "rt_oracle.c")],
+                   check=True)
+    exe = tmp_path / "host_sanitize"
+    srcs = [os.path.join(CSRC, f) for f in ("rt_host.cpp", "rt_bvh.cpp", "rt_lightgrid.cpp", "rt_sched.cpp",
+                                            "rt_cpu.cpp")]
+    subprocess.run(["g++", *SAN, "-std=c++17", "-I", CSRC, "-I", os.path.join(REPO, "include"), "-I",
+                    os.path.join(REPO, "oracle"), "-o", str(exe), os.path.join(REPO, "tests", "native",
+                                                                               "host_sanitize.cpp"),
+                    *srcs, str(orc_o), "-lm"], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    env.pop("LD_PRELOAD", None)
+    out = subprocess.run([str(exe), os.path.join(REPO, "cs420-ray-tracer_amd", "scenes"), str(tmp_path), "400"],
+                         capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
+    assert "sanitized 400 iterations ok" in out.stdout
