@@ -107,7 +107,9 @@ int render_single(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::
 // G devices in one process: cyclic 8-row bands, ncclGather to device 0, unpermute.
 int render_multi(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::vector<uint8_t> &img, Result &res) {
   const int G = o.gpus, W = o.width, H = o.height, band = 8;
-  const int nb = (H + band - 1) / band, R = ((nb + G - 1) / G) * band;
+  rt_rows layout;
+  CK(rt_rows_for_shard(H, band, 0, G, &layout));  // the layout bench.py's ranks use
+  const int R = layout.count;
   const size_t shard_bytes = (size_t)R * W * 3;
   std::vector<rt_ctx *> ctx(G, nullptr);
   std::vector<hipStream_t> streams(G);
@@ -136,7 +138,8 @@ int render_multi(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::v
     }
     auto t0 = std::chrono::high_resolution_clock::now();
     for (int g = 0; g < G; g++) {
-      rt_rows rows{band, g, G, R};
+      rt_rows rows;
+      CK(rt_rows_for_shard(H, band, g, G, &rows));
       CK(rt_render_async(ctx[g], &cam, W, H, o.depth, &rows, shard[g]));
     }
     NK(ncclGroupStart());

@@ -119,6 +119,15 @@ extern "C" {
 
 int rt_abi_version(void) { return RT_HIP_ABI_VERSION; }
 
+int rt_rows_for_shard(int height, int band, int rank, int num_shards, rt_rows *out) {
+  if (!out || height < 0 || band < 1 || num_shards < 1 || rank < 0 || rank >= num_shards) return RT_ERR_INVALID_ARG;
+  const long long nb = ((long long)height + band - 1) / band;          // bands of the image
+  const long long per = (nb + num_shards - 1) / num_shards;           // bands per rank
+  if (per * band > 0x7fffffffLL) return RT_ERR_INVALID_ARG;
+  *out = rt_rows{band, rank, num_shards, (int32_t)(per * band)};
+  return RT_OK;
+}
+
 const char *rt_error_string(int status) {
   switch (status) {
     case RT_OK: return "ok";

@@ -22,7 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(HERE, "librt_hip.so")
 
 RT_MAX_DEPTH = 64
-ABI_VERSION = 4  # RT_HIP_ABI_VERSION in include/rt_hip.h
+ABI_VERSION = 5  # RT_HIP_ABI_VERSION in include/rt_hip.h
 MAX_FRAMES = 32  # RT_MAX_FRAMES
 
 
@@ -83,6 +83,7 @@ SIGNATURES = {
     "rt_write_ppm": (C.c_int, [C.c_char_p, _P, C.c_int, C.c_int, C.c_int]),
     "rt_error_string": (C.c_char_p, [C.c_int]),
     "rt_abi_version": (C.c_int, []),
+    "rt_rows_for_shard": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(rt_rows)]),
     "rt_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "rt_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "rt_destroy": (None, [_P]),
@@ -243,10 +244,12 @@ class Scene:
 
 
 def rows_for_shard(height: int, band: int, rank: int, world: int) -> rt_rows:
-    """Cyclic bands of `band` rows: rank r renders bands r, r+G, r+2G, ..."""
-    nb = -(-height // band)
-    per = -(-nb // world)
-    return rt_rows(band, rank, world, per * band)
+    """Cyclic bands of `band` rows: rank r renders bands r, r+G, r+2G, ...
+    (rt_rows_for_shard: the one layout ray_hip --gpus and bench.py share)."""
+    rows = rt_rows()
+    _check(lib().rt_rows_for_shard(height, band, rank, world, C.byref(rows)),
+           f"rt_rows_for_shard({height}, {band}, {rank}, {world})")
+    return rows
 
 
 class Renderer:

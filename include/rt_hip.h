@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 4  /* 4: the reference hybrid interface (rt_hip_compat.h) */
+#define RT_HIP_ABI_VERSION 5  /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -116,6 +116,13 @@ typedef struct rt_rows {
     int32_t stride;
     int32_t count;
 } rt_rows;
+
+/* The multi-GPU row layout every driver uses -- ray_hip --gpus G,
+ * bench.py's torch.distributed ranks, rt_unpermute_rows: rank `rank` of
+ * `num_shards` renders the cyclic bands of `band` rows rank, rank + G, ...;
+ * every rank gets the same row count ceil(ceil(H / band) / G) * band (rows past
+ * the image are padding).  Fails for band < 1, G < 1, rank outside [0, G). */
+int rt_rows_for_shard(int height, int band, int rank, int num_shards, rt_rows *out);
 
 /* Ray counts: primary = pixels traced; shadow = lights x shaded
  * hits (counted even when the GPU exits early); reflect = reflection rays

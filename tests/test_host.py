@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     lib = rt_hip.lib()
     for n in names:
         getattr(lib, n)
-    assert lib.rt_abi_version() == rt_hip.ABI_VERSION == 4
+    assert lib.rt_abi_version() == rt_hip.ABI_VERSION == 5
 
 
 def test_error_strings():
@@ -172,6 +172,14 @@ def test_rows_for_shard_covers_every_row_once():
                         if y < H:
                             seen.append(y)
                 assert sorted(seen) == list(range(H))
+                # rt_rows_for_shard: one row count for every rank (the gather's equal shards)
+                assert len({rt_hip.rows_for_shard(H, band, r, G).count for r in range(G)}) == 1
+
+
+def test_rows_for_shard_rejects_bad_layouts():
+    for args in ((1080, 0, 0, 1), (1080, 8, 2, 2), (1080, 8, -1, 2), (1080, 8, 0, 0), (-1, 8, 0, 1)):
+        with pytest.raises(rt_hip.RtError):
+            rt_hip.rows_for_shard(*args)
 
 
 def test_cli_usage_exits_cleanly():
