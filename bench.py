@@ -115,12 +115,15 @@ def cpu_baseline(scene_file: str, W: int, H: int, D: int, rays_per_frame: int, t
             "sample": f"{what}; {W}x{H} d{D}, {rays} rays in {secs:.3f} s on {threads} thread(s) of {cpu_model()}"}
 
 
-def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, cull=True, batch=4, dist_on=None):
+def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, cull=True, batch=4, dist_on=None,
+            depth=None):
     import rt_frames
 
     if dist_on is None:
         dist_on = world > 1
     scene_name, W, H, D = WORKLOADS[workload]
+    if depth is not None:
+        D = depth
     scene_file = os.path.join(PKG, "scenes", scene_name + ".txt")
     scene = rt_hip.Scene.load(scene_file)
     cam = scene.camera()
@@ -270,6 +273,8 @@ def main():
                          "the frames per RCCL gather to rank 0 (one collective per batch)")
     ap.add_argument("--force-dist", action="store_true",
                     help="rehearsal: run the N > 1 data path (RCCL process group, shard gather, unpermute) at N = 1")
+    ap.add_argument("--depth", type=int, default=None,
+                    help="diagnostic: override the workload's depth (the line then no longer measures the metric)")
     ap.add_argument("--brute-force", action="store_true",
                     help="disable the exact per-wave sphere culling: every ray tests every sphere")
     args = ap.parse_args()
@@ -293,7 +298,8 @@ def main():
 
     cull = not args.brute_force
     batch = max(1, min(rt_hip.MAX_FRAMES, args.frames_per_launch))
-    m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local, cull, batch, dist_on)
+    m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local, cull, batch, dist_on,
+                args.depth)
     also = {}
     if not args.no_also and args.workload != "complex_1920x1080_d4":
         a = measure(rt_hip, torch, dist, "complex_1920x1080_d4", max(args.steps // 2, 5), 2, world, rank, local,
@@ -344,7 +350,8 @@ def main():
             "dtype": "f64",
             "data": "synthetic: scenes/%s.txt (splitmix64 seed 420, SURVEY 8(d) generator) resident in HBM"
                     % m["scene"] if m["scene"].startswith("synth") else "scenes/%s.txt" % m["scene"],
-            "config": {"workload": args.workload, "scene": m["scene"], "width": m["W"], "height": m["H"],
+            "config": {"workload": args.workload + (f"_depth{args.depth}_override" if args.depth is not None else ""),
+                       "scene": m["scene"], "width": m["W"], "height": m["H"],
                        "depth": m["D"], "spheres": m["spheres"], "lights": m["lights"],
                        "rays_per_frame": m["frame_rays"],
                        **({"assembled_frame_equals_single_gpu_render": m["assembled_ok"]} if dist_on else {}),

@@ -71,6 +71,7 @@ __device__ __forceinline__ double length(D3 a) { return __builtin_sqrt(a.x * a.x
 #ifndef RT_FASTDIV
 #define RT_FASTDIV 0
 #endif
+
 __device__ __forceinline__ bool div_num_ok(double x) {
   const double m = __builtin_fabs(x);
   return x == 0.0 || (m >= 0x1p-600 && m <= 0x1p400);
@@ -319,8 +320,9 @@ __device__ __forceinline__ unsigned long long candidates(const SphGeo *__restric
 
 // Scene::find_intersection (scene.h:41-61): all candidate spheres in file
 // order, strict '<' (so ties keep the lowest index), t starts at 1e20.
-// Work counters (wave-uniform): n_exact = exact ray-sphere tests executed for
-// live lanes; n_cull = sphere-vs-bound tests (one per sphere per wave sweep).
+// Work counters, per lane (summed over the wave when flushed): exact = exact
+// ray-sphere tests this lane executed; cull = conservative tests it evaluated
+// (one sphere vs the wave's bound in a cull sweep, one box in a BVH walk).
 struct Work {
   unsigned long long exact = 0, cull = 0;
 #ifdef RT_STAMPS
@@ -752,7 +754,6 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
     todo &= ~grp;
     ++groups;
     const bool gact = (grp >> lane) & 1ull;
-    const unsigned live = (unsigned)__popcll(grp);
     if (kCull) {
       Bound B;
       RT_T0(tb);
@@ -765,15 +766,15 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
         RT_T0(tc);
         unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
         RT_ACC(work, 1, tc);
-        work.cull += (unsigned)(n - base < 64 ? n - base : 64);
+        work.cull += base + lane < n ? 1u : 0u;  // this lane's keep() test
         seen += __popcll(mask);
         if (have_bvh && seen > bv.min_cands) {  // loose bound: this group walks the BVH
           need = need || gact;
           break;
         }
         RT_T0(tt);
-        work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
         if (gact) {
+          work.exact += (unsigned)__popcll(mask);
           while (mask) {
             const int i = base + __builtin_ctzll(mask);
             mask &= mask - 1;
@@ -787,8 +788,8 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
     } else {
       for (int base = 0; base < n; base += 64) {
         unsigned long long mask = candidates<false>(g, rad, n, base, Bound{});
-        work.exact += (unsigned long long)live * (unsigned)__popcll(mask);
         if (gact) {
+          work.exact += (unsigned)__popcll(mask);
           while (mask) {
             const int i = base + __builtin_ctzll(mask);
             mask &= mask - 1;
@@ -882,7 +883,7 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
       unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
       RT_ACC(work, 1, tc);
       if (kCull) {
-        work.cull += (unsigned)(n - base < 64 ? n - base : 64);
+        work.cull += base + lane < n ? 1u : 0u;  // this lane's keep() test
         seen += __popcll(mask);
         if (have_bvh && seen > bv.min_cands) {
           need = need || (gact && !occ);
@@ -893,9 +894,11 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
       while (mask) {
         const int i = base + __builtin_ctzll(mask);
         mask &= mask - 1;
-        work.exact += (unsigned)__popcll(live);
         RT_CNT(work, iters, 1);
-        if (gact && !occ) test(i);
+        if (gact && !occ) {
+          work.exact += 1;
+          test(i);
+        }
         live = __ballot(gact && !occ);
         if (live == 0) break;
       }
@@ -963,9 +966,10 @@ __device__ __forceinline__ int lg_first(const LgArgs &lg, LgRange r) {
   return (r.cb >= 0 && r.ce > r.cb) ? lg.ids[r.cb] : 0;
 }
 
+// `pre` >= 0: the sphere the shaded point lies on (see below).
 __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d, D3 lp,
                                              double dist, const LgArgs &lg, int l, LgRange cell, int id0,
-                                             Work &work) {
+                                             Work &work, int pre = -1) {
   if (__ballot(act) == 0) return false;
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
@@ -975,7 +979,11 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
   bool occ = false;
   auto test = [&](int i) {
     double num;
+    #if RT_ABL == 8  // ablation (wrong images): the shadow tests read one fixed sphere (no gathers)
+    const int r = fast ? intersect_num(g[0], o, d, a4, num) : 2;
+#else
     const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+#endif
     if (r == 1) {
       if (num < qlo) occ = true;
       else if (!(num > qhi)) {
@@ -987,16 +995,54 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
       occ = intersect(g[i], o, d, a4, a2, t) && t < kInf && t < dist;
     }
   };
-  if (act) {
+  // The lane's own sphere `pre` (the shaded point lies on it) is on almost
+  // every list, and its test is decided by the first steps of the
+  // reference's arithmetic (sphere.h:29-35, the same roundings as
+  // intersect_num), without the square root:
+  //  * c < 0, the origin inside the sphere: disc > 0 and the exit root t2 is
+  //    in [0, 2.42 |r|] (|oc| <= |r|(1+2u), |b| <= 2|r|(1+6u),
+  //    disc <= 8 r^2 (1+15u), so n2 <= 4.83 |r| and t2 <= 2.415 |r|), the
+  //    reference's t is t2 (or 0), so with dist^2 > 6 r^2 (and |r| < 1e19,
+  //    t < 1e20) the point is in shadow (scene.h:78-82) whatever the other
+  //    spheres give;
+  //  * c > 0 and b > 0 (both roots negative in exact arithmetic): disc < 0
+  //    is a miss; 0 < disc < b^2 (1 - 2^-50) makes sqrt(disc) round below
+  //    b, so n2 = -b + sq < 0 and both roots are negative: a miss; the lists
+  //    then skip that sphere.  disc == 0 (the negative tangent root the
+  //    reference keeps, sphere.h:43-47) and every other case take the test.
+  bool self_miss = false;
+  if (act && pre >= 0 && fast) {
+    const SphGeo s = g[pre];
+    const double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
+    const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.rr;
+    if (c < 0.0) {
+      occ = dist * dist > 6.0 * s.rr && s.rr < 1e38;
+    } else if (c > 0.0) {
+      const double b = 2.0 * ((ocx * d.x + ocy * d.y) + ocz * d.z);
+      const double p = b * b, disc = p - a4 * c;
+      self_miss = b > 0.0 && (disc < 0.0 || (disc > 0.0 && disc < p * (1.0 - 0x1p-50)));
+    }
+  }
+  const int skip = self_miss ? pre : -1;
+  if (act && !occ) {
     const int N = lg.N, cells = 6 * N * N;
     const int32_t *st = lg.start + (size_t)l * (size_t)(cells + 2);
     // The line o + t d passes (up to rounding) through the light; the grid's
     // margins assume it does within max_off -- checked here, per ray.
+#if RT_ABL == 5  // ablation (diagnostic builds only, not exact): no per-ray line check
+    const double off = 0.0;
+#else
     const D3 w = sub(lp, o);
     const double off = __builtin_fabs(w.y * d.z - w.z * d.y) + __builtin_fabs(w.z * d.x - w.x * d.z) +
                        __builtin_fabs(w.x * d.y - w.y * d.x);
+#endif
+#if RT_ABL == 6  // ablation (wrong images): shadow rays built and checked, lists not tested
+    if (off > 1e300) occ = true;
+    return act && occ;
+#endif
     if (!(off <= lg.max_off) || cell.cb < 0) {
       for (int i = 0; i < n && !occ; ++i) {
+        if (i == skip) continue;
         work.exact += 1;
         test(i);
       }
@@ -1011,8 +1057,10 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
         const int i = nxt;
         ++k;
         if (k < len) nxt = lg.ids[k < len1 ? cell.cb + k : gb + (k - len1)];
-        work.exact += 1;
-        test(i);
+        if (i != skip) {
+          work.exact += 1;
+          test(i);
+        }
       }
     }
   }
@@ -1033,6 +1081,12 @@ __device__ __forceinline__ int quantize(double c) {
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
   unsigned long long s = v;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  return s;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long s) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   return s;

@@ -193,7 +193,11 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
         const D3 to_light = sub(lp, hp);
         const double dist = length(to_light);
         const D3 ldir = normalized(to_light);
+#if RT_ABL == 7  // ablation (wrong images): shadow queries of camera-ray hits only
+        const bool need = hit && key < 0;
+#else
         const bool need = hit;
+#endif
         RT_ACC(work, 3, t_setup);
         RT_T0(t_sh);
         bool occ = false;
@@ -207,7 +211,7 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
 #else
           const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
 #endif
-          occ = lg.on ? shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work)
+          occ = lg.on ? shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi)
                       : sweep_shadow<kCull>(g, rad, n, need, so, sd, lp, hi, dist,
                                             kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), work);
         }
@@ -471,6 +475,9 @@ __device__ __forceinline__ void store_px(uint8_t *out, unsigned pix, D3 c, bool 
     c_neg += (q0 < 0) + (q1 < 0) + (q2 < 0);
   }
   uint8_t *px = out + (size_t)pix * 3;
+#if RT_ABL == 11  // ablation (wrong images): no pixel stores
+  if (q0 + q1 + q2 != -7) return;
+#endif
   px[0] = (uint8_t)(q0 < 0 ? 0 : q0);
   px[1] = (uint8_t)(q1 < 0 ? 0 : q1);
   px[2] = (uint8_t)(q2 < 0 ? 0 : q2);
@@ -577,7 +584,11 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     bool defer = false;
     if (act) {
       if (outcome == kSpawned) {
+#if RT_ABL == 10  // ablation (wrong images): no reflection stack traffic
+        if (color.x > 1e300) ca.gstack[sidx] = StackEnt{color.x, color.y, color.z, refl};
+#else
         ca.gstack[sidx + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
+#endif
         ++lev;
         o = no;
         d = nd;
@@ -587,6 +598,9 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         defer = lev >= kernarg_late<true, offsetof(RenderArgs, defer_level)>(a.defer_level);
       } else {  // the chain ends: unwind its pixel's stack and store it
         D3 res = color;
+#if RT_ABL == 10
+        lev = 0;
+#endif
         while (lev > 0) {
           --lev;
           const StackEnt e = ca.gstack[sidx + (unsigned)lev * sstride];
@@ -636,8 +650,11 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
 }
 
 // Flushes a wave's ray counts and work counters into its counter shard.
+// Called with every lane of the wave active (the per-lane work counters are
+// summed over the wave here).
 __device__ __forceinline__ void flush_counts(unsigned long long *counters, const unsigned long long (&sums)[4],
                                              const Work &work) {
+  const unsigned long long exact = wave_sum64(work.exact), cull = wave_sum64(work.cull);
   if ((threadIdx.x & 63) == 0) {
     unsigned long long *sc = counter_shard(counters);
 #ifdef RT_STAMPS
@@ -652,8 +669,8 @@ __device__ __forceinline__ void flush_counts(unsigned long long *counters, const
 #endif
     for (int q = 0; q < 4; q++)
       if (sums[q]) atomicAdd(&sc[q], sums[q]);
-    if (work.exact) atomicAdd(&sc[4], work.exact);
-    if (work.cull) atomicAdd(&sc[5], work.cull);
+    if (exact) atomicAdd(&sc[4], exact);
+    if (cull) atomicAdd(&sc[5], cull);
   }
 }
 
@@ -830,7 +847,11 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
       if (act) {
         StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, gstack)>(a.gstack);
         if (outcome == kSpawned) {
+#if RT_ABL == 10
+          if (color.x > 1e300) gs[pixg] = StackEnt{color.x, color.y, color.z, refl};
+#else
           gs[pixg + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
+#endif
           ++lev;
           o = no;
           d = nd;
@@ -839,6 +860,9 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
           ++c_reflect;
         } else {
           D3 res = color;
+#if RT_ABL == 10
+          lev = 0;
+#endif
           while (lev > 0) {  // main.cpp:54, innermost first
             --lev;
             const StackEnt e = gs[pixg + (unsigned)lev * sstride];
