@@ -1003,11 +1003,13 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
   //    in [0, 2.42 |r|] (|oc| <= |r|(1+2u), |b| <= 2|r|(1+6u),
   //    disc <= 8 r^2 (1+15u), so n2 <= 4.83 |r| and t2 <= 2.415 |r|), the
   //    reference's t is t2 (or 0), so with dist^2 > 6 r^2 (and |r| < 1e19,
-  //    t < 1e20) the point is in shadow (scene.h:78-82) whatever the other
-  //    spheres give;
+  //    t < 1e20; r^2 > 1e-200 keeps every term normal) the point is in shadow
+  //    (scene.h:78-82) whatever the other spheres give; `fast` (a finite
+  //    direction) guards both cases: a NaN direction makes the reference's t
+  //    NaN, which is never recorded;
   //  * c > 0 and b > 0 (both roots negative in exact arithmetic): disc < 0
   //    is a miss; 0 < disc < b^2 (1 - 2^-50) makes sqrt(disc) round below
-  //    b, so n2 = -b + sq < 0 and both roots are negative: a miss; the lists
+  //    b (b^2 normal), so n2 = -b + sq < 0 and both roots are negative: a miss; the lists
   //    then skip that sphere.  disc == 0 (the negative tangent root the
   //    reference keeps, sphere.h:43-47) and every other case take the test.
   bool self_miss = false;
@@ -1016,11 +1018,11 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
     const double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
     const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.rr;
     if (c < 0.0) {
-      occ = dist * dist > 6.0 * s.rr && s.rr < 1e38;
+      occ = dist * dist > 6.0 * s.rr && s.rr < 1e38 && s.rr > 1e-200;
     } else if (c > 0.0) {
       const double b = 2.0 * ((ocx * d.x + ocy * d.y) + ocz * d.z);
       const double p = b * b, disc = p - a4 * c;
-      self_miss = b > 0.0 && (disc < 0.0 || (disc > 0.0 && disc < p * (1.0 - 0x1p-50)));
+      self_miss = b > 0.0 && (disc < 0.0 || (disc > 0.0 && p > 1e-290 && disc < p * (1.0 - 0x1p-50)));
     }
   }
   const int skip = self_miss ? pre : -1;

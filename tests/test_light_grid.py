@@ -112,3 +112,20 @@ def test_grid_in_other_layouts(monkeypatch, env):
             assert bytes(rgb) == ref, (name, diff_summary(bytes(rgb), ref))
     finally:
         r.close()
+
+
+def test_own_sphere_pretest_agrees_with_reference(tmp_path):
+    """shadow_cells decides the shaded point's own sphere before its lists
+    (rt_device.h): "in shadow" when the ray origin is inside it and
+    dist^2 > 6 r^2, "skip" when both roots are provably negative.  Both must
+    agree with the reference's test of that sphere (sphere.h:26-59 +
+    scene.h:78-82) on 4M random shaded points, grazing hits and lights on, near
+    and inside the sphere (tests/native/self_check.cpp)."""
+    exe = tmp_path / "self_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe),
+                    os.path.join(REPO, "tests", "native", "self_check.cpp")], check=True)
+    out = subprocess.run([str(exe), "4000000"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    w = out.stdout.split()
+    assert w[0] == "checked" and int(w[1]) > 3000000 and int(w[3]) > 100000 and int(w[5]) > 100000
+    assert w[-1] == "0", out.stdout
