@@ -82,7 +82,7 @@ int main(int argc, char **argv) {
   double d2 = 0;
   for (int k = 0; k < 3; k++) d2 += (hi[k] - lo[k]) * (hi[k] - lo[k]);
   const double diam = std::sqrt(d2);
-  const int N = n > 1024 ? 256 : 128;
+  const int N = n > 1024 ? 384 : 128;
   std::vector<int32_t> start, ids;
   rtk::build_light_grid(cx.data(), cy.data(), cz.data(), br.data(), n, lx.data(), ly.data(), lz.data(), nl, diam, N,
                         start, ids);
