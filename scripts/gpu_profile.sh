@@ -14,7 +14,7 @@ cd /tmp
 timeout -k 10 300 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail -5 "$OUT/bench.err"; exit 1; }
 echo "bench: $(head -c 300 "$OUT/bench.json")"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 "$ROOT/bench.py" --no-cpu-baseline > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err" || { echo "trace failed"; tail -5 "$OUT/trace_bench.err"; exit 1; }
+  python3 "$ROOT/bench.py" --no-cpu-baseline --no-also > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err" || { echo "trace failed"; tail -5 "$OUT/trace_bench.err"; exit 1; }
 echo "trace ok"
 for w in $WORKLOADS; do
   i=0; mkdir -p "$OUT/pmc_$w"
