@@ -19,7 +19,7 @@
 // tiles were the fp32 CUDA kernel's approximation.
 //
 // Extra options: --width W --height H --depth D, --threads N (CPU workers,
-// default: hardware threads - 1), --cpu-threshold N (complexity above N goes to
+// default: OMP_NUM_THREADS, else hardware threads - 1), --cpu-threshold N (complexity above N goes to
 // the CPU; -1 sends every tile there), --device N, --streams N, and --dynamic: instead of the static
 // split, tiles sorted by estimated cost form one deque; the GPU thread takes
 // the costliest from the front in batches, each CPU worker the cheapest from
@@ -277,7 +277,11 @@ int main(int argc, char **argv) {
     std::fprintf(stderr, "invalid size, tile size or stream count\n");
     return 2;
   }
-  if (o.threads < 0) o.threads = std::max(1, (int)std::thread::hardware_concurrency() - 1);
+  if (o.threads < 0) {  // OMP_NUM_THREADS (the reference's CPU section is OpenMP), else the cores but one
+    const char *omp = std::getenv("OMP_NUM_THREADS");
+    o.threads = omp && std::atoi(omp) > 0 ? std::atoi(omp) : (int)std::thread::hardware_concurrency() - 1;
+    o.threads = std::max(1, o.threads);
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {  // main_hybrid.cpp:755-761
     std::fprintf(stderr, "No HIP devices found. Cannot run hybrid version.\n");

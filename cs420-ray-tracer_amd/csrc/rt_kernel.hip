@@ -466,6 +466,7 @@ constexpr int kDeferLevel = RT_DEFER_LEVEL;
 #define RT_DEFER_CAP_DIV 8  // deferred-queue room: 1 / RT_DEFER_CAP_DIV of the launch's pixels
 #endif
 constexpr int kDeferSlot = 7;
+constexpr long long kSchedMinTiles = 1024;  // launches with fewer 8x8 tiles keep scanline order
 
 // Stores a pixel's final colour (quantised as write_ppm, main.cpp:85) at out + 3 pix.
 __device__ __forceinline__ void store_px(uint8_t *out, unsigned pix, D3 c, bool img, unsigned &c_neg) {
@@ -1170,7 +1171,11 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     gstack = reinterpret_cast<StackEnt *>(c->cstack_buf);
   }
   const int *perm = nullptr;
-  if (c->sched) {
+  // The heavy-first order pays off when a launch has many more tiles than the
+  // chip has wave slots; a small launch (a hybrid driver's 64x64 tile) keeps
+  // scanline order and skips building and uploading one (which waits for the
+  // stream whenever the tile shape changes).
+  if (c->sched && ntiles >= kSchedMinTiles) {
     int rc = tile_perm(c, cam, W, H, rows, od, 8 * kWx, 8 * kWy, ntiles, perm);
     if (rc != RT_OK) return rc;
   }
