@@ -702,7 +702,10 @@ __device__ __forceinline__ unsigned long long next_group(unsigned long long todo
 
 // Scene::find_intersection (scene.h:41-61): all candidate spheres in file
 // order, strict '<' (so ties keep the lowest index), t starts at 1e20.
-template <bool kCull>
+// kFast: the default configuration only (ordered 4-wide BVH walk); the other
+// walks are not compiled in, which keeps the default kernel's register
+// allocation free of their cold paths (render_kernel's kFast).
+template <bool kCull, bool kFast = false>
 __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
                                              bool act, D3 o, D3 d, int key, const BvhArgs &bv, double &best_t,
                                              Work &work) {
@@ -812,9 +815,13 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       test(i);
       return true;
     };
-    if (has_ordered_stack(bv) && bv.wide) bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
-    else if (has_ordered_stack(bv)) bvh_walk_ordered(bv, o, d, tmax, work, leaf);
-    else bvh_walk(bv, o, d, tmax, work, leaf);
+    if constexpr (kFast) {
+      bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
+    } else {
+      if (has_ordered_stack(bv) && bv.wide) bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
+      else if (has_ordered_stack(bv)) bvh_walk_ordered(bv, o, d, tmax, work, leaf);
+      else bvh_walk(bv, o, d, tmax, work, leaf);
+    }
   }
 #ifdef RT_STAMPS
   if (any_need) RT_ACC(work, 6, tv);

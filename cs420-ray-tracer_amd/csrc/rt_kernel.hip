@@ -138,7 +138,9 @@ __device__ __forceinline__ const T &kernarg_late(const T &x) {
 enum { kEnded = 1, kSpawned = 2 };
 // kArgMem: bv and lg are the kernel's own arguments (kernarg segment), so they
 // are re-read where needed (kernarg_late) instead of held in SGPRs throughout.
-template <bool kCull, bool kArgMem = false>
+// kFast: only the default paths (ordered 4-wide BVH walk, light-grid shadow
+// queries) are compiled in; the host picks it when the scene uses them.
+template <bool kCull, bool kArgMem = false, bool kFast = false>
 __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                        const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                        int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o, D3 d,
@@ -148,7 +150,8 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
   double bt;
   RT_T0(t_cl);
   const int bi =
-      sweep_closest<kCull>(g, rad, n, alive, o, d, key, kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt, work);
+      sweep_closest<kCull, kFast>(g, rad, n, alive, o, d, key, kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt,
+                                  work);
   RT_ACC(work, 8, t_cl);
   const bool hit = alive && bi >= 0;
   if (alive && !hit) {  // sky, main.cpp:26-30
@@ -211,9 +214,12 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
 #else
           const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
 #endif
-          occ = lg.on ? shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi)
-                      : sweep_shadow<kCull>(g, rad, n, need, so, sd, lp, hi, dist,
-                                            kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), work);
+          if constexpr (kFast)
+            occ = shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi);
+          else
+            occ = lg.on ? shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi)
+                        : sweep_shadow<kCull>(g, rad, n, need, so, sd, lp, hi, dist,
+                                              kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), work);
         }
         RT_ACC(work, 9, t_sh);
         RT_T0(t_shade);
@@ -496,7 +502,7 @@ __device__ __forceinline__ void store_px(uint8_t *out, unsigned pix, D3 c, bool 
 //     lanes whose chain ended from the queue.
 // A chain that ends unwinds its pixel's stack (sbase[sidx + level * sstride],
 // innermost first, main.cpp:54) and stores the pixel.
-template <bool kCull>
+template <bool kCull, bool kFast>
 __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                             const SphMat *__restrict__ mat, const LightD *__restrict__ slight,
                                             const RenderArgs &a, int group, int frame, const CompactArgs &ca,
@@ -579,8 +585,8 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     int outcome = 0, nkey = 0;
     D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
     double refl = 0.0;
-    bounce<kCull, true>(g, rad, mat, slight, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft, work, c_shadow,
-                        outcome, color, refl, no, nd, nkey);
+    bounce<kCull, true, kFast>(g, rad, mat, slight, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft, work,
+                               c_shadow, outcome, color, refl, no, nd, nkey);
     const unsigned sidx = pix + ca.fpx;
     bool defer = false;
     if (act) {
@@ -717,7 +723,7 @@ constexpr int wg_waves() {
   return kLdsGeo ? 4 : 1;
 }
 
-template <bool kLdsGeo, bool kCull, int kSamples, int kStack>
+template <bool kLdsGeo, bool kCull, int kSamples, int kStack, bool kFast = false>
 __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) void render_kernel(
     const RenderArgs a) {
   // Workgroups are dealt to the 8 XCDs round robin (b % 8), so every image
@@ -776,7 +782,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
   if constexpr (kStack == kStackMerge && !kLdsGeo && kSamples == 1) {
     // the wave's ray queue sits where trace_wave parks colours (launch_tiles)
     QRay *q = reinterpret_cast<QRay *>(ca.park);
-    merge_tiles<kCull>(g, rad, sm, slight, a, slot, frame, ca, q, work, sums);
+    merge_tiles<kCull, kFast>(g, rad, sm, slight, a, slot, frame, ca, q, work, sums);
   } else {
     trace_tile<kCull, kSamples, kStack, !kLdsGeo>(g, rad, sm, slight, a.n, a.nl, a.amb, kernarg_cam(frame), a.W, a.H,
                                                   a.depth, a.rows, bv, a.lg, a.od,
@@ -798,7 +804,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
 // to the end exactly as merge_tiles would have (bounce, stack entries at its
 // pixel's [level][pixel] slots), unwinds the pixel's whole stack -- the
 // levels merge_tiles wrote first -- and stores the pixel.
-template <bool kCull>
+template <bool kCull, bool kFast = false>
 __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const RenderArgs a) {
   const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards, step = gridDim.x / kShards;
   const int cap = a.dq_cap;
@@ -843,7 +849,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
       int outcome = 0, nkey = 0;
       D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
       double refl = 0.0;
-      bounce<kCull, true>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft,
+      bounce<kCull, true, kFast>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft,
                           work, c_shadow, outcome, color, refl, no, nd, nkey);
       if (act) {
         StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, gstack)>(a.gstack);
@@ -1229,10 +1235,26 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       ra.dq_cap = (int)cap;
     }
   }
-  hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
-  if constexpr (kStack == kStackMerge) {
-    if (ra.dq_cap > 0)  // 48 one-wave workgroups per shard segment
-      hipLaunchKernelGGL((render_deferred<kCull>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
+  if constexpr (kStack == kStackMerge && !kLds && kSamples == 1) {
+    // the default configuration (ordered 4-wide BVH walk, light grids) has kernels
+    // compiled with only those paths (kFast): no registers held for the others
+    const bool fast = bv.ordered && bv.wide && lg.on;
+    if (fast)
+      hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, true>), grid, dim3(64 * kWg), lds, c->stream, ra);
+    else
+      hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
+    if (ra.dq_cap > 0) {  // 48 one-wave workgroups per shard segment
+      if (fast)
+        hipLaunchKernelGGL((render_deferred<kCull, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
+      else
+        hipLaunchKernelGGL((render_deferred<kCull>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
+    }
+  } else {
+    hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
+    if constexpr (kStack == kStackMerge) {
+      if (ra.dq_cap > 0)
+        hipLaunchKernelGGL((render_deferred<kCull>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
+    }
   }
   return RT_OK;
 }
