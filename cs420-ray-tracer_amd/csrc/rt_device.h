@@ -1049,27 +1049,22 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
     if (off > 1e300) occ = true;
     return act && occ;
 #endif
-    if (!(off <= lg.max_off) || cell.cb < 0) {
-      for (int i = 0; i < n && !occ; ++i) {
-        if (i == skip) continue;
+    // the cell's list (first id prefetched), then the global list; a lane
+    // whose line cannot use the grid tests every sphere (ids 0 .. n-1) in the
+    // same loop
+    const bool all = !(off <= lg.max_off) || cell.cb < 0;
+    const int gb = st[cells], ge = st[cells + 1];
+    const int len1 = all ? n : cell.ce - cell.cb, len = all ? n : len1 + (ge - gb);
+    int k = 0;
+    int nxt = all ? 0 : id0;
+    if (!all && len1 == 0 && len > 0) nxt = lg.ids[gb];
+    while (k < len && !occ) {
+      const int i = nxt;
+      ++k;
+      if (k < len) nxt = all ? k : lg.ids[k < len1 ? cell.cb + k : gb + (k - len1)];
+      if (i != skip) {
         work.exact += 1;
         test(i);
-      }
-    } else {
-      // the cell's list (first id prefetched), then the global list
-      const int gb = st[cells], ge = st[cells + 1];
-      const int len1 = cell.ce - cell.cb, len = len1 + (ge - gb);
-      int k = 0;
-      int nxt = id0;
-      if (len1 == 0 && len > 0) nxt = lg.ids[gb];
-      while (k < len && !occ) {
-        const int i = nxt;
-        ++k;
-        if (k < len) nxt = lg.ids[k < len1 ? cell.cb + k : gb + (k - len1)];
-        if (i != skip) {
-          work.exact += 1;
-          test(i);
-        }
       }
     }
   }
