@@ -22,10 +22,9 @@
 // default: OMP_NUM_THREADS, else hardware threads - 1), --cpu-threshold N (complexity above N goes to
 // the CPU; -1 sends every tile there), --device N, --streams N, and --dynamic: instead of the static
 // split, tiles sorted by estimated cost form one deque; the GPU thread takes
-// the costliest from the front in batches, each CPU worker the cheapest from
-// the back, until it is empty (on MI355X the GPU renders a 64x64 tile in tens
-// of microseconds, a CPU core in tens of milliseconds, so the deque hands the
-// CPU only what it can finish in the GPU's shadow).
+// the costliest from the front in batches (one rt_render_tiles launch each),
+// each CPU worker the cheapest from the back, until it is empty.  With
+// --pipeline every GPU tile goes into ONE rt_render_tiles launch.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -121,6 +120,15 @@ struct Gpu {
     CK(rt_render_tile(ctx[(size_t)k], &cam, W, H, depth, t.x0, t.y0, t.x1 - t.x0, t.y1 - t.y0, RT_FB_F64X3, dfb));
     return 0;
   }
+  // several tiles in ONE launch (rt_render_tiles) on the next context
+  int launch_batch(const std::vector<Tile *> &ts, int &k) {
+    k = next;
+    next = (next + 1) % (int)ctx.size();
+    std::vector<rt_tile> rects;
+    for (const Tile *t : ts) rects.push_back(rt_tile{t->x0, t->y0, t->x1 - t->x0, t->y1 - t->y0});
+    CK(rt_render_tiles(ctx[(size_t)k], &cam, W, H, depth, rects.data(), (int)rects.size(), RT_FB_F64X3, dfb));
+    return 0;
+  }
   // download_tile (main_hybrid.cpp:281-309): the tile's rows straight into the host framebuffer
   int download(const Tile &t, int k, rtc::V3 *fb) {
     const size_t pitch = (size_t)W * sizeof(rtc::V3);
@@ -171,12 +179,14 @@ int render_static(const Opts &o, const rtc::CpuTracer &cpu, Gpu &gpu, std::vecto
     }
     if (!rc) rc = gpu.sync_all();
   } else {
-    // every GPU tile launched, then one download of the whole device framebuffer
-    // and a copy of the GPU tiles' pixels (main_hybrid.cpp:535-600)
-    for (Tile *t : gpu_q) {
+    // every GPU tile launched -- here all in one launch (rt_render_tiles) --
+    // then one download of the whole device framebuffer and a copy of the GPU
+    // tiles' pixels (main_hybrid.cpp:535-600)
+    if (!gpu_q.empty()) {
       int k;
-      if ((rc = gpu.launch(*t, k))) break;
-      t->done = true;
+      rc = gpu.launch_batch(gpu_q, k);
+      if (!rc)
+        for (Tile *t : gpu_q) t->done = true;
     }
     std::vector<rtc::V3> all;
     if (!rc && !(rc = gpu.sync_all())) {
@@ -219,27 +229,25 @@ int render_dynamic(const Opts &o, const rtc::CpuTracer &cpu, Gpu &gpu, std::vect
   std::vector<std::thread> pool;
   for (int i = 0; i < o.threads; ++i) pool.emplace_back(cpu_work);
   int rc = 0;
-  const size_t batch = std::max<size_t>(1, 2 * gpu.ctx.size());
-  std::vector<Tile *> mine;
+  // the GPU takes a quarter of what is left per batch (at least 8 tiles): few
+  // launches while the deque is long, small ones near the end
+  const size_t min_batch = 8;
   for (;;) {
     size_t b, e;
     {
       std::lock_guard<std::mutex> l(mu);
       b = front;
-      e = std::min(back, front + batch);
+      e = std::min(back, front + std::max(min_batch, (back - front) / 4));
       front = e;
     }
     if (b >= e) break;
-    std::vector<int> ks;
-    for (size_t i = b; i < e && !rc; ++i) {
-      int k;
-      order[i]->gpu = true;
-      rc = gpu.launch(*order[i], k);
-      ks.push_back(k);
-    }
-    for (size_t i = b; i < e && !rc; ++i) {
-      rc = gpu.download(*order[i], ks[i - b], fb);
-      order[i]->done = true;
+    std::vector<Tile *> mine(order.begin() + (long)b, order.begin() + (long)e);
+    int k = 0;
+    for (Tile *t : mine) t->gpu = true;
+    rc = gpu.launch_batch(mine, k);  // the batch in one launch, then its tiles' rows
+    for (size_t i = 0; i < mine.size() && !rc; ++i) {
+      rc = gpu.download(*mine[i], k, fb);
+      mine[i]->done = true;
     }
     if (rc) break;
   }

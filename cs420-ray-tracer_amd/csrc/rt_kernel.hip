@@ -89,6 +89,7 @@ struct RenderArgs {
   StackEnt *gstack;
   unsigned long long *counters;
   int ntx, ntiles;
+  int nslots;                     // kStackGlobal with perm: launch slots (perm entries); ntiles otherwise
   const int *perm;
   unsigned long long *zero_next;  // counters of the next launch, zeroed by workgroup 0 (or nullptr)
   QRay *dq;                       // kStackMerge: deferred deep rays, [kShards][dq_cap] (render_deferred)
@@ -740,8 +741,8 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
     if (slot * kMergeTiles >= a.ntiles) return;  // slot = this wave's group of kMergeTiles tile slots
   } else {
     if (a.perm) {
-      if (slot >= a.ntiles) return;
-      tile = a.perm[slot];  // heaviest predicted tiles first
+      if (slot >= a.nslots) return;
+      tile = a.perm[slot];  // heaviest predicted tiles first, or a batch's listed blocks
     }
     if (tile >= a.ntiles) return;  // workgroup-uniform, before any barrier
   }
@@ -985,6 +986,12 @@ struct rt_ctx {
   // frames of the launch being enqueued (rt_render_frames_async; 1 otherwise) and their cameras
   int nframes = 1;
   const rt_camera *fcams = nullptr;
+  // rt_render_tiles: the requested tiles of the launch being enqueued, and the
+  // launch-order buffer of the blocks covering them
+  const rt_tile *req_tiles = nullptr;
+  int req_n = 0;
+  int *d_bperm = nullptr, *h_bperm = nullptr;  // h_bperm pinned
+  size_t bperm_cap = 0;
   unsigned char *cstack_buf = nullptr;
   size_t cstack_bytes = 0;
   // RT_HIP_LDS_SCENE=1: stage scenes that fit (<= kLdsBudget) in LDS, 4-wave
@@ -1149,8 +1156,45 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   const int nf = c->nframes;
   if (nf < 1 || nf > RT_MAX_FRAMES) return RT_ERR_INVALID_ARG;
   // kStackMerge: one wave per kMergeTiles consecutive tile slots
-  const long long nslots = kStack == kStackMerge ? (ntiles + kMergeTiles - 1) / kMergeTiles : ntiles;
+  long long nslots = kStack == kStackMerge ? (ntiles + kMergeTiles - 1) / kMergeTiles : ntiles;
   if (ntiles * nf > (1LL << 30)) return RT_ERR_INVALID_ARG;
+  // rt_render_tiles: the launch visits the blocks (launch tiles) that overlap
+  // a requested tile, in scanline order of the blocks
+  const int *batch_perm = nullptr;
+  if constexpr (kStack == kStackGlobal) {
+    if (c->req_tiles) {
+      const int bw = 8 * kWx, bh = 8 * kWy;
+      std::vector<unsigned char> mark((size_t)ntiles, 0);
+      for (int i = 0; i < c->req_n; i++) {
+        const rt_tile &t = c->req_tiles[i];
+        const int x1 = std::min(W, t.x + t.width), j1 = std::min(H, t.y + t.height);
+        if (t.x >= x1 || t.y >= j1) continue;
+        // framebuffer rows j (0 = bottom) are PPM rows H-1-j
+        const int y0 = H - j1, y1 = H - 1 - t.y;
+        for (int by = y0 / bh; by <= y1 / bh; by++)
+          for (int bx = t.x / bw; bx <= (x1 - 1) / bw; bx++) mark[(size_t)by * ntx + bx] = 1;
+      }
+      std::vector<int> list;
+      for (long long b = 0; b < ntiles; b++)
+        if (mark[(size_t)b]) list.push_back((int)b);
+      nslots = (long long)list.size();
+      if (nslots == 0) return RT_OK;
+      const size_t bytes = list.size() * sizeof(int);
+      RT_TRY(c, hipStreamSynchronize(c->stream));  // the previous list may still be in flight from h_bperm
+      if (c->bperm_cap < bytes) {
+        if (c->d_bperm) (void)hipFree(c->d_bperm);
+        if (c->h_bperm) (void)hipHostFree(c->h_bperm);
+        c->d_bperm = c->h_bperm = nullptr;
+        c->bperm_cap = 0;
+        RT_TRY(c, hipMalloc(&c->d_bperm, bytes));
+        RT_TRY(c, hipHostMalloc(&c->h_bperm, bytes, hipHostMallocDefault));
+        c->bperm_cap = bytes;
+      }
+      std::memcpy(c->h_bperm, list.data(), bytes);
+      RT_TRY(c, hipMemcpyAsync(c->d_bperm, c->h_bperm, bytes, hipMemcpyHostToDevice, c->stream));
+      batch_perm = c->d_bperm;
+    }
+  }
   const dim3 grid((unsigned)(nslots * nf));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   lds = (lds + 31) & ~(size_t)31;
@@ -1181,7 +1225,9 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   // chip has wave slots; a small launch (a hybrid driver's 64x64 tile) keeps
   // scanline order and skips building and uploading one (which waits for the
   // stream whenever the tile shape changes).
-  if (c->sched && ntiles >= kSchedMinTiles) {
+  if (batch_perm) {
+    perm = batch_perm;
+  } else if (c->sched && ntiles >= kSchedMinTiles) {
     int rc = tile_perm(c, cam, W, H, rows, od, 8 * kWx, 8 * kWy, ntiles, perm);
     if (rc != RT_OK) return rc;
   }
@@ -1207,6 +1253,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.counters = c->d_counters;
   ra.ntx = ntx;
   ra.ntiles = (int)ntiles;
+  ra.nslots = (int)nslots;
   ra.perm = perm;
   // zero the other counter half for the next launch (enqueue's alternation)
   const int next = (int)((c->launches + 1) & 1);
@@ -1418,6 +1465,8 @@ void rt_destroy(rt_ctx *c) {
   if (c->dq_buf) (void)hipFree(c->dq_buf);
   if (c->d_perm) (void)hipFree(c->d_perm);
   if (c->h_perm) (void)hipHostFree(c->h_perm);
+  if (c->d_bperm) (void)hipFree(c->d_bperm);
+  if (c->h_bperm) (void)hipHostFree(c->h_bperm);
   for (int i = 0; i < rt_ctx::kRing; i++) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
@@ -1735,6 +1784,23 @@ int rt_render_tile(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, int
   const Rows r{1, H - ye, 1, xw > 0 ? th : 0};
   RT_TRY(c, hipSetDevice(c->device));
   return enqueue(c, cam, W, H, depth, r, OutDesc{fb_device, fb_format, 1, tile_x, xw});
+}
+
+int rt_render_tiles(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, const rt_tile *tiles, int ntiles,
+                    int fb_format, void *fb_device) {
+  if (!c || !cam || !fb_device || W <= 0 || H <= 0 || ntiles < 0 || (ntiles > 0 && !tiles)) return RT_ERR_INVALID_ARG;
+  if (fb_format != RT_FB_RGB8 && fb_format != RT_FB_F32X3 && fb_format != RT_FB_F64X3) return RT_ERR_INVALID_ARG;
+  for (int i = 0; i < ntiles; i++)
+    if (tiles[i].x < 0 || tiles[i].y < 0 || tiles[i].width < 0 || tiles[i].height < 0) return RT_ERR_INVALID_ARG;
+  if (!c->has_scene) return RT_ERR_NO_SCENE;
+  if (depth > RT_MAX_DEPTH) return RT_ERR_DEPTH;
+  RT_TRY(c, hipSetDevice(c->device));
+  c->req_tiles = tiles;
+  c->req_n = ntiles;
+  const int rc = enqueue(c, cam, W, H, depth, Rows{1, 0, 1, H}, OutDesc{fb_device, fb_format, 1, 0, W});
+  c->req_tiles = nullptr;
+  c->req_n = 0;
+  return rc;
 }
 
 int rt_kernel_times(rt_ctx *c, double *ms_out, int max_n, int *n_out) {

@@ -22,7 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(HERE, "librt_hip.so")
 
 RT_MAX_DEPTH = 64
-ABI_VERSION = 5  # RT_HIP_ABI_VERSION in include/rt_hip.h
+ABI_VERSION = 6  # RT_HIP_ABI_VERSION in include/rt_hip.h
 MAX_FRAMES = 32  # RT_MAX_FRAMES
 
 
@@ -52,6 +52,10 @@ class rt_scene(C.Structure):
 class rt_camera(C.Structure):
     _fields_ = [("position", C.c_double * 3), ("forward", C.c_double * 3), ("right", C.c_double * 3),
                 ("up", C.c_double * 3), ("scale", C.c_double)]
+
+
+class rt_tile(C.Structure):
+    _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("width", C.c_int32), ("height", C.c_int32)]
 
 
 class rt_rows(C.Structure):
@@ -101,6 +105,8 @@ SIGNATURES = {
     "rt_unpermute_rows": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     "rt_render_tile": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.c_int, _P]),
+    "rt_render_tiles": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.POINTER(rt_tile), C.c_int,
+                                  C.c_int, _P]),
     "rt_set_antialias": (C.c_int, [_P, C.c_int]),
 }
 
@@ -311,6 +317,13 @@ class Renderer:
         """launch_gpu_kernel tile semantics (kernel.cu:185-200) into a full-image device framebuffer."""
         _check(lib().rt_render_tile(self._ctx, C.byref(cam), width, height, depth, tile_x, tile_y, tile_w, tile_h,
                                     fb_format, C.c_void_p(fb_device_ptr)), "rt_render_tile", self._ctx)
+
+    def render_tiles(self, cam: rt_camera, width: int, height: int, depth: int, tiles, fb_format: int,
+                     fb_device_ptr: int):
+        """rt_render_tiles: every (x, y, w, h) tile of `tiles` in ONE launch (the 8x8 blocks covering them)."""
+        arr = (rt_tile * max(1, len(tiles)))(*[rt_tile(*t) for t in tiles])
+        _check(lib().rt_render_tiles(self._ctx, C.byref(cam), width, height, depth, arr, len(tiles), fb_format,
+                                     C.c_void_p(fb_device_ptr)), "rt_render_tiles", self._ctx)
 
     def stats(self) -> rt_stats:
         st = rt_stats()

@@ -20,6 +20,7 @@
  *   rt_write_ppm                    <- write_ppm()            src/main.cpp:69-91
  *   rt_kernel_times                 <- cudaEventElapsedTime around the kernel, src/main_gpu.cu:496-519
  *   rt_unpermute_rows               <- (new) reassembly of the multi-GPU row shards
+ *   rt_render_tiles                 <- the same for a list of tiles in one launch (the hybrid driver's GPU share)
  *   rt_render_tile                  <- launch_gpu_kernel's tile semantics  src/kernel.cu:185-200 (x = tile_x + ...,
  *                                      y = tile_y + ..., fb[y*W + x], kernel.cu:99-112), as main_hybrid.cpp:457-470
  *                                      calls it; float3 / Vec3 / RGB8 framebuffers
@@ -49,7 +50,8 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 5  /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard */
+#define RT_HIP_ABI_VERSION 6  /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
+                                   6: rt_render_tiles */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -220,6 +222,23 @@ int rt_kernel_times(rt_ctx *ctx, double *ms_out, int max_n, int *n_out);
  * kernel's fp32 approximation. */
 int rt_render_tile(rt_ctx *ctx, const rt_camera *cam, int image_width, int image_height, int depth, int tile_x,
                    int tile_y, int tile_width, int tile_height, int fb_format, void *fb_device);
+
+/* One launch_gpu_kernel tile (kernel.cu:185-200): pixels x in [x, x + width),
+ * framebuffer rows j in [y, y + height) (j = 0 the bottom row). */
+typedef struct rt_tile {
+    int32_t x, y, width, height;
+} rt_tile;
+
+/* Many tiles in ONE launch (a hybrid driver's GPU share of a frame,
+ * main_hybrid.cpp:457-470 / 535-548, without a launch and a sync per tile):
+ * every 8x8-pixel block of the image that overlaps a tile is rendered into the
+ * full-image DEVICE framebuffer exactly as rt_render_tile renders it, so the
+ * tiles' pixels are rt_render_tile's; the other pixels of those blocks are
+ * written too (with their own colours), all others are not touched.
+ * Asynchronous on the context stream; waits for the stream first when the
+ * context's block list is still in use. */
+int rt_render_tiles(rt_ctx *ctx, const rt_camera *cam, int image_width, int image_height, int depth,
+                    const rt_tile *tiles, int num_tiles, int fb_format, void *fb_device);
 
 /* Samples per pixel for later renders: 1 (default, the serial path) or 4 (the
  * reference GPU's `-a` antialias mode, main_gpu.cu:249-333: offsets

@@ -12,6 +12,9 @@ compared byte for byte.
   main.cpp:156), its fp32 rounding (RT_FB_F32X3, the reference's float3 fb)
   and the golden RGB8 image (RT_FB_RGB8), including ragged edge tiles and
   tiles that overhang the image (clipped as kernel.cu:103).
+* rt_render_tiles -- a list of such tiles in one launch (the hybrid
+  driver's GPU share): the tiles' pixels as rt_render_tile's, only the 8x8
+  blocks overlapping them written.
 * rt_set_antialias(4) -- the `-a` mode (main_gpu.cu:249-333) in the serial
   fp64 semantics, against the oracle's restatement (orc_render_aa).  The
   reference has no CPU antialias path, so this parity is pinned through the
@@ -122,6 +125,72 @@ def test_tile_leaves_other_pixels_alone(gpu_renderer):
     assert gpu_renderer.stats().rays_primary == 0
     with pytest.raises(rt_hip.RtError):
         gpu_renderer.render_tile(sc.camera(), W, H, D, 0, 0, 8, 8, 9, fb.data_ptr())
+
+
+@pytest.mark.parametrize("tiles", [
+    [(0, 0, 32, 32), (40, 13, 17, 9), (90, 50, 100, 100)],      # ragged, overhanging
+    [(tx, ty, 13, 7) for tx, ty, _, _ in _tiles(97, 61, 13, 7)],  # every pixel, unaligned tiles
+    [(5, 5, 3, 3), (5, 5, 3, 3), (6, 6, 30, 2)],                  # duplicated and overlapping
+])
+def test_tiles_batch_match_oracle_framebuffer(gpu_renderer, tiles):
+    """rt_render_tiles: the listed tiles' pixels in ONE launch equal rt_render_tile's
+    (the oracle's fp64 framebuffer within MAX_ULP); only the 8x8 blocks that
+    overlap a tile are written."""
+    import orc
+    import rt_hip
+    import torch
+
+    name = "complex_97x61_d4"
+    m = manifest()[name]
+    W, H, D = m["width"], m["height"], m["depth"]
+    sc = rt_hip.Scene.load(scene_path(m["scene"]))
+    gpu_renderer.upload(sc)
+    fb = torch.full((H * W * 3,), float("nan"), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # the fill (torch's stream) lands before the launch
+    gpu_renderer.render_tiles(sc.camera(), W, H, D, tiles, rt_hip.RT_FB_F64X3, fb.data_ptr())
+    gpu_renderer.stats()
+    got = fb.cpu().numpy().reshape(H, W, 3)
+    _, _, _, ref_fb = orc.OracleScene(scene_path(m["scene"])).render(W, H, D, threads=4, want_fb=True)
+    ref = np.array(ref_fb, dtype=np.float64).reshape(H, W, 3)[::-1]  # index j*W + x, j = 0 the bottom row
+    want = np.zeros((H, W), bool)  # the tiles' pixels
+    blocks = np.zeros((H, W), bool)  # the 8x8 blocks (PPM row order) that overlap a tile
+    for x, y, w, h in tiles:
+        x1, j1 = min(W, x + w), min(H, y + h)
+        if x >= x1 or y >= j1:
+            continue
+        want[y:j1, x:x1] = True
+        p0, p1 = H - j1, H - 1 - y  # PPM rows of the tile
+        for by in range(p0 // 8, p1 // 8 + 1):
+            for bx in range(x // 8, (x1 - 1) // 8 + 1):
+                r0, r1 = by * 8, min(H, by * 8 + 8)  # PPM rows -> framebuffer rows j = H-1-row
+                blocks[H - r1:H - r0, bx * 8:min(W, bx * 8 + 8)] = True
+    assert ulp_diff(got[want], ref[want]).max() <= MAX_ULP
+    assert np.isfinite(got[blocks]).all()
+    assert np.isnan(got[~blocks]).all()
+
+
+def test_tiles_batch_rgb8_and_errors(gpu_renderer):
+    import rt_hip
+    import torch
+
+    name = "medium_1280x720_d10"
+    m = manifest()[name]
+    W, H, D = m["width"], m["height"], m["depth"]
+    sc = rt_hip.Scene.load(scene_path(m["scene"]))
+    gpu_renderer.upload(sc)
+    rgb = torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    gpu_renderer.render_tiles(sc.camera(), W, H, D, list(_tiles(W, H, 64, 64)), rt_hip.RT_FB_RGB8, rgb.data_ptr())
+    st = gpu_renderer.stats()
+    assert rgb.cpu().numpy().tobytes() == golden_rgb(name)
+    assert st.rays_primary == W * H
+    gpu_renderer.render_tiles(sc.camera(), W, H, D, [], rt_hip.RT_FB_RGB8, rgb.data_ptr())  # nothing to do
+    assert gpu_renderer.stats().rays_primary == 0
+    for bad in ([(0, 0, -1, 4)], [(-3, 0, 4, 4)]):
+        with pytest.raises(rt_hip.RtError):
+            gpu_renderer.render_tiles(sc.camera(), W, H, D, bad, rt_hip.RT_FB_RGB8, rgb.data_ptr())
+    with pytest.raises(rt_hip.RtError):
+        gpu_renderer.render_tiles(sc.camera(), W, H, D, [(0, 0, 8, 8)], 9, rgb.data_ptr())
 
 
 @pytest.fixture
