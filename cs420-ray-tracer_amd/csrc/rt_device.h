@@ -401,6 +401,22 @@ __device__ __forceinline__ int2 *ordered_stack(const BvhArgs &bv) {
   return base + (threadIdx.x & 63);
 }
 __device__ __forceinline__ bool has_ordered_stack(const BvhArgs &bv) { return bv.ostk || bv.ostk_off >= 0; }
+// The same entry when the stacks are known to sit in dynamic LDS (ostk ==
+// nullptr, the kFast kernels): an LDS-typed pointer, so pushes and pops are
+// ds_write / ds_read instead of flat accesses (which also wait for the
+// outstanding global loads).
+// An entry is (node reference, entry t bits) = int2 {x, y}, read and written
+// here as one 64-bit word (x in the low half).
+typedef __attribute__((address_space(3))) unsigned long long LdsU64;
+__device__ __forceinline__ LdsU64 *ordered_stack_lds(const BvhArgs &bv) {
+  typedef __attribute__((address_space(3))) unsigned char LdsByte;
+  LdsByte *base = (LdsByte *)(rt_dyn_lds) + bv.ostk_off;
+  return reinterpret_cast<LdsU64 *>(base) + (size_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * bv.odepth * 64 +
+         (threadIdx.x & 63);
+}
+__device__ __forceinline__ unsigned long long stk_entry(int ref, float t) {
+  return ((unsigned long long)(unsigned)__float_as_int(t) << 32) | (unsigned)ref;
+}
 
 
 // Visits every leaf whose (grown) box the line meets and whose entry does not
@@ -530,7 +546,7 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
 // node-steps per primary query, 89 -> 46 per secondary, synth10k), each one
 // with four independent box tests.  Every leaf that can hold a closer root is
 // still visited, so the lexicographic (t, index) minimum is unchanged.
-template <typename T, typename F>
+template <bool kLdsStack = false, typename T, typename F>
 __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d, T &&tmax_fn, Work &work,
                                                   F &&leaf_fn) {
   const float ox = (float)(o.x - bv.c0x), oy = (float)(o.y - bv.c0y), oz = (float)(o.z - bv.c0z);
@@ -538,16 +554,37 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
   const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
   const float dd = (dx * dx + dy * dy + dz * dz) * (1.0f + 1e-5f);
   const float m = bv.margin;
+  // (lo - m - ox) regrouped as lo - (ox + m): one subtraction per plane; the
+  // two roundings stay ~2^-24 of the diameter, far inside the margin m (1e-6
+  // of it), so the grown slab still contains the exact one
+  const float lx = ox + m, ly = oy + m, lz = oz + m, hx = ox - m, hy = oy - m, hz = oz - m;
+  // The prune bound in fp32, rounded up (re-read after every leaf, where the
+  // best t can shrink): an entry t > tmf is > tmax_fn() too, so every box the
+  // fp64 comparison keeps is kept (a box at tmax < t <= tmf is kept as well,
+  // which costs a visit, never a result); NaNs keep boxes either way.
+  auto tmax_f = [&] {
+    const double x = tmax_fn();
+    float f = (float)x;
+    if ((double)f < x) {  // one float up: f is finite here (x > f)
+      const int b = __float_as_int(f);
+      f = f == 0.0f ? 0x1p-149f : __int_as_float(f > 0.0f ? b + 1 : b - 1);
+    }
+    return f;
+  };
+  float tmf = tmax_f();
   {
     const BvhNode &r0 = bv.nodes[0];
-    const float ax = (r0.lo[0] - m - ox) * ix, bx = (r0.hi[0] + m - ox) * ix;
-    const float ay = (r0.lo[1] - m - oy) * iy, by = (r0.hi[1] + m - oy) * iy;
-    const float az = (r0.lo[2] - m - oz) * iz, bz = (r0.hi[2] + m - oz) * iz;
+    const float ax = (r0.lo[0] - lx) * ix, bx = (r0.hi[0] - hx) * ix;
+    const float ay = (r0.lo[1] - ly) * iy, by = (r0.hi[1] - hy) * iy;
+    const float az = (r0.lo[2] - lz) * iz, bz = (r0.hi[2] - hz) * iz;
     const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-    if (!(tn <= tf && !((double)tn > tmax_fn()))) return;
+    if (!(tn <= tf && !(tn > tmf))) return;
   }
-  int2 *st = ordered_stack(bv);
+  auto st = [&] {
+    if constexpr (kLdsStack) return ordered_stack_lds(bv);
+    else return reinterpret_cast<unsigned long long *>(ordered_stack(bv));
+  }();
   int sp = 0;
   int ref = bv.root4;
   for (;;) {
@@ -559,12 +596,12 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
       int hits = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float ax = (nd->lox[k] - m - ox) * ix, bx = (nd->hix[k] + m - ox) * ix;
-        const float ay = (nd->loy[k] - m - oy) * iy, by = (nd->hiy[k] + m - oy) * iy;
-        const float az = (nd->loz[k] - m - oz) * iz, bz = (nd->hiz[k] + m - oz) * iz;
+        const float ax = (nd->lox[k] - lx) * ix, bx = (nd->hix[k] - hx) * ix;
+        const float ay = (nd->loy[k] - ly) * iy, by = (nd->hiy[k] - hy) * iy;
+        const float az = (nd->loz[k] - lz) * iz, bz = (nd->hiz[k] - hz) * iz;
         const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
         const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-        const bool h = tn <= tf && !((double)tn > tmax_fn());  // NaN (unused slot) -> false
+        const bool h = tn <= tf && !(tn > tmf);  // NaN (unused slot) -> false
         hits += h ? 1 : 0;
         // sort key: a hit sorts below every miss (fminf keeps it finite-or-below-inf)
         t[k] = h ? fminf(tn, 3.0e38f) : __builtin_inff();
@@ -582,9 +619,9 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
       ce(1, 3);
       ce(1, 2);
       if (hits > 0) {
-        if (hits > 3) st[(sp++) * 64] = make_int2(r[3], __float_as_int(t[3]));
-        if (hits > 2) st[(sp++) * 64] = make_int2(r[2], __float_as_int(t[2]));
-        if (hits > 1) st[(sp++) * 64] = make_int2(r[1], __float_as_int(t[1]));
+        if (hits > 3) st[(sp++) * 64] = stk_entry(r[3], t[3]);
+        if (hits > 2) st[(sp++) * 64] = stk_entry(r[2], t[2]);
+        if (hits > 1) st[(sp++) * 64] = stk_entry(r[1], t[1]);
         ref = r[0];
         continue;
       }
@@ -598,13 +635,14 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
         if (cx * cx + cy * cy + cz * cz > R * R * dd) continue;
         if (!leaf_fn((int)bv.prims[first + k])) return;
       }
+      tmf = tmax_f();
     }
     bool more = false;
     while (sp > 0) {
       --sp;
-      const int2 e = st[sp * 64];
-      if (!((double)__int_as_float(e.y) > tmax_fn())) {
-        ref = e.x;
+      const unsigned long long e = st[sp * 64];
+      if (!(__int_as_float((int)(e >> 32)) > tmf)) {
+        ref = (int)(unsigned)e;
         more = true;
         break;
       }
@@ -816,7 +854,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       return true;
     };
     if constexpr (kFast) {
-      bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
+      bvh_walk_ordered4<true>(bv, o, d, tmax, work, leaf);
     } else {
       if (has_ordered_stack(bv) && bv.wide) bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
       else if (has_ordered_stack(bv)) bvh_walk_ordered(bv, o, d, tmax, work, leaf);

@@ -850,8 +850,18 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
       int outcome = 0, nkey = 0;
       D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
       double refl = 0.0;
+#if RT_ABL == 12  // ablation (wrong images): deferred rays find their closest hit and end (no shading)
+      {
+        double bt = 0.0;
+        const int bi = sweep_closest<kCull, kFast>(a.geo, a.radius, a.n, act,  o, d, key,
+                                                   kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv), bt, work);
+        outcome = kEnded;
+        color = mk(bt, (double)bi, 0.0);
+      }
+#else
       bounce<kCull, true, kFast>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft,
                           work, c_shadow, outcome, color, refl, no, nd, nkey);
+#endif
       if (act) {
         StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, gstack)>(a.gstack);
         if (outcome == kSpawned) {

@@ -65,6 +65,11 @@ struct Bvh4 {
 };
 
 static long g_maxstk[3] = {0, 0, 0};
+struct QR {
+  V o, d;
+  int lev;
+};
+static std::vector<QR> g_deep;  // rays of level >= 2 in the order the tiles spawn them
 static double g_zero[4][4];  // per class: lane queries, zero-term lanes, wave queries, all-zero waves
 static const std::vector<BvhNode> *g_nodes;
 static const std::vector<int32_t> *g_prims;
@@ -316,6 +321,7 @@ int main(int argc, char **argv) {
           V rd = d[l] - nrm[l] * (2 * dot(d[l], nrm[l]));
           o[l] = hp[l] + nrm[l] * 0.001;
           d[l] = nrmz(rd);
+          if (lev + 1 == 2) g_deep.push_back({o[l], d[l], lev + 1});
         }
       }
     }
@@ -334,5 +340,67 @@ int main(int argc, char **argv) {
     std::printf("zero-term shadow queries, %s: lanes %.1f %%, whole waves %.1f %%\n", c ? "secondary" : "primary",
                 100 * g_zero[c][1] / g_zero[c][0], 100 * g_zero[c][3] / g_zero[c][2]);
   std::printf("max stack: ordered %ld ordered4 %ld\n", g_maxstk[1], g_maxstk[2]);
+  // level-2 rays packed 64 per wave in spawn order (the deferred queue): the
+  // ordered4 closest walk's lane utilisation per wave (sum of lane node visits
+  // / 64 x the wave's max) against a walk whose finished lanes refill
+  {
+    std::vector<long> nodes_of(g_deep.size());
+    double sum = 0;
+    for (size_t k = 0; k < g_deep.size(); k++) {
+      long nn = 0, nt = 0;
+      double t = INFINITY;
+      int b = -1;
+      walk2(s, strats[2], g_deep[k].o, g_deep[k].d, false, 0, t, b, nn, nt);
+      nodes_of[k] = nn + nt;
+      sum += nn + nt;
+    }
+    double wsum = 0;
+    for (size_t k = 0; k < g_deep.size(); k += 64) {
+      long mx = 0;
+      for (size_t j = k; j < std::min(g_deep.size(), k + 64); j++) mx = std::max(mx, nodes_of[j]);
+      wsum += 64.0 * mx;
+    }
+    // the same rays sorted by direction octant, then a coarse origin grid cell
+    {
+      V lo{1e300, 1e300, 1e300}, hi{-1e300, -1e300, -1e300};
+      for (auto &q : g_deep)
+        lo = {std::min(lo.x, q.o.x), std::min(lo.y, q.o.y), std::min(lo.z, q.o.z)},
+        hi = {std::max(hi.x, q.o.x), std::max(hi.y, q.o.y), std::max(hi.z, q.o.z)};
+      for (int bits : {0, 1, 2, 3, 4}) {
+        std::vector<std::pair<long, size_t>> key(g_deep.size());
+        for (size_t k = 0; k < g_deep.size(); k++) {
+          const QR &q = g_deep[k];
+          long oct = (q.d.x < 0) | ((q.d.y < 0) << 1) | ((q.d.z < 0) << 2);
+          const int G = 1 << bits;
+          auto cell = [&](double v, double a, double b) {
+            int c = (int)((v - a) / std::max(1e-300, b - a) * G);
+            return (long)std::min(std::max(c, 0), G - 1);
+          };
+          long m = (cell(q.o.x, lo.x, hi.x) * G + cell(q.o.y, lo.y, hi.y)) * G + cell(q.o.z, lo.z, hi.z);
+          key[k] = {oct * 100000 + m, k};
+        }
+        std::stable_sort(key.begin(), key.end());
+        double ws = 0;
+        for (size_t k = 0; k < key.size(); k += 64) {
+          long mx = 0;
+          for (size_t j = k; j < std::min(key.size(), k + 64); j++) mx = std::max(mx, nodes_of[key[j].second]);
+          ws += 64.0 * mx;
+        }
+        std::printf("  sorted by octant + %d^3 origin cells: lane util %.3f\n", 1 << bits, sum / std::max(1.0, ws));
+      }
+    }
+    if (const char *dump = std::getenv("BVH_SIM_DUMP")) {  // per-ray walk steps, spawn order
+      if (FILE *f = std::fopen(dump, "w")) {
+        for (long v : nodes_of) std::fprintf(f, "%ld\n", v);
+        std::fclose(f);
+      }
+    }
+    std::vector<long> srt = nodes_of;
+    std::sort(srt.begin(), srt.end());
+    auto pct = [&](double p) { return srt.empty() ? 0L : srt[(size_t)(p * (srt.size() - 1))]; };
+    std::printf("level-2 rays %zu: node+leaf steps mean %.1f p50 %ld p90 %ld p99 %ld max %ld; wave-packed lane util %.3f\n",
+                g_deep.size(), sum / std::max<size_t>(1, g_deep.size()), pct(0.5), pct(0.9), pct(0.99),
+                srt.empty() ? 0L : srt.back(), sum / std::max(1.0, wsum));
+  }
   return 0;
 }
