@@ -538,6 +538,17 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
   }
 }
 
+// x rounded up to fp32 (the walks' prune bound: an entry t above it is above
+// x too).  NaN stays NaN (every comparison with it keeps the box).
+__device__ __forceinline__ float float_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) {  // one float up: f is finite here (x > f)
+    const int b = __float_as_int(f);
+    f = f == 0.0f ? 0x1p-149f : __int_as_float(f > 0.0f ? b + 1 : b - 1);
+  }
+  return f;
+}
+
 // Ordered closest-hit walk over the 4-wide nodes (rt_bvh.h BvhNode4): the
 // same grown fp32 slab test as bvh_walk_ordered on up to four child boxes,
 // the nearest entered, the other hits pushed farthest first (so the nearest
@@ -562,15 +573,7 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
   // best t can shrink): an entry t > tmf is > tmax_fn() too, so every box the
   // fp64 comparison keeps is kept (a box at tmax < t <= tmf is kept as well,
   // which costs a visit, never a result); NaNs keep boxes either way.
-  auto tmax_f = [&] {
-    const double x = tmax_fn();
-    float f = (float)x;
-    if ((double)f < x) {  // one float up: f is finite here (x > f)
-      const int b = __float_as_int(f);
-      f = f == 0.0f ? 0x1p-149f : __int_as_float(f > 0.0f ? b + 1 : b - 1);
-    }
-    return f;
-  };
+  auto tmax_f = [&] { return float_up(tmax_fn()); };
   float tmf = tmax_f();
   {
     const BvhNode &r0 = bv.nodes[0];
@@ -648,6 +651,127 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
       }
     }
     if (!more) return;
+  }
+}
+
+// bvh_walk_ordered4 (LDS stacks) as a resumable state machine, for a kernel
+// whose lanes are at different stages of their rays (render_deferred_walk):
+// walk4_begin tests the root box, each walk4_step visits the pending node or
+// leaf and pops the next pending entry (false: the walk is over).  The
+// visits, their order and the pruning are bvh_walk_ordered4's, so the closest
+// hit is the same.  The fp32 form of the ray (walk4_ray) is recomputed
+// wherever a kernel resumes walks, so it is not live across other work.
+struct Walk4Ray {
+  float ox, oy, oz, dx, dy, dz, ix, iy, iz, dd, lx, ly, lz, hx, hy, hz;
+};
+__device__ __forceinline__ Walk4Ray walk4_ray(const BvhArgs &bv, D3 o, D3 d) {
+  Walk4Ray r;
+  r.ox = (float)(o.x - bv.c0x), r.oy = (float)(o.y - bv.c0y), r.oz = (float)(o.z - bv.c0z);
+  r.dx = (float)d.x, r.dy = (float)d.y, r.dz = (float)d.z;
+  r.ix = 1.0f / r.dx, r.iy = 1.0f / r.dy, r.iz = 1.0f / r.dz;
+  r.dd = (r.dx * r.dx + r.dy * r.dy + r.dz * r.dz) * (1.0f + 1e-5f);
+  const float m = bv.margin;
+  r.lx = r.ox + m, r.ly = r.oy + m, r.lz = r.oz + m, r.hx = r.ox - m, r.hy = r.oy - m, r.hz = r.oz - m;
+  return r;
+}
+__device__ __forceinline__ bool walk4_begin(const BvhArgs &bv, const Walk4Ray &r, float tmf, int &ref, int &sp) {
+  const BvhNode &r0 = bv.nodes[0];
+  const float ax = (r0.lo[0] - r.lx) * r.ix, bx = (r0.hi[0] - r.hx) * r.ix;
+  const float ay = (r0.lo[1] - r.ly) * r.iy, by = (r0.hi[1] - r.hy) * r.iy;
+  const float az = (r0.lo[2] - r.lz) * r.iz, bz = (r0.hi[2] - r.hz) * r.iz;
+  const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+  const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+  ref = bv.root4;
+  sp = 0;
+  return tn <= tf && !(tn > tmf);
+}
+// leaf_fn(sphere index) tests one sphere; tmf_fn() is the current prune bound
+// (float_up of the closest-hit margin), re-read after a leaf.
+template <typename T, typename F>
+__device__ __forceinline__ bool walk4_step(const BvhArgs &bv, const Walk4Ray &r, T &&tmf_fn, Work &work, F &&leaf_fn,
+                                           int &ref, int &sp, float &tmf) {
+  LdsU64 *st = ordered_stack_lds(bv);
+  work.cull += 1;
+  if (ref >= 0) {
+    const BvhNode4 *nd = bv.n4 + ref;
+    float t[4];
+    int c[4];
+    int hits = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float ax = (nd->lox[k] - r.lx) * r.ix, bx = (nd->hix[k] - r.hx) * r.ix;
+      const float ay = (nd->loy[k] - r.ly) * r.iy, by = (nd->hiy[k] - r.hy) * r.iy;
+      const float az = (nd->loz[k] - r.lz) * r.iz, bz = (nd->hiz[k] - r.hz) * r.iz;
+      const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+      const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+      const bool h = tn <= tf && !(tn > tmf);
+      hits += h ? 1 : 0;
+      t[k] = h ? fminf(tn, 3.0e38f) : __builtin_inff();
+      c[k] = nd->c[k];
+    }
+    auto ce = [&](int a, int b) {
+      const bool sw = t[b] < t[a];
+      const float ta = sw ? t[b] : t[a], tb = sw ? t[a] : t[b];
+      const int ca = sw ? c[b] : c[a], cb = sw ? c[a] : c[b];
+      t[a] = ta, t[b] = tb, c[a] = ca, c[b] = cb;
+    };
+    ce(0, 1);
+    ce(2, 3);
+    ce(0, 2);
+    ce(1, 3);
+    ce(1, 2);
+    if (hits > 0) {
+      if (hits > 3) st[(sp++) * 64] = stk_entry(c[3], t[3]);
+      if (hits > 2) st[(sp++) * 64] = stk_entry(c[2], t[2]);
+      if (hits > 1) st[(sp++) * 64] = stk_entry(c[1], t[1]);
+      ref = c[0];
+      return true;
+    }
+  } else {
+    const int leaf = -(ref + 1), first = leaf >> 4, cnt = leaf & 15;
+    for (int k = 0; k < cnt; ++k) {
+      const float4 q = bv.pf[first + k];  // fp32 prefilter, as bvh_walk
+      const float wx = q.x - r.ox, wy = q.y - r.oy, wz = q.z - r.oz;
+      const float cx = wy * r.dz - wz * r.dy, cy = wz * r.dx - wx * r.dz, cz = wx * r.dy - wy * r.dx;
+      const float R = q.w + bv.pmargin;
+      if (cx * cx + cy * cy + cz * cz > R * R * r.dd) continue;
+      leaf_fn((int)bv.prims[first + k]);
+    }
+    tmf = tmf_fn();
+  }
+  while (sp > 0) {
+    --sp;
+    const unsigned long long e = st[sp * 64];
+    if (!(__int_as_float((int)(e >> 32)) > tmf)) {
+      ref = (int)(unsigned)e;
+      return true;
+    }
+  }
+  return false;
+}
+
+// One candidate of the closest-hit search (sweep_closest's exact test): (bt,
+// bi) is the lexicographic (t, index) minimum so far and bn its numerator.
+__device__ __forceinline__ void closest_test(const SphGeo &s, int i, D3 o, D3 d, double a4, double a2, bool fast,
+                                             double &bt, double &bn, int &bi) {
+  double num;
+  const int r = fast ? intersect_num(s, o, d, a4, num) : 2;
+  if (r == 1) {
+    if (num < bn || i < bi) {
+      const double t = num / a2;
+      if (t < bt || (t == bt && i < bi)) {
+        bt = t;
+        bn = num;
+        bi = i;
+      }
+    }
+  } else if (r == 2) {
+    double t;
+    if (intersect(s, o, d, a4, a2, t) && (t < bt || (t == bt && i < bi))) {
+      bt = t;
+      bn = __builtin_inf();  // no numerator for this best: every later candidate divides
+      bi = i;
+    }
   }
 }
 

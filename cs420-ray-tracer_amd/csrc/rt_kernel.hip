@@ -141,19 +141,17 @@ enum { kEnded = 1, kSpawned = 2 };
 // are re-read where needed (kernarg_late) instead of held in SGPRs throughout.
 // kFast: only the default paths (ordered 4-wide BVH walk, light-grid shadow
 // queries) are compiled in; the host picks it when the scene uses them.
+// The part of bounce() after the closest hit (bi, bt) is known: sky or
+// shading with the shadow queries, and the reflection decision.  Lanes with
+// alive = false take no part; it has no wave-wide operation that needs every
+// lane active (render_deferred_walk calls it for the lanes whose walk ended).
 template <bool kCull, bool kArgMem = false, bool kFast = false>
-__device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const double *__restrict__ rad,
-                                       const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
-                                       int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o, D3 d,
-                                       int key, int dleft, Work &work, unsigned &c_shadow, int &outcome, D3 &color,
-                                       double &refl, D3 &no, D3 &nd, int &nkey) {
+__device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                          const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
+                                          int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o,
+                                          D3 d, int key, int dleft, int bi, double bt, Work &work, unsigned &c_shadow,
+                                          int &outcome, D3 &color, double &refl, D3 &no, D3 &nd, int &nkey) {
   outcome = 0;
-  double bt;
-  RT_T0(t_cl);
-  const int bi =
-      sweep_closest<kCull, kFast>(g, rad, n, alive, o, d, key, kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt,
-                                  work);
-  RT_ACC(work, 8, t_cl);
   const bool hit = alive && bi >= 0;
   if (alive && !hit) {  // sky, main.cpp:26-30
     const double st = 0.5 * (d.y + 1.0);
@@ -269,6 +267,22 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
       outcome = kEnded;
     }
   }
+}
+
+template <bool kCull, bool kArgMem = false, bool kFast = false>
+__device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                       const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
+                                       int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o, D3 d,
+                                       int key, int dleft, Work &work, unsigned &c_shadow, int &outcome, D3 &color,
+                                       double &refl, D3 &no, D3 &nd, int &nkey) {
+  double bt;
+  RT_T0(t_cl);
+  const int bi =
+      sweep_closest<kCull, kFast>(g, rad, n, alive, o, d, key, kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt,
+                                  work);
+  RT_ACC(work, 8, t_cl);
+  shade_hit<kCull, kArgMem, kFast>(g, rad, mat, slight, n, nl, amb, bv, lg_arg, alive, o, d, key, dleft, bi, bt, work,
+                                   c_shadow, outcome, color, refl, no, nd, nkey);
 }
 
 // trace_ray for one camera ray per lane, the wave walking the levels together
@@ -899,6 +913,133 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
   flush_counts(kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters), sums, work);
 }
 
+// render_deferred for scenes with a BVH, with the walks decoupled from the
+// shading (kFast configuration).  A lane's closest-hit walk advances one node
+// or leaf per step (walk4_step); a lane whose walk ended waits, and the wave
+// shades once kShadeAt lanes are ready (or no lane is walking): shade_hit for
+// the ready lanes only, after which a spawned reflection ray starts its walk
+// and an ended chain stores its pixel and takes the next queued ray.  In
+// render_deferred a wave's walk lasts as long as its longest one (the
+// level >= 2 rays' walks are long-tailed: scripts/bvh_sim.cpp models 0.36 of
+// the lanes busy); here the lanes whose walks end early start the next ray's.
+// Same tests, same per-ray results: the closest hit of each ray is its
+// lexicographic (t, index) minimum (walk4_step, closest_test), shading and
+// the stack unwinding are render_deferred's.
+#ifndef RT_SHADE_AT
+#define RT_SHADE_AT 40
+#endif
+constexpr int kShadeAt = RT_SHADE_AT;
+template <bool kCull>
+__global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(const RenderArgs a) {
+  const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards, step = gridDim.x / kShards;
+  const int cap = a.dq_cap;
+  const unsigned long long cnt = a.counters[(size_t)shard * kShardStride + kDeferSlot];
+  const unsigned n_dq = (unsigned)(cnt < (unsigned long long)cap ? cnt : (unsigned long long)cap);
+  if (first * 64u >= n_dq) return;
+  const int lane = (int)(threadIdx.x & 63);
+  const unsigned npx_frame = (unsigned)((size_t)a.rows.count * a.od.xw);
+  const unsigned sstride = npx_frame * (unsigned)a.frames;
+  Work work;
+  unsigned c_shadow = 0, c_reflect = 0, c_neg = 0;
+  unsigned kk = 0;  // next stream entry (wave-uniform), as render_deferred
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  bool act = false, walking = false;
+  D3 o = mk(0.0, 0.0, 0.0), d = o;
+  int key = -1, dleft = 0, lev = 0;
+  unsigned pixg = 0;
+  // the walk of this lane's ray: pending reference and stack depth, the best
+  // hit so far (t, numerator, sphere) and the fp32 prune bound
+  int ref = 0, sp = 0, bi = -1;
+  double bt = kInf, bn = __builtin_inf();
+  float tmf = 0.0f;
+  auto prune = [&](const BvhArgs &bv) { return float_up(bt + 2e-6 * (bv.diam + __builtin_fabs(bt))); };
+  auto begin = [&](const BvhArgs &bv) {  // a new ray: an empty best, the root box
+    bt = kInf;
+    bn = __builtin_inf();
+    bi = -1;
+    tmf = prune(bv);
+    walking = walk4_begin(bv, walk4_ray(bv, o, d), tmf, ref, sp);
+  };
+  while (true) {
+    {
+      const unsigned long long idle = ~__ballot(act);
+      if (idle) {
+        const unsigned k = kk + (unsigned)__popcll(idle & lt);
+        const unsigned i = (first + (k >> 6) * step) * 64u + (k & 63u);
+        if (!act && i < n_dq) {
+          const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[(size_t)shard * (size_t)cap + i];
+          o = mk(e.ox, e.oy, e.oz);
+          d = mk(e.dx, e.dy, e.dz);
+          lev = e.orig;
+          dleft = e.dleft;
+          key = e.key;
+          pixg = (unsigned)e.pix;
+          act = true;
+          begin(kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv));
+        }
+        kk += (unsigned)__popcll(idle);
+      }
+    }
+    if (__ballot(act) == 0) break;
+    // walk until enough lanes are ready to shade (or no lane walks)
+    if (__ballot(walking)) {
+      const BvhArgs &bv = kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv);
+      const Walk4Ray r = walk4_ray(bv, o, d);
+      const double a4 = 4.0 * dot(d, d), a2 = 0.5 * a4;
+      const bool fast = a2_ok(a2);
+      const SphGeo *__restrict__ g = a.geo;
+      while (true) {
+        const unsigned long long wm = __ballot(walking);
+        if (wm == 0 || __popcll(__ballot(act) & ~wm) >= kShadeAt) break;
+        if (walking) {
+          auto leaf = [&](int i) {
+            work.exact += 1;
+            closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi);
+          };
+          walking = walk4_step(bv, r, [&] { return prune(bv); }, work, leaf, ref, sp, tmf);
+        }
+      }
+    }
+    const bool ready = act && !walking;
+    if (__ballot(ready)) {
+      int outcome = 0, nkey = 0;
+      D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
+      double refl = 0.0;
+      shade_hit<kCull, true, true>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, ready, o, d, key,
+                                   dleft, bi, bt, work, c_shadow, outcome, color, refl, no, nd, nkey);
+      bool spawned = false;
+      if (ready) {
+        StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, gstack)>(a.gstack);
+        if (outcome == kSpawned) {
+          gs[pixg + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
+          ++lev;
+          o = no;
+          d = nd;
+          key = nkey;
+          --dleft;
+          ++c_reflect;
+          spawned = true;
+        } else {
+          D3 res = color;
+          while (lev > 0) {  // main.cpp:54, innermost first
+            --lev;
+            const StackEnt e = gs[pixg + (unsigned)lev * sstride];
+            res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
+          }
+          const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
+          const unsigned f = pixg / npx_frame;
+          store_px(static_cast<uint8_t *>(od.ptr) + (size_t)f * (size_t)od.fstride, pixg - f * npx_frame, res, true,
+                   c_neg);
+          act = false;
+        }
+      }
+      if (spawned) begin(kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv));
+    }
+  }
+  unsigned long long sums[4] = {0ull, wave_sum(c_shadow), wave_sum(c_reflect), wave_sum(c_neg)};
+  flush_counts(kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters), sums, work);
+}
+
 // Reassemble rank-major shards into PPM row order (one workgroup per row).
 __global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                            int W, int H, int band, int G, int R) {
@@ -988,6 +1129,7 @@ struct rt_ctx {
   int samples = 1;  // 4: the antialias mode (rt_set_antialias)
   int stack_mode = 4;  // RT_HIP_STACK: 4 merged reflection levels (default), 1 per-pixel global stack (one tile per wave)
   bool defer = true;          // RT_HIP_DEFER: kStackMerge defers rays of level >= kDeferLevel to render_deferred
+  bool defer_walk = true;     // RT_HIP_DEFER_WALK: deferred rays of a scene whose closest hits always walk the BVH use render_deferred_walk
   int merge_q = 64;           // kStackMerge: the launch's LDS queue entries per wave (launch_render4 picks it)
   int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (16, 32 or 64)
   int defer_level = kDeferLevel;  // RT_HIP_DEFER_LEVEL (>= 1)
@@ -1301,7 +1443,12 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     else
       hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
     if (ra.dq_cap > 0) {  // 48 one-wave workgroups per shard segment
-      if (fast)
+      // the walk kernel where every closest hit walks the BVH anyway (large
+      // scenes: synth10k 12.2 -> 11.0 ms per 8-frame launch); small scenes keep
+      // the cull sweeps (synth200 1 % slower on the walk kernel)
+      if (fast && c->defer_walk && kCull && bv.nnodes > 0 && bv.always)
+        hipLaunchKernelGGL((render_deferred_walk<kCull>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
+      else if (fast)
         hipLaunchKernelGGL((render_deferred<kCull, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
       else
         hipLaunchKernelGGL((render_deferred<kCull>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
@@ -1428,6 +1575,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH4")) c->bvh_wide = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_DEFER_WALK")) c->defer_walk = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_LEVEL")) c->defer_level = std::max(1, std::min(RT_MAX_DEPTH, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(16, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(1024, std::atoi(e)));

@@ -350,16 +350,17 @@ def test_bvh_far_from_origin(bvh_renderer):
 @pytest.fixture(params=[{"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_SCHED": "0"}, {"RT_HIP_STACK": "1"},
                         {"RT_HIP_STACK": "1", "RT_HIP_SCHED": "0"}, {"RT_HIP_STACK": "4", "RT_HIP_LDS_SCENE": "1"},
                         {"RT_HIP_MERGE_Q": "16"}, {"RT_HIP_DEFER": "0"}, {"RT_HIP_DEFER_LEVEL": "1"},
-                        {"RT_HIP_DEFER_LEVEL": "3"}],
+                        {"RT_HIP_DEFER_LEVEL": "3"}, {"RT_HIP_DEFER_WALK": "0"}],
                 ids=["lds-scene", "scanline-order", "global-stack", "global-stack-scanline", "merge-lds-scene",
-                     "merge-queue-16", "no-defer", "defer-level-1", "defer-level-3"])
+                     "merge-queue-16", "no-defer", "defer-level-1", "defer-level-3", "defer-walk-off"])
 def stack_renderer(request, monkeypatch):
     """Non-default kernel layouts (RT_HIP_STACK=1: one tile per wave with the
     per-pixel global stack instead of merged levels; RT_HIP_LDS_SCENE=1:
     scenes that fit staged in LDS with 4-wave workgroups; RT_HIP_SCHED=0: tiles
     launched in scanline order instead of heaviest-predicted first;
     RT_HIP_MERGE_Q / RT_HIP_DEFER / RT_HIP_DEFER_LEVEL: merge-queue size and
-    the deferred-ray kernel)."""
+    the deferred-ray kernel; RT_HIP_DEFER_WALK=0: large scenes' deferred rays
+    through render_deferred instead of render_deferred_walk)."""
     import rt_hip
 
     for k, v in request.param.items():
@@ -400,14 +401,17 @@ def test_stack_modes_depth_edges(stack_renderer, depth):
             assert np.array_equal(got[k], want[y])
 
 
-@pytest.mark.parametrize("walk", [{}, {"RT_HIP_BVH4": "0"}, {"RT_HIP_BVH_ORDERED": "0"}],
-                         ids=["ordered4", "ordered2", "stackless"])
+@pytest.mark.parametrize("walk", [{}, {"RT_HIP_BVH4": "0"}, {"RT_HIP_BVH_ORDERED": "0"},
+                                  {"RT_HIP_DEFER_WALK": "0"}, {"RT_HIP_DEFER_LEVEL": "1"}],
+                         ids=["ordered4", "ordered2", "stackless", "defer-walk-off", "defer-walk-level-1"])
 @pytest.mark.parametrize("seed,count", [(101, 700), (102, 1100), (103, 1600)])
 def test_large_scenes_global_memory_paths(monkeypatch, walk, seed, count):
     """Scenes read through L2 with the BVH fallback: the ordered 4-wide walk
     (default), the ordered two-child walk (RT_HIP_BVH4=0) and the stackless
     preorder walk (RT_HIP_BVH_ORDERED=0) against the oracle; above 1024 spheres
-    every group walks the tree (256-cell shadow grids, 2-sphere leaves)."""
+    every group walks the tree (256-cell shadow grids, 2-sphere leaves) and the
+    deferred rays go through render_deferred_walk (RT_HIP_DEFER_WALK=0: through
+    render_deferred; RT_HIP_DEFER_LEVEL=1: every reflection ray through it)."""
     import orc
     import rt_hip
 
