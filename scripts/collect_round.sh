@@ -1,13 +1,14 @@
 #!/bin/bash
-# Copy a gpu_round_profile.sh result into profiles/$TAG and fold the PMC passes
-# into profiles/pmc_traffic.json.  Usage: TAG=r1_final bash scripts/collect_round.sh
+# Copy a scripts/gpu_profile.sh result (gpurun_out/prof_$TAG) into
+# profiles/$TAG and fold its PMC passes into profiles/pmc_traffic.json.
+#   TAG=r2e bash scripts/collect_round.sh
 set -e
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-TAG="${TAG:-r1}"
-SRC="$ROOT/gpurun_out/round_$TAG"
+TAG="${TAG:-r2}"
+SRC="$ROOT/gpurun_out/prof_$TAG"
 DST="$ROOT/profiles/$TAG"
 mkdir -p "$DST"
-cp "$SRC/bench.json" "$SRC/pytest_gpu.log" "$DST/"
+cp "$SRC/bench.json" "$DST/"
 cp "$SRC"/trace/run_kernel_stats.csv "$DST/kernel_stats.csv"
 python3 "$ROOT/scripts/prof_summary.py" "$SRC/trace/run_kernel_trace.csv" --labels synth200 > "$DST/trace_summary.json"
 cp "$SRC/trace_bench.json" "$DST/trace_bench.json"

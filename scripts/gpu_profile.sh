@@ -2,7 +2,7 @@
 # Round profile on one GPU: the default bench line, a rocprofv3 kernel trace of
 # the same command, and the PMC passes (scripts/pmc_r2_passes.txt, one
 # rocprofv3 run per pass) for each workload in $WORKLOADS.  Output under
-# gpurun_out/prof_$TAG/.  Each GPU step has its own time limit; the script stops
+# gpurun_out/prof_$TAG/ (then scripts/collect_round.sh).  Each GPU step has its own time limit; the script stops
 # at the first failing step.
 ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
 TAG="${TAG:-r2}"
