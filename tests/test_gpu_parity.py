@@ -430,3 +430,70 @@ def test_large_scenes_global_memory_paths(monkeypatch, walk, seed, count):
                                                                        counts["reflect"])
     finally:
         r.close()
+
+
+def _mirror_cloud(seed: int, n: int) -> str:
+    """A camera inside a cloud of mirrors: nearly every pixel reflects at least
+    twice, so the level-2 rays outnumber the deferred queue's room."""
+    import random
+
+    rng = random.Random(seed)
+    lines = []
+    for _ in range(n):
+        lines.append("sphere %.6f %.6f %.6f %.6f %.3f %.3f %.3f %.2f 0.5 %d" % (
+            rng.uniform(-14, 14), rng.uniform(-14, 14), rng.uniform(-14, 14), rng.uniform(0.6, 2.2),
+            rng.random(), rng.random(), rng.random(), rng.choice([0.8, 0.9, 1.0]), rng.choice([5, 20, 60])))
+    lines.append("light 0 30 0 1 1 1 1")
+    lines.append("light 20 -10 25 0.6 0.5 0.4 1")
+    lines.append("ambient 0.1 0.1 0.1")
+    lines.append("camera 0.3 0.2 0.1 5 1 -7 80")
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("n", [400, 1300], ids=["render_deferred", "render_deferred_walk"])
+def test_deferred_queue_overflow_vs_oracle(n):
+    """More level-2 rays than the deferred queue holds (room: 1/8 of the
+    launch's pixels): the rays that find their shard segment full continue in
+    the merged megakernel. Checked: the level-2 ray count exceeds the room; the
+    image and ray counts equal a render without deferral (RT_HIP_DEFER=0); every
+    31st row equals the oracle's.  n = 1300 takes the walk kernel
+    (render_deferred_walk), n = 400 render_deferred."""
+    import os
+
+    import orc
+    import rt_hip
+
+    W, H, D = 512, 384, 6
+    text = _mirror_cloud(7, n)
+    sc = rt_hip.Scene.parse(text)
+    r = rt_hip.Renderer(0)
+    try:
+        r.upload(sc)
+        _, st2 = r.render(sc.camera(), W, H, 2)
+        _, st3 = r.render(sc.camera(), W, H, 3)
+        assert st3.rays_reflect - st2.rays_reflect > W * H // 8
+        rgb, st = r.render(sc.camera(), W, H, D)
+    finally:
+        r.close()
+    old = os.environ.get("RT_HIP_DEFER")
+    os.environ["RT_HIP_DEFER"] = "0"
+    try:
+        r0 = rt_hip.Renderer(0)
+    finally:
+        if old is None:
+            del os.environ["RT_HIP_DEFER"]
+        else:
+            os.environ["RT_HIP_DEFER"] = old
+    try:
+        r0.upload(sc)
+        rgb0, st0 = r0.render(sc.camera(), W, H, D)
+    finally:
+        r0.close()
+    assert bytes(rgb) == bytes(rgb0), diff_summary(bytes(rgb), bytes(rgb0))
+    assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (st0.rays_primary, st0.rays_shadow,
+                                                                   st0.rays_reflect)
+    full = np.frombuffer(bytes(rgb), np.uint8).reshape(H, W, 3)
+    ref = orc.OracleScene(text=text)
+    for y in range(0, H, 31):
+        row, _, _ = ref.render(W, H, D, band=1, first=y, stride=1, count=1, threads=8)
+        assert full[y].tobytes() == row, f"row {y}"
