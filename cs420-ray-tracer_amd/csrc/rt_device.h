@@ -216,6 +216,37 @@ __device__ __forceinline__ double wmin(double v) {
   }
   return v;
 }
+// x rounded up to fp32 (the walks' prune bound: an entry t above it is above
+// x too).  NaN stays NaN (every comparison with it keeps the box).
+__device__ __forceinline__ float float_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) {  // one float up: f is finite here (x > f)
+    const int b = __float_as_int(f);
+    f = f == 0.0f ? 0x1p-149f : __int_as_float(f > 0.0f ? b + 1 : b - 1);
+  }
+  return f;
+}
+
+// An upper bound of the wave's maximum of a double, wave-uniform: each lane's
+// value rounded UP to fp32 (float_up; negatives count as 0, NaN stays NaN and
+// wins), reduced on the 32-bit patterns -- ordered like the values for
+// non-negative floats, NaN above +inf -- with DPP row shifts and broadcasts
+// (no LDS crossbar), the result read from lane 63.  Called only where all 64
+// lanes are active.
+__device__ __forceinline__ double wmax_up(double v) {
+  const float f = float_up(v);
+  unsigned b = f >= 0.0f ? __float_as_uint(f) : (f != f ? 0x7fc00000u : 0u);
+  auto step = [&](unsigned x) { b = x > b ? x : b; };
+  step((unsigned)__builtin_amdgcn_update_dpp(0, (int)b, 0x111, 0xf, 0xf, false));  // row_shr:1
+  step((unsigned)__builtin_amdgcn_update_dpp(0, (int)b, 0x112, 0xf, 0xf, false));  // row_shr:2
+  step((unsigned)__builtin_amdgcn_update_dpp(0, (int)b, 0x113, 0xf, 0xf, false));  // row_shr:3
+  step((unsigned)__builtin_amdgcn_update_dpp(0, (int)b, 0x114, 0xf, 0xe, false));  // row_shr:4, banks 1-3
+  step((unsigned)__builtin_amdgcn_update_dpp(0, (int)b, 0x118, 0xf, 0xc, false));  // row_shr:8, banks 2-3
+  step((unsigned)__builtin_amdgcn_update_dpp(0, (int)b, 0x142, 0xa, 0xf, false));  // row_bcast:15, rows 1, 3
+  step((unsigned)__builtin_amdgcn_update_dpp(0, (int)b, 0x143, 0xc, 0xf, false));  // row_bcast:31, rows 2, 3
+  return (double)__uint_as_float(__builtin_amdgcn_readlane(b, 63));
+}
+
 // Make a wave-uniform double live in SGPRs (the value is identical in every lane).
 __device__ __forceinline__ double uni(double v) {
   unsigned long long b = __double_as_longlong(v);
@@ -274,8 +305,8 @@ __device__ __forceinline__ Bound make_bound(bool act, D3 o, D3 d, D3 P) {
   double slack = act ? (__builtin_fabs(pc.x) + __builtin_fabs(pc.y) + __builtin_fabs(pc.z)) * (1.0 + 1e-9) +
                            1e-6 * (__builtin_fabs(po.x) + __builtin_fabs(po.y) + __builtin_fabs(po.z))
                      : 0.0;
-  const double s2max = uni(wmax(s2));
-  B.slack = uni(wmax(slack));
+  const double s2max = wmax_up(s2);
+  B.slack = wmax_up(slack);
   B.px = uni(P.x);
   B.py = uni(P.y);
   B.pz = uni(P.z);
@@ -536,17 +567,6 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
     }
     if (!more) return;
   }
-}
-
-// x rounded up to fp32 (the walks' prune bound: an entry t above it is above
-// x too).  NaN stays NaN (every comparison with it keeps the box).
-__device__ __forceinline__ float float_up(double x) {
-  float f = (float)x;
-  if ((double)f < x) {  // one float up: f is finite here (x > f)
-    const int b = __float_as_int(f);
-    f = f == 0.0f ? 0x1p-149f : __int_as_float(f > 0.0f ? b + 1 : b - 1);
-  }
-  return f;
 }
 
 // Ordered closest-hit walk over the 4-wide nodes (rt_bvh.h BvhNode4): the
