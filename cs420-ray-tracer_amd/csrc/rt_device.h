@@ -98,6 +98,41 @@ __device__ __forceinline__ D3 normalized(D3 a) {
   double len = length(a);
   return div3(a, len);  // vec3.h:26-29: x/len, y/len, z/len
 }
+// normalized(a), bit-identical, with a fast path for |a| within a few ulps of
+// 1 -- the renderer normalises already-normalised directions again (Ray()'s
+// constructor, ray.h:12: the camera ray and the shadow direction, scene.h:72)
+// and reflections of unit vectors (main.cpp:46).  With u = 2^-53 and
+// s = (x*x + y*y) + z*z (length()'s sum, same order), s - 1 is exact near 1
+// and s = 1 + t u with t in {-4..0} or {2, 4, 6} (the grid spacing is u below
+// 1, 2u above).  sqrt(1 + t u) = 1 + t u / 2 - O(u^2), so the correctly
+// rounded length is 1 - ceil(-t/2) u below 1 (an odd -t is a midpoint minus
+// the O(u^2) term: it rounds away from 1) and 1 + 2 floor(t/4) u above:
+//   t in {0, 2} -> len 1;  {-1, -2} -> 1 - u;  {-3, -4} -> 1 - 2u;  {4, 6} -> 1 + 2u.
+// Each quotient x / len is then Markstein's correction with the correctly
+// rounded reciprocal rcp = RN(1/len) (1, 1 + 2u, 1 + 2u, 1 - 2u):
+// q0 = x rcp, r = fma(-q0, len, x) (exact), q = fma(r, rcp, q0) = RN(x / len)
+// -- valid while nothing underflows (|x| >= 2^-959); copysign keeps the sign
+// of a zero numerator (x = -0 gives -0, as -0 / len).  Checked against IEEE
+// division for 500 M numerators over the exponent range and at binade edges
+// and for random, reflected and perturbed vectors (tests/native/renorm_check.cpp).
+// Any other length, a tiny component or a NaN takes normalized().
+__device__ __forceinline__ D3 renormalized(D3 a) {
+  constexpr double u = 0x1p-53;
+  const double s = (a.x * a.x + a.y * a.y) + a.z * a.z;
+  const double t = (s - 1.0) * 0x1p53;
+  auto usable = [](double x) { return __builtin_fabs(x) >= 0x1p-959 || x == 0.0; };
+  if (__builtin_expect(t >= -4.0 && t <= 6.0 && usable(a.x) && usable(a.y) && usable(a.z), 1)) {
+    const double len = t > 3.0 ? 1.0 + 2.0 * u : (t > -0.5 ? 1.0 : (t > -2.5 ? 1.0 - u : 1.0 - 2.0 * u));
+    const double rcp = t > 3.0 ? 1.0 - 2.0 * u : (t > -0.5 ? 1.0 : 1.0 + 2.0 * u);
+    auto q = [&](double x) {
+      const double q0 = x * rcp;
+      return __builtin_copysign(__builtin_fma(__builtin_fma(-q0, len, x), rcp, q0), x);
+    };
+    return mk(q(a.x), q(a.y), q(a.z));
+  }
+  return normalized(a);
+}
+
 // ocml's fp64 pow needs ~50 VGPRs when inlined into the render loop; called
 // out of line it only adds its own frame where little of the caller is live.
 __device__ __attribute__((noinline)) double pow_call(double x, double y) { return pow(x, y); }

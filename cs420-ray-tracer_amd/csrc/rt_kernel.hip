@@ -210,8 +210,10 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
 #endif
 #if RT_ABL == 4  // ablation: shadow rays without the second normalisation / offset
           const D3 so = hp, sd = ldir;
+#elif RT_ABL == 13  // ablation (not exact): shadow rays without the second normalisation
+          const D3 so = add(hp, scale(ldir, kEps)), sd = ldir;
 #else
-          const D3 so = add(hp, scale(ldir, kEps)), sd = normalized(ldir);
+          const D3 so = add(hp, scale(ldir, kEps)), sd = renormalized(ldir);
 #endif
           if constexpr (kFast)
             occ = shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi);
@@ -257,7 +259,7 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
         const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));
         const D3 rd = sub(d, scale(scale(nrm, 2.0), dot(d, nrm)));
         no = add(hp, scale(nrm, kEps));
-        nd = normalized(rd);
+        nd = renormalized(rd);
         nkey = hi;
         refl = m.refl;
         outcome = kSpawned;
@@ -381,7 +383,7 @@ __device__ __forceinline__ void trace_tile(const SphGeo *__restrict__ g, const d
     const double su = ((u - 0.5) * cam.scale) * 1.0, sv = (v - 0.5) * cam.scale;
     const D3 dir = add(add(mk(cam.fx, cam.fy, cam.fz), scale(mk(cam.rx, cam.ry, cam.rz), su)),
                        scale(mk(cam.ux, cam.uy, cam.uz), sv));
-    const D3 d = normalized(normalized(dir));  // get_ray normalises, Ray() normalises again
+    const D3 d = renormalized(normalized(dir));  // get_ray normalises, Ray() normalises again
     const D3 o = mk(cam.px, cam.py, cam.pz);
     const int pix = k * od.xw + (x - od.x0);
     const D3 c = trace_wave<kCull, kArgMem, kArgMem>(g, rad, mat, slight, n, nl, amb, depth, bv, lg, in_img, o, d,
@@ -577,7 +579,11 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         const double su = ((u - 0.5) * cam.scale) * 1.0, sv = (v - 0.5) * cam.scale;
         const D3 dir = add(add(mk(cam.fx, cam.fy, cam.fz), scale(mk(cam.rx, cam.ry, cam.rz), su)),
                            scale(mk(cam.ux, cam.uy, cam.uz), sv));
-        d = normalized(normalized(dir));
+#if RT_ABL == 13
+        d = normalized(dir);
+#else
+        d = renormalized(normalized(dir));
+#endif
         o = mk(cam.px, cam.py, cam.pz);
         pix = (unsigned)(k * W + x);
         key = -1;
