@@ -1105,8 +1105,7 @@ struct rt_ctx {
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
   double rmax = 0;
   int bvh_min = 24, bvh_on = 1, bvh_groups = 2, bvh_leaf = 4;
-  // RT_HIP_BVH_LEAF; 0 = 4, or 2 above kBvhAlwaysAbove spheres (synth10k: with
-  // the 256 grid 6.95 -> 6.46 ms; neither helps synth200)
+  // RT_HIP_BVH_LEAF; 0 = 2, or 1 above kBvhAlwaysAbove spheres (rt_upload_scene)
   int bvh_leaf_opt = 0;
   // -1 (auto): every group walks the BVH when the scene has more than
   // kBvhAlwaysAbove spheres (a linear cull sweep is O(n) per group)
@@ -1709,7 +1708,9 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     br[i] = s->spheres[i].radius;
   }
   const bool big = n > kBvhAlwaysAbove;
-  c->bvh_leaf = c->bvh_leaf_opt ? c->bvh_leaf_opt : 2;  // 2 measured +0.6..0.9 % over 4 with the merged levels
+  // leaves of 2 spheres (+0.6..0.9 % over 4 on synth200 with the merged levels);
+  // 1 above kBvhAlwaysAbove, where every closest hit walks (synth10k 4.37 -> 4.16 ms)
+  c->bvh_leaf = c->bvh_leaf_opt ? c->bvh_leaf_opt : (big ? 1 : 2);
   c->lg_n = c->lg_n_opt ? c->lg_n_opt : (big ? 384 : 128);
   std::vector<BvhNode> nodes;
   std::vector<int32_t> prims;

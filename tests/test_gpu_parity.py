@@ -409,7 +409,7 @@ def test_large_scenes_global_memory_paths(monkeypatch, walk, seed, count):
     """Scenes read through L2 with the BVH fallback: the ordered 4-wide walk
     (default), the ordered two-child walk (RT_HIP_BVH4=0) and the stackless
     preorder walk (RT_HIP_BVH_ORDERED=0) against the oracle; above 1024 spheres
-    every group walks the tree (256-cell shadow grids, 2-sphere leaves) and the
+    every group walks the tree (384-cell shadow grids, 1-sphere leaves) and the
     deferred rays go through render_deferred_walk (RT_HIP_DEFER_WALK=0: through
     render_deferred; RT_HIP_DEFER_LEVEL=1: every reflection ray through it)."""
     import orc
