@@ -935,7 +935,6 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
 #define RT_SHADE_AT 40
 #endif
 constexpr int kShadeAt = RT_SHADE_AT;
-template <bool kCull>
 __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(const RenderArgs a) {
   const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards, step = gridDim.x / kShards;
   const int cap = a.dq_cap;
@@ -1011,7 +1010,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
       int outcome = 0, nkey = 0;
       D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
       double refl = 0.0;
-      shade_hit<kCull, true, true>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, ready, o, d, key,
+      shade_hit<true, true, true>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, ready, o, d, key,
                                    dleft, bi, bt, work, c_shadow, outcome, color, refl, no, nd, nkey);
       bool spawned = false;
       if (ready) {
@@ -1451,8 +1450,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       // the walk kernel where every closest hit walks the BVH anyway (large
       // scenes: synth10k 12.2 -> 11.0 ms per 8-frame launch); small scenes keep
       // the cull sweeps (synth200 1 % slower on the walk kernel)
-      if (fast && c->defer_walk && kCull && bv.nnodes > 0 && bv.always)
-        hipLaunchKernelGGL((render_deferred_walk<kCull>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
+      if (kCull && fast && c->defer_walk && bv.nnodes > 0 && bv.always)
+        hipLaunchKernelGGL(render_deferred_walk, dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
       else if (fast)
         hipLaunchKernelGGL((render_deferred<kCull, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
       else
