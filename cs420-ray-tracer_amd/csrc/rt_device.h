@@ -1170,11 +1170,39 @@ struct LgArgs {
 struct LgRange {
   int cb, ce;
 };
+// lg_cell (rt_lightgrid.h) with the two quotients p/m, q/m formed as p * rcp(m)
+// (v_rcp_f32, within 1 ulp): each within 2^-22 relative of the IEEE
+// quotient, an angle error far inside the grids' 4e-6 rad slack;
+// tests/native/lg_check.cpp checks the lists against cells binned with
+// +-2^-22 quotient errors.
+__device__ __forceinline__ int lg_cell_rcp(float ux, float uy, float uz, int N) {
+  const float ax = __builtin_fabsf(ux), ay = __builtin_fabsf(uy), az = __builtin_fabsf(uz);
+  int face;
+  float m, p, q;
+  if (ax >= ay && ax >= az) {
+    face = ux >= 0 ? 0 : 1;
+    m = ax, p = uy, q = uz;
+  } else if (ay >= az) {
+    face = uy >= 0 ? 2 : 3;
+    m = ay, p = ux, q = uz;
+  } else {
+    face = uz >= 0 ? 4 : 5;
+    m = az, p = ux, q = uy;
+  }
+  if (!(m > 1e-30f) || !(m <= 3.4e38f) || p != p || q != q) return -1;
+  const float r = __builtin_amdgcn_rcpf(m);
+  const float fa = (p * r + 1.0f) * 0.5f * (float)N, fb = (q * r + 1.0f) * 0.5f * (float)N;
+  int i = (int)(fa < 0.f ? 0.f : fa), j = (int)(fb < 0.f ? 0.f : fb);
+  i = i > N - 1 ? N - 1 : i;
+  j = j > N - 1 ? N - 1 : j;
+  return (face * N + j) * N + i;
+}
+
 __device__ __forceinline__ LgRange lg_range(const LgArgs &lg, int l, D3 hp, D3 lp, bool act) {
   LgRange r{0, 0};
   if (act) {
     const int N = lg.N, cells = 6 * N * N;
-    const int c = lg_cell((float)(hp.x - lp.x), (float)(hp.y - lp.y), (float)(hp.z - lp.z), N);
+    const int c = lg_cell_rcp((float)(hp.x - lp.x), (float)(hp.y - lp.y), (float)(hp.z - lp.z), N);
     if (c < 0) {
       r.cb = -1;
     } else {

@@ -34,7 +34,7 @@ constexpr double kLgSlack = 4e-6;
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
-inline int lg_cell(float ux, float uy, float uz, int N) {
+inline int lg_cell(float ux, float uy, float uz, int N, float rel = 0.0f) {
   const float ax = ux < 0 ? -ux : ux, ay = uy < 0 ? -uy : uy, az = uz < 0 ? -uz : uz;
   int face;
   float m, p, q;
@@ -49,7 +49,10 @@ inline int lg_cell(float ux, float uy, float uz, int N) {
     m = az, p = ux, q = uy;
   }
   if (!(m > 1e-30f) || !(m <= 3.4e38f) || p != p || q != q) return -1;
-  const float fa = (p / m + 1.0f) * 0.5f * (float)N, fb = (q / m + 1.0f) * 0.5f * (float)N;
+  // rel: a relative error of the quotients (0 here; tests/native/lg_check.cpp
+  // bins with +-2^-22 too, the device's rcp-based quotients, lg_cell_rcp)
+  const float fa = ((p / m) * (1.0f + rel) + 1.0f) * 0.5f * (float)N,
+              fb = ((q / m) * (1.0f + rel) + 1.0f) * 0.5f * (float)N;
   int i = (int)(fa < 0.f ? 0.f : fa), j = (int)(fb < 0.f ? 0.f : fb);
   i = i > N - 1 ? N - 1 : i;
   j = j > N - 1 ? N - 1 : j;

@@ -94,12 +94,19 @@ int main(int argc, char **argv) {
       const double off = std::fabs(w.y * sd.z - w.z * sd.y) + std::fabs(w.z * sd.x - w.x * sd.z) +
                          std::fabs(w.x * sd.y - w.y * sd.x);
       if (!(off <= max_off)) continue;  // the device tests every sphere for such rays
+      // the device bins with quotients within 2^-22 of the IEEE ones (lg_cell_rcp):
+      // a sphere must be listed in the cell of every such binning
       const int c = rtk::lg_cell((float)-sd.x, (float)-sd.y, (float)-sd.z, N);
+      const int cm = rtk::lg_cell((float)-sd.x, (float)-sd.y, (float)-sd.z, N, -0x1p-22f);
+      const int cp = rtk::lg_cell((float)-sd.x, (float)-sd.y, (float)-sd.z, N, 0x1p-22f);
       if (c < 0) continue;
       const int32_t *st = start.data() + (size_t)l * (cells + 2);
-      std::vector<char> listed(n, 0);
+      std::vector<char> listed(n, 0), in_c(n, 0), in_m(n, 0), in_p(n, 0);
+      for (int k = st[c]; k < st[c + 1]; k++) in_c[ids[k]] = 1;
+      for (int k = st[cm]; k < st[cm + 1]; k++) in_m[ids[k]] = 1;
+      for (int k = st[cp]; k < st[cp + 1]; k++) in_p[ids[k]] = 1;
+      for (int i = 0; i < n; i++) listed[i] = in_c[i] && in_m[i] && in_p[i];
       for (int k = st[cells]; k < st[cells + 1]; k++) listed[ids[k]] = 1;
-      for (int k = st[c]; k < st[c + 1]; k++) listed[ids[k]] = 1;
       queries++;
       for (int i = 0; i < n; i++) {
         double t;
