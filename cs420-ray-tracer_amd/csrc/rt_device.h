@@ -114,8 +114,7 @@ __device__ __forceinline__ D3 normalized(D3 a) {
 // -- valid while nothing underflows (|x| >= 2^-959); copysign keeps the sign
 // of a zero numerator (x = -0 gives -0, as -0 / len).  Checked against IEEE
 // division for 500 M numerators over the exponent range and at binade edges
-// and for random, reflected and perturbed vectors (tests/native/renorm_check.cpp
-// on the host, tests/native/renorm_gpu_check.hip on the device).
+// and for random, reflected and perturbed vectors (tests/native/renorm_check.cpp).
 // Any other length, a tiny component or a NaN takes normalized().
 __device__ __forceinline__ D3 renormalized(D3 a) {
   constexpr double u = 0x1p-53;
