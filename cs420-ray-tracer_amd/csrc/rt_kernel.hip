@@ -489,6 +489,9 @@ constexpr int kDeferLevel = RT_DEFER_LEVEL;
 #define RT_DEFER_CAP_DIV 8  // deferred-queue room: 1 / RT_DEFER_CAP_DIV of the launch's pixels
 #endif
 constexpr int kDeferSlot = 7;
+// u64 slot of a counter shard: the deferred kernels' next queue entry of that
+// shard segment (lanes take entries dynamically; zeroed with the launch's counters)
+constexpr int kFetchSlot = 24;
 constexpr long long kSchedMinTiles = 1024;  // launches with fewer 8x8 tiles keep scanline order
 
 // Stores a pixel's final colour (quantised as write_ppm, main.cpp:85) at out + 3 pix.
@@ -827,7 +830,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
 // levels merge_tiles wrote first -- and stores the pixel.
 template <bool kCull, bool kFast = false>
 __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const RenderArgs a) {
-  const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards, step = gridDim.x / kShards;
+  const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards;
   const int cap = a.dq_cap;
   const unsigned long long cnt = a.counters[(size_t)shard * kShardStride + kDeferSlot];
   const unsigned n_dq = (unsigned)(cnt < (unsigned long long)cap ? cnt : (unsigned long long)cap);
@@ -837,22 +840,26 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
   const unsigned sstride = npx_frame * (unsigned)a.frames;
   Work work;
   unsigned c_shadow = 0, c_reflect = 0, c_neg = 0;
-  // This workgroup's entries, in order: chunk first, first + step, ...; entry
-  // k of that stream is queue index (first + (k / 64) * step) * 64 + k % 64.
-  // A lane whose chain ends takes the stream's next entry, so the wave stays
-  // full until the stream runs out instead of finishing each chunk's longest
-  // chain with its other lanes idle.
-  unsigned kk = 0;  // next stream entry (wave-uniform)
+  // Lanes without a ray take the shard segment's next entries (one
+  // wave-aggregated atomic on its fetch slot), so the wave stays full until
+  // the segment runs out and the workgroups of a segment finish together
+  // instead of each finishing its own static stream's longest chains.
   const unsigned long long lt = (1ull << lane) - 1ull;
-  bool act = false;
+  bool act = false, more = true;
   D3 o = mk(0.0, 0.0, 0.0), d = o;
   int key = -1, dleft = 0, lev = 0;
   unsigned pixg = 0;
+  unsigned long long *fetch = kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters) +
+                              (size_t)shard * kShardStride + kFetchSlot;
   while (true) {
     const unsigned long long idle = ~__ballot(act);
-    if (idle) {
-      const unsigned k = kk + (unsigned)__popcll(idle & lt);
-      const unsigned i = (first + (k >> 6) * step) * 64u + (k & 63u);
+    if (idle && more) {
+      const int fi = __builtin_ctzll(idle);
+      unsigned long long base = 0;
+      if (lane == fi) base = atomicAdd(fetch, (unsigned long long)__popcll(idle));
+      base = __shfl(base, fi, 64);
+      const unsigned long long i = base + (unsigned long long)__popcll(idle & lt);
+      more = base + (unsigned long long)__popcll(idle) < n_dq;
       if (!act && i < n_dq) {
         const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[(size_t)shard * (size_t)cap + i];
         o = mk(e.ox, e.oy, e.oz);
@@ -863,7 +870,6 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
         pixg = (unsigned)e.pix;
         act = true;
       }
-      kk += (unsigned)__popcll(idle);
     }
     if (__ballot(act) == 0) break;
     {
@@ -936,7 +942,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
 #endif
 constexpr int kShadeAt = RT_SHADE_AT;
 __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(const RenderArgs a) {
-  const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards, step = gridDim.x / kShards;
+  const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards;
   const int cap = a.dq_cap;
   const unsigned long long cnt = a.counters[(size_t)shard * kShardStride + kDeferSlot];
   const unsigned n_dq = (unsigned)(cnt < (unsigned long long)cap ? cnt : (unsigned long long)cap);
@@ -946,9 +952,10 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
   const unsigned sstride = npx_frame * (unsigned)a.frames;
   Work work;
   unsigned c_shadow = 0, c_reflect = 0, c_neg = 0;
-  unsigned kk = 0;  // next stream entry (wave-uniform), as render_deferred
   const unsigned long long lt = (1ull << lane) - 1ull;
-  bool act = false, walking = false;
+  bool act = false, walking = false, more = true;
+  unsigned long long *fetch = kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters) +
+                              (size_t)shard * kShardStride + kFetchSlot;  // as render_deferred
   D3 o = mk(0.0, 0.0, 0.0), d = o;
   int key = -1, dleft = 0, lev = 0;
   unsigned pixg = 0;
@@ -968,9 +975,13 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
   while (true) {
     {
       const unsigned long long idle = ~__ballot(act);
-      if (idle) {
-        const unsigned k = kk + (unsigned)__popcll(idle & lt);
-        const unsigned i = (first + (k >> 6) * step) * 64u + (k & 63u);
+      if (idle && more) {
+        const int fi = __builtin_ctzll(idle);
+        unsigned long long base = 0;
+        if (lane == fi) base = atomicAdd(fetch, (unsigned long long)__popcll(idle));
+        base = __shfl(base, fi, 64);
+        const unsigned long long i = base + (unsigned long long)__popcll(idle & lt);
+        more = base + (unsigned long long)__popcll(idle) < n_dq;
         if (!act && i < n_dq) {
           const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[(size_t)shard * (size_t)cap + i];
           o = mk(e.ox, e.oy, e.oz);
@@ -982,7 +993,6 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
           act = true;
           begin(kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv));
         }
-        kk += (unsigned)__popcll(idle);
       }
     }
     if (__ballot(act) == 0) break;
