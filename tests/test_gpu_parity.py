@@ -497,3 +497,21 @@ def test_deferred_queue_overflow_vs_oracle(n):
     for y in range(0, H, 31):
         row, _, _ = ref.render(W, H, D, band=1, first=y, stride=1, count=1, threads=8)
         assert full[y].tobytes() == row, f"row {y}"
+
+
+def test_cfg5_synth10k_4k_sampled_oracle_rows(gpu_renderer):
+    """BASELINE cfg 5 at its full size (synth10k 3840x2160 d6, the BVH walks,
+    384-cell shadow grids and render_deferred_walk): three rows through the
+    sphere cloud equal the oracle's."""
+    import orc
+    import rt_hip
+
+    W, H, D = 3840, 2160, 6
+    sc = rt_hip.Scene.load(scene_path("synth10k"))
+    gpu_renderer.upload(sc)
+    full, _ = gpu_renderer.render(sc.camera(), W, H, D)
+    full = np.frombuffer(bytes(full), np.uint8).reshape(H, W, 3)
+    ref = orc.OracleScene(scene_path("synth10k"))
+    for y in (H // 3, H // 2, (2 * H) // 3):
+        rgb, _, _ = ref.render(W, H, D, band=1, first=y, stride=1, count=1, threads=16)
+        assert full[y].tobytes() == rgb, f"row {y}"
