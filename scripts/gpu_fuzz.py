@@ -1,0 +1,76 @@
+"""Randomised parity sweep (a design/validation tool, not a test): random
+scenes -- 1 to 1,500 spheres (so both the cull sweeps and the always-BVH
+paths, render_deferred and render_deferred_walk), tiny to huge radii, mirror
+clouds, 0 to 6 lights, cameras inside spheres -- rendered on cuda:0 through
+the C-ABI at small sizes and random depths, against the oracle byte for byte
+and ray count for ray count.  Prints one line per scene and a summary; exits
+non-zero on the first mismatch.
+  python scripts/gpu_fuzz.py [SECONDS] [SEED]"""
+import os
+import random
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "cs420-ray-tracer_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import orc  # noqa: E402  (the checker)
+import rt_hip  # noqa: E402
+
+
+def scene(rng):
+    n = rng.choice([1, 2, 5, 30, 200, 700, 1100, 1500])
+    spread = rng.choice([0.5, 5.0, 20.0, 1000.0])
+    mirror = rng.random() < 0.3
+    lines = []
+    for _ in range(n):
+        r = rng.choice([1e-3, 0.05, 0.3, 1.0, 4.0]) * rng.uniform(0.5, 1.5) * spread / 10
+        refl = rng.choice([0.8, 0.9, 1.0]) if mirror else rng.choice([0.0, 0.0, 0.3, 0.7, 1.0])
+        lines.append("sphere %.9g %.9g %.9g %.9g %.3f %.3f %.3f %.2f 0.5 %d" % (
+            rng.uniform(-spread, spread), rng.uniform(-spread, spread), rng.uniform(-3 * spread, spread), r,
+            rng.random(), rng.random(), rng.random(), refl, rng.choice([0, 1, 5, 20, 100, 200])))
+    for _ in range(rng.randint(0, 6)):
+        lines.append("light %.6g %.6g %.6g %.3f %.3f %.3f 1" % (
+            rng.uniform(-2 * spread, 2 * spread), rng.uniform(-spread, 3 * spread), rng.uniform(-3 * spread, spread),
+            rng.random(), rng.random(), rng.random()))
+    lines.append("ambient %.3f %.3f %.3f" % (rng.random() * 0.3, rng.random() * 0.3, rng.random() * 0.3))
+    cam = [rng.uniform(-spread, spread) * 0.3 for _ in range(3)]
+    look = [rng.uniform(-spread, spread) * 0.5, rng.uniform(-spread, spread) * 0.5, -2 * spread]
+    lines.append("camera %.6g %.6g %.6g %.6g %.6g %.6g %d" % (*cam, *look, rng.choice([20, 45, 60, 90, 140])))
+    return "\n".join(lines) + "\n"
+
+
+def main():
+    budget = float(sys.argv[1]) if len(sys.argv) > 1 else 300.0
+    rng = random.Random(int(sys.argv[2]) if len(sys.argv) > 2 else 20261016)
+    r = rt_hip.Renderer(0)
+    t0, k, px = time.time(), 0, 0
+    try:
+        while time.time() - t0 < budget:
+            text = scene(rng)
+            W, H, D = rng.choice([(1, 1), (7, 5), (64, 48), (96, 64), (160, 90)]) + (rng.choice([0, 1, 2, 4, 8]),)
+            sc = rt_hip.Scene.parse(text)
+            r.upload(sc)
+            rgb, st = r.render(sc.camera(), W, H, D)
+            ref, cnt, _ = orc.OracleScene(text=text).render(W, H, D, threads=16)
+            ok = bytes(rgb) == ref and (st.rays_primary, st.rays_shadow, st.rays_reflect) == (
+                cnt["primary"], cnt["shadow"], cnt["reflect"])
+            k += 1
+            px += W * H
+            if not ok:
+                bad = sum(a != b for a, b in zip(bytes(rgb), ref))
+                print("MISMATCH scene %d (%dx%d d%d, %d spheres): %d bytes differ" % (
+                    k, W, H, D, sc.num_spheres, bad), flush=True)
+                with open(os.path.join(REPO, "gpurun_out", "fuzz_mismatch.txt"), "w") as f:
+                    f.write("%d %d %d\n%s" % (W, H, D, text))
+                return 1
+            if k % 25 == 0:
+                print("%d scenes ok (%d pixels), %.0f s" % (k, px, time.time() - t0), flush=True)
+    finally:
+        r.close()
+    print("fuzz: %d scenes, %d pixels, all byte-identical to the oracle" % (k, px))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
