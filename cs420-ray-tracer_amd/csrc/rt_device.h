@@ -1316,6 +1316,53 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
   return act && occ;
 }
 
+// Closest hit of camera rays through the camera grid (rt_lightgrid.h
+// build_point_grid): the rays leave the grid's point P exactly, so every
+// sphere the reference's test can report lies on the list of the cell of d;
+// the list ascends by a lower bound of the sphere's t, so the scan stops at
+// the first entry whose bound exceeds the best t found so far (every later
+// entry can only give a larger t: no strict-< win, no tie).  The result is
+// the lexicographic (t, index) minimum over all spheres, as sweep_closest's.
+// A lane whose direction cannot be binned tests every sphere.
+struct CgArgs {
+  const int32_t *start;  // [6N^2 + 1]
+  const int2 *ent;       // (sphere, tlo bits)
+  int N;
+  int on;  // the launch's frames all share the grid's camera position
+};
+__device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d,
+                                           const CgArgs &cg, double &best_t, Work &work) {
+  const double a = dot(d, d);
+  const double a4 = 4.0 * a, a2 = 2.0 * a;
+  double bt = kInf, bn = __builtin_inf();
+  int bi = -1;
+  const bool fast = a2_ok(a2);
+  int cb = 0, len = 0;
+  bool all = false;
+  if (act) {
+    const int c = lg_cell_rcp((float)d.x, (float)d.y, (float)d.z, cg.N);
+    if (c < 0) {
+      all = true;
+      len = n;
+    } else {
+      cb = cg.start[c];
+      len = cg.start[c + 1] - cb;
+    }
+  }
+  int k = 0;
+  int2 e = (len > 0 && !all) ? cg.ent[cb] : make_int2(0, (int)0xff800000u);  // -inf
+  while (k < len) {
+    const int i = all ? k : e.x;
+    if ((double)__int_as_float(e.y) > bt) break;
+    ++k;
+    if (k < len && !all) e = cg.ent[cb + k];  // the next entry, loaded during this test
+    work.exact += 1;
+    closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi);
+  }
+  best_t = bt;
+  return bi;
+}
+
 struct Cam {
   double px, py, pz, fx, fy, fz, rx, ry, rz, ux, uy, uz, scale;
 };

@@ -85,6 +85,7 @@ struct RenderArgs {
   Rows rows;
   BvhArgs bv;
   LgArgs lg;
+  CgArgs cg;  // camera grid of the launch's (shared) camera position; cg.on = 0: none
   OutDesc od;
   StackEnt *gstack;
   unsigned long long *counters;
@@ -276,12 +277,22 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
                                        const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                        int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o, D3 d,
                                        int key, int dleft, Work &work, unsigned &c_shadow, int &outcome, D3 &color,
-                                       double &refl, D3 &no, D3 &nd, int &nkey) {
-  double bt;
+                                       double &refl, D3 &no, D3 &nd, int &nkey, bool cam_pass = false) {
+  double bt = kInf;
   RT_T0(t_cl);
-  const int bi =
-      sweep_closest<kCull, kFast>(g, rad, n, alive, o, d, key, kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt,
-                                  work);
+  int bi = -1;
+  // cam_pass (kFast merged kernels, wave-uniform): every alive lane holds a
+  // camera ray of a frame whose position is the camera grid's point
+  bool swept = false;
+  if constexpr (kFast && kArgMem) {
+    if (cam_pass) {
+      bi = cam_closest(g, n, alive, o, d, kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{}), bt, work);
+      swept = true;
+    }
+  }
+  if (!swept)
+    bi = sweep_closest<kCull, kFast>(g, rad, n, alive, o, d, key, kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv),
+                                     bt, work);
   RT_ACC(work, 8, t_cl);
   shade_hit<kCull, kArgMem, kFast>(g, rad, mat, slight, n, nl, amb, bv, lg_arg, alive, o, d, key, dleft, bi, bt, work,
                                    c_shadow, outcome, color, refl, no, nd, nkey);
@@ -610,7 +621,8 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
     double refl = 0.0;
     bounce<kCull, true, kFast>(g, rad, mat, slight, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft, work,
-                               c_shadow, outcome, color, refl, no, nd, nkey);
+                               c_shadow, outcome, color, refl, no, nd, nkey,
+                               kFast && tile_pass && kernarg_late<true, offsetof(RenderArgs, cg)>(a.cg).on);
     const unsigned sidx = pix + ca.fpx;
     bool defer = false;
     if (act) {
@@ -1110,6 +1122,20 @@ struct rt_ctx {
   int lg_n = 128, lg_on = 1;  // lg_n: the grid of the uploaded scene
   int lg_n_opt = 0;            // RT_HIP_SHADOW_GRID_N; 0 = 128, or 384 above kBvhAlwaysAbove spheres
   double lg_max_off = 0.0;
+  // camera grid (rt_lightgrid.h build_point_grid): the closest hit of camera
+  // rays in the merged kFast kernels, built per camera position and cached
+  int cg_mode = 1;    // RT_HIP_CAM_GRID: 0 off, 1 launches of >= kCgMinFrames frames or a repeated position, 2 always
+  int cg_n_opt = 0;   // RT_HIP_CAM_GRID_N; 0 = kCgN
+  int32_t *d_cg_start = nullptr;
+  int2 *d_cg_ent = nullptr;
+  size_t cg_start_cap = 0, cg_ent_cap = 0;
+  int cg_n = 0;
+  bool cg_ok = false;                  // the grid for (cg_pos, cg_gen) exists
+  double cg_pos[3] = {0, 0, 0};
+  unsigned long long cg_gen = ~0ull;   // scene_gen it was built (or refused) for
+  double last_pos[3] = {0, 0, 0};      // the previous launch's camera position
+  bool have_last = false;
+  std::vector<double> h_sx, h_sy, h_sz, h_sr;  // sphere centres and radii (grid builds)
   double c0[3] = {0, 0, 0};
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
   double rmax = 0;
@@ -1206,6 +1232,8 @@ void free_scene(rt_ctx *c) {
   if (c->d_lg_start) (void)hipFree(c->d_lg_start);
   if (c->d_lg_ids) (void)hipFree(c->d_lg_ids);
   c->d_lg_start = c->d_lg_ids = nullptr;
+  c->cg_ok = false;
+  c->cg_gen = ~0ull;
   c->d_bvh = nullptr;
   c->d_prims = nullptr;
   c->bvh_nodes = 0;
@@ -1262,6 +1290,70 @@ LgArgs lg_args(const rt_ctx *c) {
   g.on = (c->lg_on && c->cull && c->d_lg_start) ? 1 : 0;
   g.max_off = c->lg_max_off;
   return g;
+}
+
+constexpr int kCgN = 512;          // camera grid cells per face edge
+constexpr int kCgMinFrames = 8;    // RT_HIP_CAM_GRID=1: launches this long build a grid at once
+constexpr int kCgMaxGlobal = 32;   // spheres containing the camera (on every list)
+constexpr size_t kCgMaxEntries = size_t(64) << 20;
+
+// The camera grid for this launch (cg.on = 0: the launch sweeps as before).
+// Used when every frame of the launch has the same camera position; built
+// (host, rt_lightgrid.cpp) when that position or the scene changed, for
+// launches of kCgMinFrames frames or more or a position repeated from the
+// previous launch (a single still frame does not pay for a build).
+int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
+  out = CgArgs{};
+  if (c->cg_mode == 0 || !c->cull || c->nsph == 0) return RT_OK;
+  const double pos[3] = {cam.px, cam.py, cam.pz};
+  for (int f = 1; f < nf; f++) {
+    const rt_camera &cm = c->fcams[f];
+    if (std::memcmp(cm.position, pos, sizeof pos) != 0) return RT_OK;
+  }
+  const bool repeat = c->have_last && std::memcmp(c->last_pos, pos, sizeof pos) == 0;
+  std::memcpy(c->last_pos, pos, sizeof pos);
+  c->have_last = true;
+  const bool cached = c->cg_gen == c->scene_gen && std::memcmp(c->cg_pos, pos, sizeof pos) == 0;
+  if (!cached) {
+    if (!(c->cg_mode == 2 || nf >= kCgMinFrames || repeat)) return RT_OK;
+    const int N = c->cg_n_opt ? c->cg_n_opt : kCgN;
+    double d2 = 0.0;
+    for (int k = 0; k < 3; k++) {
+      const double l = std::min(c->lo[k], pos[k]), h = std::max(c->hi[k], pos[k]);
+      d2 += (h - l) * (h - l);
+    }
+    std::vector<int32_t> start, ent;
+    const bool ok = build_point_grid(c->h_sx.data(), c->h_sy.data(), c->h_sz.data(), c->h_sr.data(), c->nsph,
+                                     pos[0], pos[1], pos[2], std::sqrt(d2), N, kCgMaxGlobal, kCgMaxEntries, start,
+                                     ent);
+    c->cg_ok = false;
+    c->cg_gen = c->scene_gen;
+    std::memcpy(c->cg_pos, pos, sizeof pos);
+    if (ok) {
+      RT_TRY(c, hipStreamSynchronize(c->stream));  // launches in flight read the previous grid
+      const size_t sb = start.size() * sizeof(int32_t), eb = ent.size() * sizeof(int32_t) + sizeof(int2);
+      if (c->cg_start_cap < sb) {
+        if (c->d_cg_start) (void)hipFree(c->d_cg_start);
+        c->d_cg_start = nullptr;
+        c->cg_start_cap = 0;
+        RT_TRY(c, hipMalloc(&c->d_cg_start, sb));
+        c->cg_start_cap = sb;
+      }
+      if (c->cg_ent_cap < eb) {
+        if (c->d_cg_ent) (void)hipFree(c->d_cg_ent);
+        c->d_cg_ent = nullptr;
+        c->cg_ent_cap = 0;
+        RT_TRY(c, hipMalloc(&c->d_cg_ent, eb));
+        c->cg_ent_cap = eb;
+      }
+      RT_TRY(c, hipMemcpy(c->d_cg_start, start.data(), sb, hipMemcpyHostToDevice));
+      if (!ent.empty()) RT_TRY(c, hipMemcpy(c->d_cg_ent, ent.data(), ent.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      c->cg_n = N;
+      c->cg_ok = true;
+    }
+  }
+  if (c->cg_ok) out = CgArgs{c->d_cg_start, c->d_cg_ent, c->cg_n, 1};
+  return RT_OK;
 }
 
 Cam to_cam(const rt_camera &cm) {
@@ -1452,6 +1544,10 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     // the default configuration (ordered 4-wide BVH walk, light grids) has kernels
     // compiled with only those paths (kFast): no registers held for the others
     const bool fast = bv.ordered && bv.wide && lg.on;
+    if (fast && kCull) {
+      const int rc = cam_grid(c, cam, nf, ra.cg);
+      if (rc != RT_OK) return rc;
+    }
     if (fast)
       hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, true>), grid, dim3(64 * kWg), lds, c->stream, ra);
     else
@@ -1593,6 +1689,8 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_DEFER_LEVEL")) c->defer_level = std::max(1, std::min(RT_MAX_DEPTH, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(16, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_CAM_GRID")) c->cg_mode = std::max(0, std::min(2, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_CAM_GRID_N")) c->cg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
   auto bail = [&](int rc) {
     rt_destroy(c);
     return rc;
@@ -1639,6 +1737,8 @@ void rt_destroy(rt_ctx *c) {
   if (c->h_perm) (void)hipHostFree(c->h_perm);
   if (c->d_bperm) (void)hipFree(c->d_bperm);
   if (c->h_bperm) (void)hipHostFree(c->h_bperm);
+  if (c->d_cg_start) (void)hipFree(c->d_cg_start);
+  if (c->d_cg_ent) (void)hipFree(c->d_cg_ent);
   for (int i = 0; i < rt_ctx::kRing; i++) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
@@ -1787,6 +1887,10 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     build_light_grid(sx.data(), sy.data(), sz.data(), br.data(), n, lx.data(), ly.data(), lz.data(), nl, diam,
                      c->lg_n, lg_start, lg_ids);
     c->lg_max_off = std::isfinite(diam) ? 1e-7 * diam : 0.0;
+    c->h_sx = sx;
+    c->h_sy = sy;
+    c->h_sz = sz;
+    c->h_sr = br;
     if ((e = hipMalloc(&c->d_lg_start, sizeof(int32_t) * (lg_start.size() + 1))) != hipSuccess ||
         (e = hipMalloc(&c->d_lg_ids, sizeof(int32_t) * (lg_ids.size() + 1))) != hipSuccess ||
         (!lg_start.empty() && (e = hipMemcpy(c->d_lg_start, lg_start.data(), sizeof(int32_t) * lg_start.size(),

@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
+#include <utility>
 
 namespace rtk {
 namespace {
@@ -119,6 +121,97 @@ void build_light_grid(const double *cx, const double *cy, const double *cz, cons
     ids.insert(ids.end(), global.begin(), global.end());
     st[cells + 1] = (int32_t)ids.size();
   }
+}
+
+bool build_point_grid(const double *cx, const double *cy, const double *cz, const double *r, int n, double px,
+                      double py, double pz, double diam, int N, int max_global, size_t max_entries,
+                      std::vector<int32_t> &start, std::vector<int32_t> &ent) {
+  start.clear();
+  ent.clear();
+  if (N < 1 || !std::isfinite(px) || !std::isfinite(py) || !std::isfinite(pz) || !std::isfinite(diam)) return false;
+  const int cells = 6 * N * N;
+  constexpr int kT = 8;
+  const int NT = (N + kT - 1) / kT;
+  std::vector<Patch> cellp((size_t)cells), tilep((size_t)6 * NT * NT);
+  for (int f = 0; f < 6; f++)
+    for (int j = 0; j < N; j++)
+      for (int i = 0; i < N; i++) cellp[(size_t)(f * N + j) * N + i] = make_patch(f, N, i, i + 1, j, j + 1);
+  for (int f = 0; f < 6; f++)
+    for (int tj = 0; tj < NT; tj++)
+      for (int ti = 0; ti < NT; ti++)
+        tilep[(size_t)(f * NT + tj) * NT + ti] =
+            make_patch(f, N, ti * kT, std::min(N, ti * kT + kT), tj * kT, std::min(N, tj * kT + kT));
+  Patch facep[6];
+  for (int f = 0; f < 6; f++) facep[f] = make_patch(f, N, 0, N, 0, N);
+  // (tlo, sphere) per cell; a sphere met both ways keeps its smaller bound
+  std::vector<std::vector<std::pair<float, int32_t>>> lists((size_t)cells);
+  std::vector<int32_t> global;
+  size_t total = 0;
+  auto mark = [&](const Dir &v, double ca, double sa, double alpha, float tlo, int32_t s) {
+    for (int f = 0; f < 6; f++) {
+      if (!meets(v, ca, sa, alpha, facep[f])) continue;
+      for (int tj = 0; tj < NT; tj++)
+        for (int ti = 0; ti < NT; ti++) {
+          if (!meets(v, ca, sa, alpha, tilep[(size_t)(f * NT + tj) * NT + ti])) continue;
+          for (int j = tj * kT; j < std::min(N, tj * kT + kT); j++)
+            for (int i = ti * kT; i < std::min(N, ti * kT + kT); i++) {
+              const size_t c = (size_t)(f * N + j) * N + i;
+              if (!meets(v, ca, sa, alpha, cellp[c])) continue;
+              auto &L = lists[c];
+              if (!L.empty() && L.back().second == s) {
+                L.back().first = std::min(L.back().first, tlo);
+              } else {
+                L.emplace_back(tlo, s);
+                ++total;
+              }
+            }
+        }
+    }
+  };
+  // fp32 bound at or below x (float(x) rounds to nearest)
+  auto down = [](double x) {
+    float f = (float)x;
+    if ((double)f > x) f = std::nextafter(f, -INFINITY);
+    return f;
+  };
+  for (int s = 0; s < n; s++) {
+    const double vx = cx[s] - px, vy = cy[s] - py, vz = cz[s] - pz;
+    const double D = std::sqrt(vx * vx + vy * vy + vz * vz);
+    // the light grid's radius: >= |r| + the rounding of the reference's test
+    const double R = std::fabs(r[s]) * (1.0 + 1e-6) + 1e-6 * (D + diam);
+    if (!std::isfinite(D) || !std::isfinite(R) || !(D > R)) {
+      global.push_back(s);  // contains (or nearly) P, or non-finite: every direction, tlo = -inf
+      if ((int)global.size() > max_global) return false;
+      continue;
+    }
+    const Dir v{vx / D, vy / D, vz / D}, w{-v.x, -v.y, -v.z};
+    const double alpha = std::asin(R / D) + kLgSlack;
+    const double ca = std::cos(alpha), sa = std::sin(alpha);
+    // ahead: every root is >= (D - R) / |d| (|d| = 1 within a few ulps; the
+    // rounding of the computed root is inside R's margin); behind: only the
+    // disc == 0 root, >= -(D + R)
+    mark(v, ca, sa, alpha, down((D - R) * (1.0 - 1e-9)), s);
+    mark(w, ca, sa, alpha, down(-(D + R) * (1.0 + 1e-9)), s);
+    if (total > max_entries) return false;
+  }
+  if (total + (size_t)cells * global.size() > max_entries) return false;
+  start.assign((size_t)cells + 1, 0);
+  ent.reserve(2 * (total + (size_t)cells * global.size()));
+  for (int c = 0; c < cells; c++) {
+    auto &L = lists[c];
+    for (int32_t s : global) L.emplace_back(-INFINITY, s);
+    std::sort(L.begin(), L.end());  // (tlo, index) ascending
+    start[c] = (int32_t)(ent.size() / 2);
+    for (const auto &e : L) {
+      int32_t bits;
+      std::memcpy(&bits, &e.first, sizeof bits);
+      ent.push_back(e.second);
+      ent.push_back(bits);
+    }
+    if (ent.size() / 2 > (size_t)INT32_MAX) return false;
+  }
+  start[cells] = (int32_t)(ent.size() / 2);
+  return true;
 }
 
 }  // namespace rtk

@@ -20,6 +20,7 @@
 // (falling back to testing every sphere); directions are binned in fp32
 // (angle error < 1e-6 rad) and every disk is grown by kLgSlack = 4e-6 rad.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -66,5 +67,20 @@ inline int lg_cell(float ux, float uy, float uz, int N, float rel = 0.0f) {
 void build_light_grid(const double *cx, const double *cy, const double *cz, const double *r, int n,
                       const double *lx, const double *ly, const double *lz, int nl, double diam, int N,
                       std::vector<int32_t> &start, std::vector<int32_t> &ids);
+
+// Camera grid: the same cube map around the camera position P, for the
+// closest hit of camera rays (origin exactly P, camera.h:17-25).  A cell lists
+// every sphere whose grown disk meets it seen along +u (roots t >= 0) or along
+// -u (the negative tangent root that sphere.h:43-47 keeps at disc == 0), each
+// entry with a lower bound `tlo` of any t the reference's test can return for
+// it (D - R ahead, -(D + R) behind, -inf for spheres that contain or nearly
+// contain P, which are on every list), entries ascending by (tlo, index): a
+// closest-hit scan may stop at the first entry whose tlo exceeds its best t.
+// Entry k of cell c is ent[2k] = sphere index, ent[2k + 1] = tlo as fp32 bits
+// (rounded down), k in [start[c], start[c + 1]).  Returns false (no grid) when
+// more than max_global spheres contain P or the lists exceed max_entries.
+bool build_point_grid(const double *cx, const double *cy, const double *cz, const double *r, int n, double px,
+                      double py, double pz, double diam, int N, int max_global, size_t max_entries,
+                      std::vector<int32_t> &start, std::vector<int32_t> &ent);
 
 }  // namespace rtk

@@ -129,3 +129,82 @@ def test_own_sphere_pretest_agrees_with_reference(tmp_path):
     w = out.stdout.split()
     assert w[0] == "checked" and int(w[1]) > 3000000 and int(w[3]) > 100000 and int(w[5]) > 100000
     assert w[-1] == "0", out.stdout
+
+
+def test_camera_grid_lists_and_scan(tmp_path):
+    """Camera grid (rt_lightgrid.h build_point_grid, rt_device.h cam_closest):
+    every sphere the reference's test reports a hit for on a camera ray, with
+    t of either sign, is on the looked-up cell's list (device binning and its
+    +-2^-22 quotient errors) with tlo <= t, and the early-exit scan returns
+    find_intersection's (t, index) -- random scenes at scales 0.1..1000, far
+    from the origin, negative radii, cameras inside / on spheres, rays aimed at
+    silhouettes ahead of and behind the camera (tests/native/cg_check.cpp)."""
+    exe = tmp_path / "cg_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-o", str(exe),
+                    os.path.join(REPO, "tests", "native", "cg_check.cpp"), os.path.join(CSRC, "rt_lightgrid.cpp")],
+                   check=True)
+    out = subprocess.run([str(exe), "40"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    w = out.stdout.split()
+    assert w[0] == "checked" and int(w[1]) > 100000 and int(w[2]) > 200000, out.stdout
+    assert w[4] == "0" and w[6] == "0", out.stdout
+
+
+CAM_SCENES = dict(GRID_SCENES)
+CAM_SCENES.update({
+    # the camera inside a mirror sphere that holds the other spheres
+    "camera_inside": "sphere 0 0 -3 20 0.9 0.9 0.9 0.8 1 20\nsphere 0 0 -6 1 1 0 0 0.5 1 10\n"
+                     "sphere 2 1 -4 0.5 0 1 0 0.9 1 50\nsphere -2 -1 3 1 0 0 1 0.3 1 5\n"
+                     "light 0 5 -3 1 1 1 1\ncamera 0 0 0 0 0 -6 70\n",
+    # the camera exactly on a sphere's surface, spheres behind it and a negative radius
+    "camera_on_surface": "sphere 0 0 1 1 0.5 0.5 0.5 0.5 1 10\nsphere 0 0 -6 -1.5 1 0.5 0 0.4 1 20\n"
+                         "sphere 3 0 4 1 0 1 1 0.6 1 10\nsphere 0 -101 -5 100 0.5 0.5 0.5 0.2 1 5\n"
+                         "light 4 6 2 1 1 1 1\ncamera 0 0 0 0 0 -6 80\n",
+})
+
+
+@pytest.fixture(params=["512", "64", "7", "1"], ids=lambda n: "camgrid" + n)
+def camgrid_renderer(request, monkeypatch):
+    import rt_hip
+
+    monkeypatch.setenv("RT_HIP_CAM_GRID", "2")
+    monkeypatch.setenv("RT_HIP_CAM_GRID_N", request.param)
+    r = rt_hip.Renderer(0)
+    yield r
+    r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CAM_SCENES))
+def test_camera_grid_scenes_vs_oracle(camgrid_renderer, name):
+    import orc
+    import rt_hip
+
+    text = CAM_SCENES[name]
+    W, H, D = 96, 72, 5
+    sc = rt_hip.Scene.parse(text)
+    camgrid_renderer.upload(sc)
+    ref, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=4)
+    rgb, st = camgrid_renderer.render(sc.camera(), W, H, D)
+    assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
+    assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
+                                                                   counts["reflect"])
+
+
+@pytest.mark.gpu
+def test_camera_grid_goldens(monkeypatch):
+    """Every golden fixture through the camera grid (forced) is byte-identical."""
+    import rt_hip
+    from conftest import golden_rgb, manifest, scene_path
+
+    monkeypatch.setenv("RT_HIP_CAM_GRID", "2")
+    r = rt_hip.Renderer(0)
+    try:
+        for name, m in sorted(manifest().items()):
+            sc = rt_hip.Scene.load(scene_path(m["scene"]))
+            r.upload(sc)
+            rgb, st = r.render(sc.camera(), m["width"], m["height"], m["depth"])
+            want = golden_rgb(name)
+            assert bytes(rgb) == want, (name, diff_summary(bytes(rgb), want))
+    finally:
+        r.close()
