@@ -4,6 +4,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <utility>
 
 namespace rtk {
@@ -123,19 +126,46 @@ void build_light_grid(const double *cx, const double *cy, const double *cz, cons
   }
 }
 
+// The cell patches of an N x N face have the same angular radius on all six
+// faces (the faces are permutations / reflections of each other), so the
+// camera grid keeps one (cos, sin) of rad + slack per (i, j) for each N it
+// has seen and forms the cell centres on the fly.
+struct CellTable {
+  int N = 0;
+  std::vector<double> cb, sb;  // per (j * N + i)
+};
+const CellTable &cell_table(int N) {
+  static std::mutex mu;
+  static std::vector<std::unique_ptr<CellTable>> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const auto &t : cache)
+    if (t->N == N) return *t;
+  auto t = std::make_unique<CellTable>();
+  t->N = N;
+  t->cb.resize((size_t)N * N);
+  t->sb.resize((size_t)N * N);
+  for (int j = 0; j < N; j++)
+    for (int i = 0; i < N; i++) {
+      const Patch p = make_patch(0, N, i, i + 1, j, j + 1);
+      t->cb[(size_t)j * N + i] = p.cb;
+      t->sb[(size_t)j * N + i] = p.sb;
+    }
+  cache.push_back(std::move(t));
+  return *cache.back();
+}
+
 bool build_point_grid(const double *cx, const double *cy, const double *cz, const double *r, int n, double px,
                       double py, double pz, double diam, int N, int max_global, size_t max_entries,
                       std::vector<int32_t> &start, std::vector<int32_t> &ent) {
   start.clear();
   ent.clear();
-  if (N < 1 || !std::isfinite(px) || !std::isfinite(py) || !std::isfinite(pz) || !std::isfinite(diam)) return false;
+  if (N < 1 || N > 4096 || !std::isfinite(px) || !std::isfinite(py) || !std::isfinite(pz) || !std::isfinite(diam))
+    return false;
   const int cells = 6 * N * N;
   constexpr int kT = 8;
   const int NT = (N + kT - 1) / kT;
-  std::vector<Patch> cellp((size_t)cells), tilep((size_t)6 * NT * NT);
-  for (int f = 0; f < 6; f++)
-    for (int j = 0; j < N; j++)
-      for (int i = 0; i < N; i++) cellp[(size_t)(f * N + j) * N + i] = make_patch(f, N, i, i + 1, j, j + 1);
+  const CellTable &ct = cell_table(N);
+  std::vector<Patch> tilep((size_t)6 * NT * NT);
   for (int f = 0; f < 6; f++)
     for (int tj = 0; tj < NT; tj++)
       for (int ti = 0; ti < NT; ti++)
@@ -143,30 +173,27 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
             make_patch(f, N, ti * kT, std::min(N, ti * kT + kT), tj * kT, std::min(N, tj * kT + kT));
   Patch facep[6];
   for (int f = 0; f < 6; f++) facep[f] = make_patch(f, N, 0, N, 0, N);
-  // (tlo, sphere) per cell; a sphere met both ways keeps its smaller bound
-  std::vector<std::vector<std::pair<float, int32_t>>> lists((size_t)cells);
-  std::vector<int32_t> global;
-  size_t total = 0;
-  auto mark = [&](const Dir &v, double ca, double sa, double alpha, float tlo, int32_t s) {
-    for (int f = 0; f < 6; f++) {
-      if (!meets(v, ca, sa, alpha, facep[f])) continue;
-      for (int tj = 0; tj < NT; tj++)
-        for (int ti = 0; ti < NT; ti++) {
-          if (!meets(v, ca, sa, alpha, tilep[(size_t)(f * NT + tj) * NT + ti])) continue;
-          for (int j = tj * kT; j < std::min(N, tj * kT + kT); j++)
-            for (int i = ti * kT; i < std::min(N, ti * kT + kT); i++) {
-              const size_t c = (size_t)(f * N + j) * N + i;
-              if (!meets(v, ca, sa, alpha, cellp[c])) continue;
-              auto &L = lists[c];
-              if (!L.empty() && L.back().second == s) {
-                L.back().first = std::min(L.back().first, tlo);
-              } else {
-                L.emplace_back(tlo, s);
-                ++total;
-              }
-            }
-        }
-    }
+  // blocks of kB x kB tiles between the faces and the tiles: a small disk
+  // tests one face's blocks and one block's tiles, not every tile
+  constexpr int kB = 8;
+  const int NB = (NT + kB - 1) / kB;
+  std::vector<Patch> blockp((size_t)6 * NB * NB);
+  for (int f = 0; f < 6; f++)
+    for (int bj = 0; bj < NB; bj++)
+      for (int bi = 0; bi < NB; bi++)
+        blockp[(size_t)(f * NB + bj) * NB + bi] = make_patch(f, N, bi * kB * kT, std::min(N, (bi + 1) * kB * kT),
+                                                             bj * kB * kT, std::min(N, (bj + 1) * kB * kT));
+  // records (cell, tlo, sphere)
+  struct Rec {
+    int32_t cell;
+    float tlo;
+    int32_t s;
+  };
+  struct Disk {
+    Dir v;
+    double ca, sa, alpha;
+    float tlo;
+    int32_t s;
   };
   // fp32 bound at or below x (float(x) rounds to nearest)
   auto down = [](double x) {
@@ -174,6 +201,9 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
     if ((double)f > x) f = std::nextafter(f, -INFINITY);
     return f;
   };
+  std::vector<Disk> disks;
+  std::vector<int32_t> global;
+  disks.reserve(2 * (size_t)n);
   for (int s = 0; s < n; s++) {
     const double vx = cx[s] - px, vy = cy[s] - py, vz = cz[s] - pz;
     const double D = std::sqrt(vx * vx + vy * vy + vz * vz);
@@ -184,33 +214,114 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
       if ((int)global.size() > max_global) return false;
       continue;
     }
-    const Dir v{vx / D, vy / D, vz / D}, w{-v.x, -v.y, -v.z};
+    const Dir v{vx / D, vy / D, vz / D};
     const double alpha = std::asin(R / D) + kLgSlack;
     const double ca = std::cos(alpha), sa = std::sin(alpha);
     // ahead: every root is >= (D - R) / |d| (|d| = 1 within a few ulps; the
     // rounding of the computed root is inside R's margin); behind: only the
     // disc == 0 root, >= -(D + R)
-    mark(v, ca, sa, alpha, down((D - R) * (1.0 - 1e-9)), s);
-    mark(w, ca, sa, alpha, down(-(D + R) * (1.0 + 1e-9)), s);
-    if (total > max_entries) return false;
+    disks.push_back(Disk{v, ca, sa, alpha, down((D - R) * (1.0 - 1e-9)), s});
+    disks.push_back(Disk{Dir{-v.x, -v.y, -v.z}, ca, sa, alpha, down(-(D + R) * (1.0 + 1e-9)), s});
   }
-  if (total + (size_t)cells * global.size() > max_entries) return false;
-  start.assign((size_t)cells + 1, 0);
-  ent.reserve(2 * (total + (size_t)cells * global.size()));
-  for (int c = 0; c < cells; c++) {
-    auto &L = lists[c];
-    for (int32_t s : global) L.emplace_back(-INFINITY, s);
-    std::sort(L.begin(), L.end());  // (tlo, index) ascending
-    start[c] = (int32_t)(ent.size() / 2);
-    for (const auto &e : L) {
-      int32_t bits;
-      std::memcpy(&bits, &e.first, sizeof bits);
-      ent.push_back(e.second);
-      ent.push_back(bits);
+  const size_t fcells = (size_t)N * N;
+  // kThreads workers over slices of the spheres, records per worker.  A
+  // sphere whose two disks (very wide ones) both meet a cell is listed there
+  // twice: the second test of it changes nothing (same t, same index)
+  constexpr int kThreads = 8;
+  std::vector<Rec> recs[kThreads];
+  bool over[kThreads] = {};
+  auto build_slice = [&](int w) {
+    std::vector<Rec> &out = recs[w];
+    const size_t pairs = disks.size() / 2, lo = pairs * w / kThreads, hi = pairs * (w + 1) / kThreads;
+    for (size_t di = 2 * lo; di < 2 * hi; di++) {
+      const Disk &k = disks[di];
+      const Dir &v = k.v;
+      const double ca = k.ca, sa = k.sa, alpha = k.alpha;
+      const bool wide = alpha + kLgSlack >= 3.0;  // meets() takes every patch then
+      for (int f = 0; f < 6; f++) {
+        if (!meets(v, ca, sa, alpha, facep[f])) continue;
+        for (int bj = 0; bj < NB; bj++)
+          for (int bi = 0; bi < NB; bi++) {
+            if (!meets(v, ca, sa, alpha, blockp[(size_t)(f * NB + bj) * NB + bi])) continue;
+            for (int tj = bj * kB; tj < std::min(NT, (bj + 1) * kB); tj++)
+              for (int ti = bi * kB; ti < std::min(NT, (bi + 1) * kB); ti++) {
+                const Patch &tp = tilep[(size_t)(f * NT + tj) * NT + ti];
+                if (!meets(v, ca, sa, alpha, tp)) continue;
+                // a tile well inside the disk takes all its cells untested (a
+                // list may hold extra spheres, never miss one)
+                const bool inside = alpha < 3.0 && alpha > tp.rad + 1e-3 &&
+                                    v.x * tp.c.x + v.y * tp.c.y + v.z * tp.c.z >= std::cos(alpha - tp.rad - 1e-3);
+                for (int j = tj * kT; j < std::min(N, tj * kT + kT); j++) {
+                  const double b = -1.0 + (2.0 * j + 1.0) / N;
+                  for (int i = ti * kT; i < std::min(N, ti * kT + kT); i++) {
+                    const size_t ij = (size_t)j * N + i;
+                    if (!inside) {
+                      Patch p;
+                      p.c = face_dir(f, -1.0 + (2.0 * i + 1.0) / N, b);
+                      p.rad = wide ? 3.2 : 0.0;  // only meets()'s "whole sphere" shortcut reads it
+                      p.cb = ct.cb[ij];
+                      p.sb = ct.sb[ij];
+                      if (!meets(v, ca, sa, alpha, p)) continue;
+                    }
+                    out.push_back(Rec{(int32_t)((size_t)f * fcells + ij), k.tlo, k.s});
+                  }
+                }
+              }
+          }
+      }
+      if (out.size() > max_entries) {
+        over[w] = true;
+        return;
+      }
     }
-    if (ent.size() / 2 > (size_t)INT32_MAX) return false;
+  };
+  {
+    std::vector<std::thread> th;
+    for (int w = 1; w < kThreads; w++) th.emplace_back(build_slice, w);
+    build_slice(0);
+    for (auto &t : th) t.join();
   }
-  start[cells] = (int32_t)(ent.size() / 2);
+  size_t nrec = 0;
+  for (int w = 0; w < kThreads; w++) {
+    if (over[w]) return false;
+    nrec += recs[w].size();
+  }
+  const size_t total = nrec + (size_t)cells * global.size();
+  if (total > max_entries || total > (size_t)INT32_MAX) return false;
+  // counting sort by cell, then each cell's list by (tlo, index)
+  start.assign((size_t)cells + 1, 0);
+  for (int w = 0; w < kThreads; w++)
+    for (const Rec &e : recs[w]) start[(size_t)e.cell + 1]++;
+  for (int c = 0; c < cells; c++) start[(size_t)c + 1] += start[c] + (int32_t)global.size();
+  ent.resize(2 * total);
+  auto emit_face = [&](int f) {
+    std::vector<std::pair<float, int32_t>> L;
+    std::vector<size_t> fill(fcells);
+    std::vector<std::pair<float, int32_t>> flat(
+        (size_t)(start[(size_t)(f + 1) * fcells] - start[(size_t)f * fcells]));
+    const size_t base = (size_t)start[(size_t)f * fcells];
+    for (size_t ij = 0; ij < fcells; ij++) {
+      fill[ij] = (size_t)start[f * fcells + ij] - base;
+      for (int32_t s : global) flat[fill[ij]++] = {-INFINITY, s};
+    }
+    for (int w = 0; w < kThreads; w++)
+      for (const Rec &e : recs[w])
+        if ((size_t)e.cell / fcells == (size_t)f) flat[fill[(size_t)e.cell - f * fcells]++] = {e.tlo, e.s};
+    for (size_t ij = 0; ij < fcells; ij++) {
+      const size_t b = (size_t)start[f * fcells + ij] - base, e = (size_t)start[f * fcells + ij + 1] - base;
+      if (e - b > 1) std::sort(flat.begin() + (long)b, flat.begin() + (long)e);
+      for (size_t k = b; k < e; k++) {
+        ent[2 * (base + k)] = flat[k].second;
+        std::memcpy(&ent[2 * (base + k) + 1], &flat[k].first, sizeof(int32_t));
+      }
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int f = 1; f < 6; f++) th.emplace_back(emit_face, f);
+    emit_face(0);
+    for (auto &t : th) t.join();
+  }
   return true;
 }
 

@@ -172,6 +172,29 @@ void grid_case(int n, int nl) {
     const int c = rtk::lg_cell((float)uni(-1, 1), (float)uni(-1, 1), (float)uni(-1, 1), N);
     CHECK(c >= -1 && c < 6 * N * N);
   }
+  // the camera grid around a random point or a sphere's centre
+  std::vector<int32_t> cst, cent;
+  const int s0 = n > 0 ? irand(0, n - 1) : 0;
+  const bool at_centre = n > 0 && irand(0, 1) == 1;
+  const double qx = at_centre ? cx[s0] : uni(-20, 20), qy = at_centre ? cy[s0] : uni(-20, 20),
+               qz = at_centre ? cz[s0] : uni(-20, 20);
+  if (rtk::build_point_grid(cx.data(), cy.data(), cz.data(), r.data(), n, qx, qy, qz, 200.0, N, 8,
+                            size_t(1) << 22, cst, cent)) {
+    const size_t cells = 6 * (size_t)N * N;
+    CHECK(cst.size() == cells + 1 && cst[0] == 0 && (size_t)cst[cells] * 2 == cent.size());
+    for (size_t c = 0; c < cells; ++c) {
+      CHECK(cst[c] <= cst[c + 1]);
+      for (int32_t k = cst[c]; k < cst[c + 1]; ++k) {
+        CHECK(cent[2 * (size_t)k] >= 0 && cent[2 * (size_t)k] < n);
+        float t0, t1;
+        std::memcpy(&t1, &cent[2 * (size_t)k + 1], sizeof t1);
+        if (k > cst[c]) {
+          std::memcpy(&t0, &cent[2 * (size_t)k - 1], sizeof t0);
+          CHECK(!(t1 < t0));  // ascending bounds
+        }
+      }
+    }
+  }
 }
 
 void sched_case() {
