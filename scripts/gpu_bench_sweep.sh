@@ -17,7 +17,7 @@ while IFS= read -r args; do
   for w in $args; do if [ ${#rest[@]} -eq 0 ] && [[ "$w" == *=* ]]; then envs+=("$w"); else rest+=("$w"); fi; done
   timeout -k 10 300 env "${envs[@]}" python bench.py --no-cpu-baseline "${rest[@]}" ${BENCH_ARGS} > "$out.json" 2> "$out.err" || { echo "rc=$? for $args"; tail -5 "$out.err"; exit 1; }
   python -c "
-import json; d=json.load(open('$out.json')); a=d['also'].get('complex_1920x1080_d4',{})
+import json; d=json.load(open('$out.json')); a=d.get('also',{}).get('complex_1920x1080_d4',{})
 print('%-55s %9.1f Mrays/s k=%.4f ms/frame launches=%s | complex %9.1f' % ('$args', d['value'], d['roofline']['kernel_ms_per_frame'], d['config']['launch_frames'], a.get('mrays_per_s',0)))"
   i=$((i+1))
 done <<< "$SWEEP"
