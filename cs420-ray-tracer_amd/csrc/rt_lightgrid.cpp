@@ -62,70 +62,6 @@ inline bool meets(const Dir &v, double ca, double sa, double alpha, const Patch 
   return v.x * p.c.x + v.y * p.c.y + v.z * p.c.z >= ca * p.cb - sa * p.sb - 1e-12;
 }
 
-}  // namespace
-
-void build_light_grid(const double *cx, const double *cy, const double *cz, const double *r, int n,
-                      const double *lx, const double *ly, const double *lz, int nl, double diam, int N,
-                      std::vector<int32_t> &start, std::vector<int32_t> &ids) {
-  const int cells = 6 * N * N;
-  const size_t stride = (size_t)cells + 2;
-  start.assign(stride * (size_t)nl, 0);
-  ids.clear();
-  constexpr int kT = 8;  // patches of kT x kT cells for the coarse pass
-  const int NT = (N + kT - 1) / kT;
-  std::vector<Patch> cellp((size_t)cells), tilep((size_t)6 * NT * NT);
-  for (int f = 0; f < 6; f++)
-    for (int j = 0; j < N; j++)
-      for (int i = 0; i < N; i++) cellp[(size_t)(f * N + j) * N + i] = make_patch(f, N, i, i + 1, j, j + 1);
-  for (int f = 0; f < 6; f++)
-    for (int tj = 0; tj < NT; tj++)
-      for (int ti = 0; ti < NT; ti++)
-        tilep[(size_t)(f * NT + tj) * NT + ti] =
-            make_patch(f, N, ti * kT, std::min(N, ti * kT + kT), tj * kT, std::min(N, tj * kT + kT));
-  Patch facep[6];
-  for (int f = 0; f < 6; f++) facep[f] = make_patch(f, N, 0, N, 0, N);
-  const double dm = std::isfinite(diam) ? diam : 0.0;
-  std::vector<std::vector<int32_t>> lists((size_t)cells);
-  std::vector<int32_t> global;
-  for (int l = 0; l < nl; l++) {
-    for (auto &v : lists) v.clear();
-    global.clear();
-    const bool light_ok = std::isfinite(lx[l]) && std::isfinite(ly[l]) && std::isfinite(lz[l]);
-    for (int s = 0; s < n; s++) {
-      const double vx = cx[s] - lx[l], vy = cy[s] - ly[l], vz = cz[s] - lz[l];
-      const double D = std::sqrt(vx * vx + vy * vy + vz * vz);
-      const double R = std::fabs(r[s]) * (1.0 + 1e-6) + 1e-6 * (D + dm);  // >= r + max_off + rounding
-      if (!light_ok || !std::isfinite(D) || !std::isfinite(R) || !(D > R) || !std::isfinite(dm)) {
-        global.push_back(s);  // contains (or nearly) the light, or non-finite: every direction
-        continue;
-      }
-      const Dir v{vx / D, vy / D, vz / D};
-      const double alpha = std::asin(R / D) + kLgSlack;
-      const double ca = std::cos(alpha), sa = std::sin(alpha);
-      for (int f = 0; f < 6; f++) {
-        if (!meets(v, ca, sa, alpha, facep[f])) continue;
-        for (int tj = 0; tj < NT; tj++)
-          for (int ti = 0; ti < NT; ti++) {
-            if (!meets(v, ca, sa, alpha, tilep[(size_t)(f * NT + tj) * NT + ti])) continue;
-            for (int j = tj * kT; j < std::min(N, tj * kT + kT); j++)
-              for (int i = ti * kT; i < std::min(N, ti * kT + kT); i++) {
-                const size_t c = (size_t)(f * N + j) * N + i;
-                if (meets(v, ca, sa, alpha, cellp[c])) lists[c].push_back(s);
-              }
-          }
-      }
-    }
-    int32_t *st = start.data() + stride * (size_t)l;
-    for (int c = 0; c < cells; c++) {
-      st[c] = (int32_t)ids.size();
-      ids.insert(ids.end(), lists[c].begin(), lists[c].end());
-    }
-    st[cells] = (int32_t)ids.size();
-    ids.insert(ids.end(), global.begin(), global.end());
-    st[cells + 1] = (int32_t)ids.size();
-  }
-}
-
 // The cell patches of an N x N face have the same angular radius on all six
 // faces (the faces are permutations / reflections of each other), so the
 // camera grid keeps one (cos, sin) of rad + slack per (i, j) for each N it
@@ -154,6 +90,119 @@ const CellTable &cell_table(int N) {
   return *cache.back();
 }
 
+// The cube map's patch hierarchy: faces, blocks of kB x kB tiles, tiles of
+// kT x kT cells, cells (from the cached per-N table).  for_cells calls fn(c)
+// for every cell a disk (centre v, angular radius alpha, ca/sa its cos/sin)
+// meets; a tile well inside the disk gives all its cells untested (a list may
+// hold extra spheres, never miss one).
+struct CubeGrid {
+  static constexpr int kT = 8, kB = 8;
+  int N, NT, NB;
+  const CellTable *ct;
+  std::vector<Patch> tilep, blockp;
+  Patch facep[6];
+  explicit CubeGrid(int n) : N(n), NT((n + kT - 1) / kT), NB((NT + kB - 1) / kB), ct(&cell_table(n)) {
+    tilep.resize((size_t)6 * NT * NT);
+    for (int f = 0; f < 6; f++)
+      for (int tj = 0; tj < NT; tj++)
+        for (int ti = 0; ti < NT; ti++)
+          tilep[(size_t)(f * NT + tj) * NT + ti] =
+              make_patch(f, N, ti * kT, std::min(N, ti * kT + kT), tj * kT, std::min(N, tj * kT + kT));
+    blockp.resize((size_t)6 * NB * NB);
+    for (int f = 0; f < 6; f++)
+      for (int bj = 0; bj < NB; bj++)
+        for (int bi = 0; bi < NB; bi++)
+          blockp[(size_t)(f * NB + bj) * NB + bi] = make_patch(f, N, bi * kB * kT, std::min(N, (bi + 1) * kB * kT),
+                                                               bj * kB * kT, std::min(N, (bj + 1) * kB * kT));
+    for (int f = 0; f < 6; f++) facep[f] = make_patch(f, N, 0, N, 0, N);
+  }
+  template <class F>
+  void for_cells(const Dir &v, double ca, double sa, double alpha, F &&fn) const {
+    const bool wide = alpha + kLgSlack >= 3.0;  // meets() takes every patch then
+    for (int f = 0; f < 6; f++) {
+      if (!meets(v, ca, sa, alpha, facep[f])) continue;
+      for (int bj = 0; bj < NB; bj++)
+        for (int bi = 0; bi < NB; bi++) {
+          if (!meets(v, ca, sa, alpha, blockp[(size_t)(f * NB + bj) * NB + bi])) continue;
+          for (int tj = bj * kB; tj < std::min(NT, (bj + 1) * kB); tj++)
+            for (int ti = bi * kB; ti < std::min(NT, (bi + 1) * kB); ti++) {
+              const Patch &tp = tilep[(size_t)(f * NT + tj) * NT + ti];
+              if (!meets(v, ca, sa, alpha, tp)) continue;
+              const bool inside = alpha < 3.0 && alpha > tp.rad + 1e-3 &&
+                                  v.x * tp.c.x + v.y * tp.c.y + v.z * tp.c.z >= std::cos(alpha - tp.rad - 1e-3);
+              for (int j = tj * kT; j < std::min(N, tj * kT + kT); j++) {
+                const double b = -1.0 + (2.0 * j + 1.0) / N;
+                for (int i = ti * kT; i < std::min(N, ti * kT + kT); i++) {
+                  const size_t ij = (size_t)j * N + i;
+                  if (!inside) {
+                    Patch p;
+                    p.c = face_dir(f, -1.0 + (2.0 * i + 1.0) / N, b);
+                    p.rad = wide ? 3.2 : 0.0;  // only meets()'s "whole sphere" shortcut reads it
+                    p.cb = ct->cb[ij];
+                    p.sb = ct->sb[ij];
+                    if (!meets(v, ca, sa, alpha, p)) continue;
+                  }
+                  fn((size_t)f * N * N + ij);
+                }
+              }
+            }
+        }
+    }
+  }
+};
+
+}  // namespace
+
+void build_light_grid(const double *cx, const double *cy, const double *cz, const double *r, int n,
+                      const double *lx, const double *ly, const double *lz, int nl, double diam, int N,
+                      std::vector<int32_t> &start, std::vector<int32_t> &ids) {
+  const int cells = 6 * N * N;
+  const size_t stride = (size_t)cells + 2;
+  start.assign(stride * (size_t)nl, 0);
+  ids.clear();
+  const CubeGrid G(N);
+  const double dm = std::isfinite(diam) ? diam : 0.0;
+  // one thread per light (its lists, then concatenated in light order)
+  std::vector<std::vector<int32_t>> lid((size_t)nl);
+  auto build_one = [&](int l) {
+    std::vector<std::vector<int32_t>> lists((size_t)cells);
+    std::vector<int32_t> global;
+    const bool light_ok = std::isfinite(lx[l]) && std::isfinite(ly[l]) && std::isfinite(lz[l]);
+    for (int s = 0; s < n; s++) {
+      const double vx = cx[s] - lx[l], vy = cy[s] - ly[l], vz = cz[s] - lz[l];
+      const double D = std::sqrt(vx * vx + vy * vy + vz * vz);
+      const double R = std::fabs(r[s]) * (1.0 + 1e-6) + 1e-6 * (D + dm);  // >= r + max_off + rounding
+      if (!light_ok || !std::isfinite(D) || !std::isfinite(R) || !(D > R) || !std::isfinite(dm)) {
+        global.push_back(s);  // contains (or nearly) the light, or non-finite: every direction
+        continue;
+      }
+      const Dir v{vx / D, vy / D, vz / D};
+      const double alpha = std::asin(R / D) + kLgSlack;
+      const double ca = std::cos(alpha), sa = std::sin(alpha);
+      G.for_cells(v, ca, sa, alpha, [&](size_t c) { lists[c].push_back(s); });
+    }
+    int32_t *st = start.data() + stride * (size_t)l;  // offsets within this light's ids for now
+    std::vector<int32_t> &out = lid[(size_t)l];
+    for (int c = 0; c < cells; c++) {
+      st[c] = (int32_t)out.size();
+      out.insert(out.end(), lists[c].begin(), lists[c].end());
+    }
+    st[cells] = (int32_t)out.size();
+    out.insert(out.end(), global.begin(), global.end());
+    st[cells + 1] = (int32_t)out.size();
+  };
+  std::vector<std::thread> th;
+  for (int l = 1; l < nl; l++) th.emplace_back(build_one, l);
+  if (nl > 0) build_one(0);
+  for (auto &t : th) t.join();
+  for (int l = 0; l < nl; l++) {
+    const int32_t base = (int32_t)ids.size();
+    int32_t *st = start.data() + stride * (size_t)l;
+    for (size_t c = 0; c < stride; c++) st[c] += base;
+    ids.insert(ids.end(), lid[(size_t)l].begin(), lid[(size_t)l].end());
+  }
+}
+
 bool build_point_grid(const double *cx, const double *cy, const double *cz, const double *r, int n, double px,
                       double py, double pz, double diam, int N, int max_global, size_t max_entries,
                       std::vector<int32_t> &start, std::vector<int32_t> &ent) {
@@ -162,27 +211,7 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
   if (N < 1 || N > 4096 || !std::isfinite(px) || !std::isfinite(py) || !std::isfinite(pz) || !std::isfinite(diam))
     return false;
   const int cells = 6 * N * N;
-  constexpr int kT = 8;
-  const int NT = (N + kT - 1) / kT;
-  const CellTable &ct = cell_table(N);
-  std::vector<Patch> tilep((size_t)6 * NT * NT);
-  for (int f = 0; f < 6; f++)
-    for (int tj = 0; tj < NT; tj++)
-      for (int ti = 0; ti < NT; ti++)
-        tilep[(size_t)(f * NT + tj) * NT + ti] =
-            make_patch(f, N, ti * kT, std::min(N, ti * kT + kT), tj * kT, std::min(N, tj * kT + kT));
-  Patch facep[6];
-  for (int f = 0; f < 6; f++) facep[f] = make_patch(f, N, 0, N, 0, N);
-  // blocks of kB x kB tiles between the faces and the tiles: a small disk
-  // tests one face's blocks and one block's tiles, not every tile
-  constexpr int kB = 8;
-  const int NB = (NT + kB - 1) / kB;
-  std::vector<Patch> blockp((size_t)6 * NB * NB);
-  for (int f = 0; f < 6; f++)
-    for (int bj = 0; bj < NB; bj++)
-      for (int bi = 0; bi < NB; bi++)
-        blockp[(size_t)(f * NB + bj) * NB + bi] = make_patch(f, N, bi * kB * kT, std::min(N, (bi + 1) * kB * kT),
-                                                             bj * kB * kT, std::min(N, (bj + 1) * kB * kT));
+  const CubeGrid G(N);
   // records (cell, tlo, sphere)
   struct Rec {
     int32_t cell;
@@ -237,38 +266,7 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
       const Disk &k = disks[di];
       const Dir &v = k.v;
       const double ca = k.ca, sa = k.sa, alpha = k.alpha;
-      const bool wide = alpha + kLgSlack >= 3.0;  // meets() takes every patch then
-      for (int f = 0; f < 6; f++) {
-        if (!meets(v, ca, sa, alpha, facep[f])) continue;
-        for (int bj = 0; bj < NB; bj++)
-          for (int bi = 0; bi < NB; bi++) {
-            if (!meets(v, ca, sa, alpha, blockp[(size_t)(f * NB + bj) * NB + bi])) continue;
-            for (int tj = bj * kB; tj < std::min(NT, (bj + 1) * kB); tj++)
-              for (int ti = bi * kB; ti < std::min(NT, (bi + 1) * kB); ti++) {
-                const Patch &tp = tilep[(size_t)(f * NT + tj) * NT + ti];
-                if (!meets(v, ca, sa, alpha, tp)) continue;
-                // a tile well inside the disk takes all its cells untested (a
-                // list may hold extra spheres, never miss one)
-                const bool inside = alpha < 3.0 && alpha > tp.rad + 1e-3 &&
-                                    v.x * tp.c.x + v.y * tp.c.y + v.z * tp.c.z >= std::cos(alpha - tp.rad - 1e-3);
-                for (int j = tj * kT; j < std::min(N, tj * kT + kT); j++) {
-                  const double b = -1.0 + (2.0 * j + 1.0) / N;
-                  for (int i = ti * kT; i < std::min(N, ti * kT + kT); i++) {
-                    const size_t ij = (size_t)j * N + i;
-                    if (!inside) {
-                      Patch p;
-                      p.c = face_dir(f, -1.0 + (2.0 * i + 1.0) / N, b);
-                      p.rad = wide ? 3.2 : 0.0;  // only meets()'s "whole sphere" shortcut reads it
-                      p.cb = ct.cb[ij];
-                      p.sb = ct.sb[ij];
-                      if (!meets(v, ca, sa, alpha, p)) continue;
-                    }
-                    out.push_back(Rec{(int32_t)((size_t)f * fcells + ij), k.tlo, k.s});
-                  }
-                }
-              }
-          }
-      }
+      G.for_cells(v, ca, sa, alpha, [&](size_t c) { out.push_back(Rec{(int32_t)c, k.tlo, k.s}); });
       if (out.size() > max_entries) {
         over[w] = true;
         return;
