@@ -1120,7 +1120,7 @@ struct rt_ctx {
   // per-light direction grids for shadow rays (rt_lightgrid.h), built at upload
   int32_t *d_lg_start = nullptr, *d_lg_ids = nullptr;
   int lg_n = 128, lg_on = 1;  // lg_n: the grid of the uploaded scene
-  int lg_n_opt = 0;            // RT_HIP_SHADOW_GRID_N; 0 = 128, or 512 above kBvhAlwaysAbove spheres
+  int lg_n_opt = 0;            // RT_HIP_SHADOW_GRID_N; 0 = 128, or 768 above kBvhAlwaysAbove spheres
   double lg_max_off = 0.0;
   // camera grid (rt_lightgrid.h build_point_grid): the closest hit of camera
   // rays in the merged kFast kernels, built per camera position and cached
@@ -1820,7 +1820,7 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
   // leaves of 2 spheres (+0.6..0.9 % over 4 on synth200 with the merged levels);
   // 1 above kBvhAlwaysAbove, where every closest hit walks (synth10k 4.37 -> 4.16 ms)
   c->bvh_leaf = c->bvh_leaf_opt ? c->bvh_leaf_opt : (big ? 1 : 2);
-  c->lg_n = c->lg_n_opt ? c->lg_n_opt : (big ? 512 : 128);
+  c->lg_n = c->lg_n_opt ? c->lg_n_opt : (big ? 768 : 128);
   std::vector<BvhNode> nodes;
   std::vector<int32_t> prims;
   build_bvh(bx.data(), by.data(), bz.data(), br.data(), n, c->bvh_leaf, nodes, prims);
