@@ -155,3 +155,28 @@ def test_frames_argument_errors(gpu_renderer):
     gpu_renderer.render_frames_async([cam], W, H, D, None, buf.data_ptr(), 0)
     gpu_renderer.stats()
     assert buf[:H * W * 3].cpu().numpy().tobytes() == golden_rgb("complex_97x61_d4")
+
+
+def test_camera_grid_rotated_views_one_position(gpu_renderer):
+    """Eight views from one camera position in one launch (the camera grid is
+    built for it: >= 8 frames at one position) -- looking at, beside, above and
+    away from the scene -- each byte-identical to the oracle's render of that
+    camera line (scene_loader.h camera grammar) with identical ray counts."""
+    import orc
+    import rt_hip
+
+    base = open(scene_path("complex")).read()
+    lines = [ln for ln in base.splitlines() if not ln.strip().startswith("camera")]
+    targets = ["0 0 -20", "6 1 -20", "-8 3 -18", "0 9 -20", "0 -6 -15", "20 2 5", "0 3 40", "-3 -1 -60"]
+    texts = ["\n".join(lines) + "\ncamera 0 3 12 %s 65\n" % t for t in targets]
+    scenes = [rt_hip.Scene.parse(t) for t in texts]
+    W, H, D = 64, 48, 4
+    gpu_renderer.upload(scenes[0])
+    frames, st, _ = _frames(gpu_renderer, [s.camera() for s in scenes], W, H, D)
+    total = {"primary": 0, "shadow": 0, "reflect": 0}
+    for f, t in enumerate(texts):
+        ref, counts, _ = orc.OracleScene(text=t).render(W, H, D, threads=4)
+        assert frames[f].tobytes() == ref, (targets[f], diff_summary(frames[f].tobytes(), ref))
+        for k in total:
+            total[k] += counts[k]
+    assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (total["primary"], total["shadow"], total["reflect"])
