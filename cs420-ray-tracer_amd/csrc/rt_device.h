@@ -9,6 +9,7 @@
 
 #include "rt_bvh.h"
 #include "rt_lightgrid.h"
+#include "rt_pow.h"
 
 #pragma clang fp contract(off)
 
@@ -133,9 +134,18 @@ __device__ __forceinline__ D3 renormalized(D3 a) {
   return normalized(a);
 }
 
-// ocml's fp64 pow needs ~50 VGPRs when inlined into the render loop; called
-// out of line it only adds its own frame where little of the caller is live.
-__device__ __attribute__((noinline)) double pow_call(double x, double y) { return pow(x, y); }
+// pow(x, y) outside int_pow's domain -- a shininess that is not a whole number
+// in 1..1024 (the parser takes any double, scene_loader.h:66-70).  dd_pow
+// (rt_pow.h) is the correctly rounded x^y in nearly all cases, so it agrees
+// with the reference's glibc pow (scene.h:113) wherever glibc is correctly
+// rounded (99.9 % of renderer-shaped operands; ocml's pow: 86 %); ocml's pow
+// remains for zero or non-finite operands and |y ln x| > 700.  Called out of
+// line: inlined, it would hold its registers across the whole render loop.
+__device__ __attribute__((noinline)) double pow_call(double x, double y) {
+  double v;
+  if (dd_pow_ok(x, y) && dd_pow(x, y, v)) return v;
+  return pow(x, y);
+}
 
 // pow(x, n) for the specular term's usual operands -- x in (0, 1 + 2^-40],
 // n a whole shininess in [1, 1024] (every scene here uses 5..200) -- by

@@ -20,7 +20,9 @@ def pytest_configure(config):
 
 
 def scene_path(name: str) -> str:
-    return os.path.join(SCENES, name + ".txt")
+    """A shipped scene, or a generated test scene (tests/golden/scenes, make_golden.py)."""
+    p = os.path.join(SCENES, name + ".txt")
+    return p if os.path.exists(p) else os.path.join(GOLDEN, "scenes", name + ".txt")
 
 
 def manifest() -> dict:

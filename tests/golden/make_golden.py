@@ -10,6 +10,16 @@ Sources of truth, in order:
 Every fixture is also rendered by the C restatement (oracle/oracle_cli) and the
 two must be byte-identical, which pins the oracle.
 
+Scenes with a fractional shininess (the parser takes any double,
+scene_loader.h:66-70; pow(rdv, shininess) at scene.h:113 then leaves the
+integer exponents every shipped scene has) are written by frac_scenes() into
+tests/golden/scenes/: complex.txt with each shininess s -> 0.73 s + 0.5 (3
+decimals), and a camera inside a cloud of mirrors with shininess drawn from
+[0.5, 2000).
+
+  python tests/golden/make_golden.py [NAME ...]   (default: every config;
+  named configs are re-rendered and merged into the existing manifest)
+
 Committed output per config: <name>.ppm.xz (binary P6 of the RGB8 bytes) and an
 entry in manifest.json with the SHA-256 of the reference's P3 text, the SHA-256
 of the RGB8 bytes, and the oracle's ray counts.
@@ -26,6 +36,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 ORACLE = os.path.join(REPO, "oracle")
 SCENES = os.path.join(REPO, "cs420-ray-tracer_amd", "scenes")
+GSCENES = os.path.join(HERE, "scenes")  # generated test scenes (frac_scenes)
 
 # name, scene, W, H, depth, source
 CONFIGS = [
@@ -44,7 +55,41 @@ CONFIGS = [
     ("simple_1080x720_d3", "simple", 1080, 720, 3, "ref_render"),
     ("medium_1080x720_d3", "medium", 1080, 720, 3, "ref_render"),
     ("complex_1080x720_d3", "complex", 1080, 720, 3, "ref_render"),
+    # fractional shininess: pow(rdv, shininess) off the integer exponents
+    ("complexfrac_960x540_d4", "complexfrac", 960, 540, 4, "ref_render"),
+    ("mirrorfrac_320x240_d6", "mirrorfrac", 320, 240, 6, "ref_render"),
 ]
+
+
+def frac_scenes():
+    """Writes tests/golden/scenes/{complexfrac,mirrorfrac}.txt (deterministic)."""
+    import random
+
+    os.makedirs(GSCENES, exist_ok=True)
+    out = []
+    for line in open(os.path.join(SCENES, "complex.txt")):
+        t = line.split()
+        if t and t[0] == "sphere" and len(t) >= 11:
+            t[10] = "%.3f" % (0.73 * float(t[10]) + 0.5)
+            line = " ".join(t) + "\n"
+        out.append(line)
+    with open(os.path.join(GSCENES, "complexfrac.txt"), "w") as f:
+        f.write("# complex.txt with shininess s -> 0.73 s + 0.5 (tests/golden/make_golden.py)\n" + "".join(out))
+    rng = random.Random(2026)
+    lines = ["# camera inside a cloud of mirrors, fractional shininess (tests/golden/make_golden.py)"]
+    for _ in range(300):
+        lines.append("sphere %.4f %.4f %.4f %.4f %.3f %.3f %.3f %.2f 0.5 %.3f" % (
+            rng.uniform(-14, 14), rng.uniform(-14, 14), rng.uniform(-14, 14), rng.uniform(0.6, 2.2), rng.random(),
+            rng.random(), rng.random(), rng.choice([0.0, 0.5, 0.8, 0.9, 1.0]), rng.uniform(0.5, 2000.0)))
+    lines += ["light 0 30 0 1 1 1 1", "light 20 -10 25 0.6 0.5 0.4 1", "light -3 2 1 0.9 0.9 0.7 1",
+              "ambient 0.1 0.1 0.1", "camera 0.3 0.2 0.1 5 1 -7 80"]
+    with open(os.path.join(GSCENES, "mirrorfrac.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def scene_file(scene: str) -> str:
+    p = os.path.join(SCENES, scene + ".txt")
+    return p if os.path.exists(p) else os.path.join(GSCENES, scene + ".txt")
 
 
 def parse_p3(data: bytes):
@@ -67,10 +112,17 @@ def p3_bytes(rgb: bytes, w: int, h: int) -> bytes:
 
 def main():
     subprocess.check_call(["make", "-s", "-C", ORACLE])
+    frac_scenes()
+    only = set(sys.argv[1:])
     manifest = {}
+    if only:
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            manifest = json.load(f)
     tmp = tempfile.mkdtemp(prefix="golden_")
     for name, scene, w, h, d, src in CONFIGS:
-        scene_path = os.path.join(SCENES, scene + ".txt")
+        if only and name not in only:
+            continue
+        scene_path = scene_file(scene)
         if src == "ray_serial":
             assert (w, h, d) == (1280, 720, 10)
             subprocess.check_call([os.path.join(ORACLE, "_ref", "ray_serial"), scene_path],

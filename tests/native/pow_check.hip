@@ -1,6 +1,8 @@
 // GPU-side check of the specular pow (tests/test_gpu_powcheck.py): for host-given
-// (x, n) pairs, writes ocml's pow(x, n) and rtk::int_pow(x, n) (rt_device.h) so
-// the test can compare both with the host's glibc pow -- the reference's.
+// operand pairs, writes ocml's pow, rtk::int_pow (rt_device.h, whole exponents)
+// and rtk::pow_call -- the product's path for every other exponent: rtk::dd_pow
+// (rt_pow.h), ocml's pow outside its domain -- so the test can compare them with
+// the host's glibc pow (the reference's) and pow_call with dd_pow's host build.
 #include <hip/hip_runtime.h>
 
 #include "../../cs420-ray-tracer_amd/csrc/rt_device.h"
@@ -13,26 +15,49 @@ __global__ void pow_kernel(const double *x, const int *n, double *ocml, double *
   dd[i] = rtk::int_pow_ok(x[i], (double)n[i], k) ? rtk::int_pow(x[i], k) : -1.0;
 }
 
-extern "C" int powcheck_run(const double *hx, const int *hn, double *hocml, double *hdd, long long count) {
-  double *x = nullptr, *o = nullptr, *d = nullptr;
-  int *n = nullptr;
-  const size_t bd = (size_t)count * sizeof(double), bi = (size_t)count * sizeof(int);
-  if (hipMalloc(&x, bd) != hipSuccess || hipMalloc(&o, bd) != hipSuccess || hipMalloc(&d, bd) != hipSuccess ||
-      hipMalloc(&n, bi) != hipSuccess)
-    return 1;
+__global__ void powf_kernel(const double *x, const double *y, double *ocml, double *prod, long long count) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  ocml[i] = pow(x[i], y[i]);
+  prod[i] = rtk::pow_call(x[i], y[i]);
+}
+
+namespace {
+template <class T>
+int run(const double *hx, const T *hy, double *ha, double *hb, long long count) {
+  double *x = nullptr, *a = nullptr, *b = nullptr;
+  T *y = nullptr;
+  const size_t bd = (size_t)count * sizeof(double), by = (size_t)count * sizeof(T);
   int rc = 0;
-  if (hipMemcpy(x, hx, bd, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(n, hn, bi, hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMalloc(&x, bd) != hipSuccess || hipMalloc(&a, bd) != hipSuccess || hipMalloc(&b, bd) != hipSuccess ||
+      hipMalloc(&y, by) != hipSuccess)
+    rc = 1;
+  if (!rc && (hipMemcpy(x, hx, bd, hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(y, hy, by, hipMemcpyHostToDevice) != hipSuccess))
     rc = 2;
   if (!rc) {
-    hipLaunchKernelGGL(pow_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, 0, x, n, o, d, count);
-    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(hocml, o, bd, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(hdd, d, bd, hipMemcpyDeviceToHost) != hipSuccess)
+    const dim3 grid((unsigned)((count + 255) / 256));
+    if constexpr (sizeof(T) == sizeof(double))
+      hipLaunchKernelGGL(powf_kernel, grid, dim3(256), 0, 0, x, (const double *)y, a, b, count);
+    else
+      hipLaunchKernelGGL(pow_kernel, grid, dim3(256), 0, 0, x, (const int *)y, a, b, count);
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(ha, a, bd, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(hb, b, bd, hipMemcpyDeviceToHost) != hipSuccess)
       rc = 3;
   }
-  (void)hipFree(x);
-  (void)hipFree(o);
-  (void)hipFree(d);
-  (void)hipFree(n);
+  if (x) (void)hipFree(x);
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  if (y) (void)hipFree(y);
   return rc;
+}
+}  // namespace
+
+extern "C" int powcheck_run(const double *hx, const int *hn, double *hocml, double *hdd, long long count) {
+  return run(hx, hn, hocml, hdd, count);
+}
+
+// fractional (any) exponents: ocml's pow and the product's pow_call
+extern "C" int powcheck_frac_run(const double *hx, const double *hy, double *hocml, double *hprod, long long count) {
+  return run(hx, hy, hocml, hprod, count);
 }

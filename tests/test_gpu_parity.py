@@ -235,7 +235,18 @@ def test_4k_shards_match_sampled_oracle_rows(gpu_renderer):
         assert full[y].tobytes() == rgb, f"row {y}"
 
 
-def _random_scene(seed: int, n: int) -> str:
+FRAC_SHININESS = (0.5, 7.5, 33.3, 1500.25)
+
+
+def _shininess(rng, frac: bool) -> str:
+    """Whole shininess (int_pow), or fractional (dd_pow: scene.h:113's pow off
+    the integers): fixed values and uniform draws in [0.5, 2000)."""
+    if not frac:
+        return "%d" % rng.choice([1, 5, 20, 100])
+    return "%.3f" % (rng.choice(FRAC_SHININESS) if rng.random() < 0.5 else rng.uniform(0.5, 2000.0))
+
+
+def _random_scene(seed: int, n: int, frac: bool = False) -> str:
     """Dense random scenes: tiny and huge spheres, spheres behind and around the
     camera, the camera inside a sphere for some seeds, many lights."""
     import random
@@ -244,9 +255,9 @@ def _random_scene(seed: int, n: int) -> str:
     lines = []
     for _ in range(n):
         r = rng.choice([0.01, 0.05, 0.2, 0.5, 1.0, 3.0]) * rng.uniform(0.5, 1.5)
-        lines.append("sphere %.6f %.6f %.6f %.6f %.3f %.3f %.3f %.2f 0.5 %d" % (
+        lines.append("sphere %.6f %.6f %.6f %.6f %.3f %.3f %.3f %.2f 0.5 %s" % (
             rng.uniform(-12, 12), rng.uniform(-8, 8), rng.uniform(-40, 10), r, rng.random(), rng.random(),
-            rng.random(), rng.choice([0.0, 0.0, 0.3, 0.7, 1.0]), rng.choice([1, 5, 20, 100])))
+            rng.random(), rng.choice([0.0, 0.0, 0.3, 0.7, 1.0]), _shininess(rng, frac)))
     for _ in range(rng.randint(1, 6)):
         lines.append("light %.3f %.3f %.3f %.3f %.3f %.3f 1" % (rng.uniform(-15, 15), rng.uniform(-5, 15),
                                                                rng.uniform(-30, 10), rng.random(), rng.random(),
@@ -275,6 +286,57 @@ def test_random_dense_scenes_vs_oracle(gpu_renderer, seed):
         assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
                                                                        counts["reflect"])
     gpu_renderer.set_culling(True)
+
+
+def _pm1(got: bytes, want: bytes):
+    """The north star's bar: every channel within 1 of the oracle's; returns the
+    number of differing channels (expected 0: the kernel is exact where the pow
+    agrees with glibc's, and a 1-ulp pow difference moves a byte only next to a
+    quantisation boundary)."""
+    d = np.abs(np.frombuffer(got, np.uint8).astype(np.int16) - np.frombuffer(want, np.uint8).astype(np.int16))
+    assert d.size and int(d.max()) <= 1, diff_summary(got, want)
+    return int((d > 0).sum())
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fractional_shininess_scenes_vs_oracle(gpu_renderer, seed):
+    """Dense random scenes whose shininess is fractional (0.5, 7.5, 33.3,
+    1500.25 and uniform draws in [0.5, 2000)): pow(rdv, shininess) is dd_pow
+    (rt_pow.h), the oracle's is glibc's.  Bar: +-1 per channel and identical ray
+    counts; the number of differing channels is printed (measured: 0)."""
+    import orc
+    import rt_hip
+
+    text = _random_scene(1000 + seed, 60 + 40 * seed, frac=True)
+    W, H, D = 96, 64, 5
+    sc = rt_hip.Scene.parse(text)
+    gpu_renderer.upload(sc)
+    ref, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=4)
+    rgb, st = gpu_renderer.render(sc.camera(), W, H, D)
+    nd = _pm1(bytes(rgb), ref)
+    print(f"fractional shininess, seed {seed}: {nd} of {len(ref)} channels differ")
+    assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
+                                                                   counts["reflect"])
+
+
+@pytest.mark.parametrize("n", [400, 1300], ids=["render_deferred", "render_deferred_walk"])
+def test_fractional_shininess_mirror_cloud_vs_oracle(gpu_renderer, n):
+    """A camera inside a cloud of mirrors with fractional shininess: every
+    reflection level (merged megakernel, render_deferred / render_deferred_walk)
+    shades with dd_pow.  +-1 per channel, identical ray counts."""
+    import orc
+    import rt_hip
+
+    W, H, D = 192, 144, 6
+    text = _mirror_cloud(11, n, frac=True)
+    sc = rt_hip.Scene.parse(text)
+    gpu_renderer.upload(sc)
+    ref, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=8)
+    rgb, st = gpu_renderer.render(sc.camera(), W, H, D)
+    nd = _pm1(bytes(rgb), ref)
+    print(f"fractional shininess mirror cloud n={n}: {nd} of {len(ref)} channels differ")
+    assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
+                                                                   counts["reflect"])
 
 
 def test_cull_equals_bruteforce_at_4k(gpu_renderer):
@@ -432,7 +494,7 @@ def test_large_scenes_global_memory_paths(monkeypatch, walk, seed, count):
         r.close()
 
 
-def _mirror_cloud(seed: int, n: int) -> str:
+def _mirror_cloud(seed: int, n: int, frac: bool = False) -> str:
     """A camera inside a cloud of mirrors: nearly every pixel reflects at least
     twice, so the level-2 rays outnumber the deferred queue's room."""
     import random
@@ -440,9 +502,10 @@ def _mirror_cloud(seed: int, n: int) -> str:
     rng = random.Random(seed)
     lines = []
     for _ in range(n):
-        lines.append("sphere %.6f %.6f %.6f %.6f %.3f %.3f %.3f %.2f 0.5 %d" % (
+        lines.append("sphere %.6f %.6f %.6f %.6f %.3f %.3f %.3f %.2f 0.5 %s" % (
             rng.uniform(-14, 14), rng.uniform(-14, 14), rng.uniform(-14, 14), rng.uniform(0.6, 2.2),
-            rng.random(), rng.random(), rng.random(), rng.choice([0.8, 0.9, 1.0]), rng.choice([5, 20, 60])))
+            rng.random(), rng.random(), rng.random(), rng.choice([0.8, 0.9, 1.0]),
+            _shininess(rng, True) if frac else "%d" % rng.choice([5, 20, 60])))
     lines.append("light 0 30 0 1 1 1 1")
     lines.append("light 20 -10 25 0.6 0.5 0.4 1")
     lines.append("ambient 0.1 0.1 0.1")

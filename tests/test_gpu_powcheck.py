@@ -1,7 +1,9 @@
 """The specular term's pow on the GPU against the reference's (glibc pow, via
-numpy on the host): ocml's general pow and rtk::int_pow (rt_device.h,
+math.pow on the host): ocml's general pow and rtk::int_pow (rt_device.h,
 double-double binary exponentiation for whole shininess) on 4M operand pairs
-shaped like the renderer's (rdv in (0, 1], many near 1; shininess 1..256).
+shaped like the renderer's (rdv in (0, 1], many near 1; shininess 1..256);
+and the product's pow for every other shininess (rtk::dd_pow, rt_pow.h) on
+fractional exponents against glibc and its own host build.
 glibc's pow is within 0.52 ulp, not always correctly rounded, so neither
 device pow matches it everywhere; int_pow is correctly rounded in nearly all
 cases and disagrees with glibc 150x less often than ocml's pow (0.09 % vs
@@ -48,3 +50,34 @@ def test_int_pow_vs_glibc_and_ocml():
     print(f"mismatches vs glibc over {used.sum()} pairs: int_pow {bad_dd}, ocml pow {bad_ocml}")
     # measured: int_pow 3,869 (0.09 %, where glibc is not correctly rounded), ocml 570,344 (14 %)
     assert bad_dd <= 0.005 * used.sum() and bad_dd <= bad_ocml
+
+
+@pytest.mark.gpu
+def test_fractional_pow_vs_glibc_and_host_build():
+    """The product's pow for exponents int_pow does not take (rtk::pow_call ->
+    rtk::dd_pow, rt_pow.h) on 2M renderer-shaped pairs with fractional shininess
+    (tests/test_pow.py's operands): bit-identical to dd_pow's host build, within
+    1 ulp of glibc's pow everywhere and equal to it on >= 99.9 % of the pairs
+    (ocml's pow: reported alongside)."""
+    import torch  # noqa: F401
+
+    from test_pow import dd_pow, operands
+
+    lib = C.CDLL(LIB)
+    P = C.POINTER(C.c_double)
+    lib.powcheck_frac_run.argtypes = [P, P, P, P, C.c_longlong]
+    x, y = operands(1 << 21)
+    ocml, prod = np.empty_like(x), np.empty_like(x)
+    assert lib.powcheck_frac_run(x.ctypes.data_as(P), y.ctypes.data_as(P), ocml.ctypes.data_as(P),
+                                 prod.ctypes.data_as(P), len(x)) == 0
+    host = dd_pow(x, y)
+    used = ~np.isnan(host)  # dd_pow's domain; elsewhere pow_call is ocml's pow
+    assert np.array_equal(prod[used].view(np.uint64), host[used].view(np.uint64)), "device dd_pow != host build"
+    assert np.array_equal(prod[~used].view(np.uint64), ocml[~used].view(np.uint64))
+    ref = np.fromiter(map(math.pow, x.tolist(), y.tolist()), np.float64, len(x))
+    assert np.all(np.abs(prod - ref) <= np.spacing(ref) * 1.0001)
+    bad = np.count_nonzero(prod[used] != ref[used])
+    bad_ocml = np.count_nonzero(ocml[used] != ref[used])
+    print(f"fractional exponents, mismatches vs glibc over {used.sum()} pairs: dd_pow {bad} "
+          f"({bad / used.sum():.4%}), ocml pow {bad_ocml} ({bad_ocml / used.sum():.2%})")
+    assert bad <= 0.001 * used.sum() and bad < bad_ocml
