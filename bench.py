@@ -28,6 +28,15 @@ Also reported:
                 `algorithmic_equivalent`: the kernel prunes pairs exactly, so
                 that rate measures the algorithm and exceeds the peak.
   hbm_write     the north star's HBM-write roofline: W*H*3 bytes per frame.
+  single_frame  ONE frame of a view the context has not rendered (the camera
+                moved per sample: no camera grid, the tile order rebuilt), one
+                launch, median of 5 -- the still frame the reference times
+                (src/main.cpp:139-161): in-stream kernel ms and host wall ms.
+  moving_camera frames of 32 distinct camera positions per launch (no camera
+                grid): the batched rate without the static-view assumption.
+  e2e           the drop-in path end to end, fresh context: parse + rt_create +
+                rt_upload_scene (BVH, light grids) + render (tile order,
+                scratch, kernel, D2H) + rt_write_ppm P3 (src/main.cpp:93-163).
   cpu_baseline  the reference's own trace_ray (oracle/_ref/ref_render, built
                 from /root/reference/src/main.cpp) on 1 host core, same
                 workload, rank 0 at N=1 only; falls back to the C port
@@ -115,8 +124,115 @@ def cpu_baseline(scene_file: str, W: int, H: int, D: int, rays_per_frame: int, t
             "sample": f"{what}; {W}x{H} d{D}, {rays} rays in {secs:.3f} s on {threads} thread(s) of {cpu_model()}"}
 
 
+def moved(rt_hip, cam, dx):
+    """A copy of `cam` with its position moved by dx along x (same basis)."""
+    c = rt_hip.rt_camera.from_buffer_copy(cam)
+    c.position[0] = cam.position[0] + dx
+    return c
+
+
+def median(xs):
+    xs = sorted(xs)
+    return xs[len(xs) // 2] if len(xs) % 2 else 0.5 * (xs[len(xs) // 2 - 1] + xs[len(xs) // 2])
+
+
+def info_or_none(r):
+    """rt_get_info, or None for an older diagnostic build (RT_HIP_LIB) without it."""
+    try:
+        return r.info()
+    except AttributeError:
+        return None
+
+
+def single_frame(rt_hip, r, cam, W, H, D, rows, out_ptr, samples=5):
+    """One-frame launches, each from a camera position the context has not seen
+    (moved 1e-3 further along x per sample), after one untimed such launch: the
+    reference's timed region (main.cpp:139-161) on a steady-state context."""
+    import time as _t
+
+    kms, wall, rate = [], [], []
+    before = info_or_none(r)
+    for k in range(samples + 1):
+        c = moved(rt_hip, cam, 1e-3 * (k + 1))
+        t0 = _t.perf_counter()
+        r.render_async(c, W, H, D, rows, out_ptr)
+        st = r.stats()  # waits for the stream
+        dt = (_t.perf_counter() - t0) * 1e3
+        if k:
+            kms.append(st.kernel_ms)
+            wall.append(dt)
+            rate.append(st.rays / st.kernel_ms / 1e3)
+    after = info_or_none(r)
+    return {"kernel_ms": round(median(kms), 4), "wall_ms": round(median(wall), 4),
+            "mrays_per_s": round(median(rate), 1), "samples": samples,
+            "camera_grid_used": bool(after.cam_grid_last) if after else None,
+            "camera_grid_builds": after.cam_grid_builds - before.cam_grid_builds if after else None,
+            "tile_order_builds": after.tile_order_builds - before.tile_order_builds if after else None,
+            "what": "one frame per launch, each from a camera position not rendered before (camera moved 1e-3 per "
+                    "sample): no camera grid, tile order rebuilt per frame (in wall_ms); median of %d" % samples}
+
+
+def moving_camera(rt_hip, torch, r, cam, W, H, D, rows, shard, F, launches=2):
+    """Launches of F frames whose camera positions all differ (an orbit-like
+    sequence moved 1e-3 per frame): no camera grid."""
+    import time as _t
+
+    cams = [moved(rt_hip, cam, 1e-3 * (f + 1)) for f in range(F)]
+    R = rows.count
+    r.render_frames_async(cams, W, H, D, rows, shard.data_ptr(), R * W * 3)  # untimed: order built, scratch sized
+    r.stats()
+    torch.cuda.synchronize()
+    t0 = _t.perf_counter()
+    for _ in range(launches):
+        r.render_frames_async(cams, W, H, D, rows, shard.data_ptr(), R * W * 3)
+    st = r.stats()
+    el = _t.perf_counter() - t0
+    ktimes = r.kernel_times(launches)
+    return {"mrays_per_s": round(st.rays * launches / el / 1e6, 1), "frames": F * launches,
+            "ms_per_frame": round(el / (F * launches) * 1e3, 4),
+            "kernel_ms_per_frame": round(sum(ktimes) / (F * launches), 4),
+            "camera_grid_used": bool(r.info().cam_grid_last),
+            "what": "%d launches of %d frames, every frame's camera position distinct (moved 1e-3 per frame)"
+                    % (launches, F)}
+
+
+def end_to_end(rt_hip, scene_file, W, H, D, device, runs=3):
+    """The drop-in path end to end in a fresh context (what ray_hip does):
+    parse, rt_create, rt_upload_scene, one synchronous render to host memory,
+    rt_write_ppm P3.  Median over `runs` of each part and of the total."""
+    import tempfile
+    import time as _t
+
+    parts = {k: [] for k in ("parse_ms", "create_ms", "upload_ms", "render_ms", "write_p3_ms", "total_ms")}
+    with tempfile.TemporaryDirectory() as tmp:
+        out = os.path.join(tmp, "output_gpu.ppm")
+        for _ in range(runs):
+            t = [_t.perf_counter()]
+            sc = rt_hip.Scene.load(scene_file)
+            cam = sc.camera()
+            t.append(_t.perf_counter())
+            r = rt_hip.Renderer(device)
+            t.append(_t.perf_counter())
+            r.upload(sc)
+            t.append(_t.perf_counter())
+            rgb, st = r.render(cam, W, H, D)
+            t.append(_t.perf_counter())
+            rt_hip.write_ppm(out, rgb, W, H)
+            t.append(_t.perf_counter())
+            r.close()
+            for k, (a, b) in zip(list(parts)[:5], zip(t, t[1:])):
+                parts[k].append((b - a) * 1e3)
+            parts["total_ms"].append((t[-1] - t[0]) * 1e3)
+            kernel_ms, rays = st.kernel_ms, st.rays
+        size = os.path.getsize(out)
+    res = {k: round(median(v), 3) for k, v in parts.items()}
+    res.update({"kernel_ms": round(kernel_ms, 4), "rays": rays, "p3_bytes": size, "runs": runs,
+                "mrays_per_s_end_to_end": round(rays / median(parts["total_ms"]) / 1e3, 1)})
+    return res
+
+
 def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, cull=True, batch=4, dist_on=None,
-            depth=None):
+            depth=None, extras=False):
     import rt_frames
 
     if dist_on is None:
@@ -197,6 +313,7 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     frames(max(warmup, F))
     render(shards[0][0])  # one single-frame launch (untimed): the ray counts of ONE frame of this rank's shard
     st = r.stats()  # syncs
+    info_warm = r.info()  # the camera grid / tile order the timed launches use (built in warmup)
     r.kernel_times()  # drop warmup launches from the history
     if dist_on:
         dist.barrier()
@@ -236,6 +353,17 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
         r.render_async(cam, W, H, D, rt_hip.rt_rows(1, 0, 1, H), full.data_ptr())
         torch.cuda.synchronize()
         assembled_ok = bool(torch.equal(full, image))
+    info_timed = r.info()
+    camera_grid = {"used_by_timed_launches": bool(info_timed.cam_grid_last), "cells_per_face_edge": info_timed.cam_grid_n,
+                   "builds_in_warmup": info_warm.cam_grid_builds,
+                   "builds_in_timed_region": info_timed.cam_grid_builds - info_warm.cam_grid_builds,
+                   "build_ms_total": round(info_warm.cam_grid_build_ms, 2),
+                   "tile_order_builds_in_timed_region": info_timed.tile_order_builds - info_warm.tile_order_builds,
+                   "upload_ms": round(info_timed.upload_ms, 2)}
+    extra = {}
+    if extras and not dist_on:
+        extra["single_frame"] = single_frame(rt_hip, r, cam, W, H, D, rows, shards[0][0].data_ptr())
+        extra["moving_camera"] = moving_camera(rt_hip, torch, r, cam, W, H, D, rows, shards[0], F)
     gather_ms = None
     if dist_on and steps > 0:
         # untimed: one batch's RCCL gather to rank 0 alone ("plus the
@@ -257,7 +385,8 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
             "launches_timed": len(ktimes), "rows_per_rank": R, "tests_exact": tests_exact,
             "tests_cull": tests_cull, "cull": cull, "gather_ms_per_batch": gather_ms,
             "rank_kernel_ms_per_frame": rank_kernel_ms, "world_size_seen": seen_world,
-            "warmup_frames_rendered": max(warmup, F), "launch_frames": rt_frames.batch_sizes(steps, F)}
+            "warmup_frames_rendered": max(warmup, F), "launch_frames": rt_frames.batch_sizes(steps, F),
+            "camera_grid": camera_grid, **extra}
 
 
 def main():
@@ -268,6 +397,8 @@ def main():
     ap.add_argument("--workload", default="synth200_1920x1080_d4", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-also", action="store_true", help="skip the complex.txt north-star line item")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the single-frame, moving-camera and end-to-end line items (N = 1 only)")
     ap.add_argument("--frames-per-launch", "--frames-per-gather", dest="frames_per_launch", type=int, default=32,
                     help="frames rendered by one kernel launch (rt_render_frames_async, 1..32); for N > 1 also "
                          "the frames per RCCL gather to rank 0 (one collective per batch)")
@@ -298,17 +429,26 @@ def main():
 
     cull = not args.brute_force
     batch = max(1, min(rt_hip.MAX_FRAMES, args.frames_per_launch))
+    extras = world == 1 and not args.no_extras
     m = measure(rt_hip, torch, dist, args.workload, args.steps, args.warmup, world, rank, local, cull, batch, dist_on,
-                args.depth)
+                args.depth, extras)
     also = {}
     if not args.no_also and args.workload != "complex_1920x1080_d4":
         a = measure(rt_hip, torch, dist, "complex_1920x1080_d4", max(args.steps // 2, 5), 2, world, rank, local,
-                    cull, batch, dist_on)
+                    cull, batch, dist_on, extras=extras)
         also["complex_1920x1080_d4"] = {
             "mrays_per_s": round(a["frame_rays"] * max(args.steps // 2, 5) / a["elapsed"] / 1e6, 2),
             "ms_per_frame": round(a["elapsed"] / max(args.steps // 2, 5) * 1e3, 4),
             "kernel_ms_per_frame": round(a["kernel_ms_per_frame"], 4), "rays_per_frame": a["frame_rays"],
             "target_mrays_per_s": 1000}
+        for k in ("single_frame", "moving_camera"):
+            if k in a:
+                also["complex_1920x1080_d4"][k] = a[k]
+    e2e = {}
+    if extras and rank == 0:
+        for wl in (args.workload, "complex_1920x1080_d4"):
+            sn, W_, H_, D_ = WORKLOADS[wl]
+            e2e[wl] = end_to_end(rt_hip, os.path.join(PKG, "scenes", sn + ".txt"), W_, H_, D_, local)
 
     if rank == 0:
         value = m["frame_rays"] * args.steps / m["elapsed"] / 1e6
@@ -372,7 +512,12 @@ def main():
                            "gather_ms_per_frame": round(m["gather_ms_per_batch"] / batch, 4)}
                           if m.get("gather_ms_per_batch") is not None else {}),
                        "parallelism": f"rows cyclic {BAND}-row bands x {world} GPU, {batch} frames per launch" +
-                                      (f" + RCCL gather to rank 0 every {batch} frames" if dist_on else "")},
+                                      (f" + RCCL gather to rank 0 every {batch} frames" if dist_on else ""),
+                       # the timed frames all see the workload's one camera (the reference renders one fixed
+                       # view): the camera grid for that position is built once, in warmup (its cost below);
+                       # single_frame / moving_camera are the rates without that assumption
+                       "view": "static camera: every frame the scene file's view",
+                       "camera_grid": m["camera_grid"]},
             # achieved = the fp64 FLOPs the render kernels EXECUTE per frame
             # (rocprofv3 PMC, 64 x (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions,
             # profiles/pmc_traffic.json taken with these kernel sources) over the
@@ -419,6 +564,11 @@ def main():
                           "bytes_per_frame": out_bytes, "bytes_per_launch": out_bytes * batch},
             "also": also,
         }
+        for k in ("single_frame", "moving_camera"):
+            if k in m:
+                line[k] = m[k]
+        if e2e:
+            line["e2e"] = e2e
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(m["scene_file"], m["W"], m["H"], m["D"], m["frame_rays"])
             # ray_openmp's loop on the host cores this job may use (16 on the GPU box)

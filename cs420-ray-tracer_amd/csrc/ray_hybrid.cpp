@@ -260,7 +260,7 @@ int render_dynamic(const Opts &o, const rtc::CpuTracer &cpu, Gpu &gpu, std::vect
 
 int main(int argc, char **argv) {
   Opts o;
-  bool tile_set = false;
+  bool tile_set = false, threads_set = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto num = [&](int &dst) {
@@ -273,7 +273,7 @@ int main(int argc, char **argv) {
     else if (a == "--width") num(o.width);
     else if (a == "--height") num(o.height);
     else if (a == "--depth") num(o.depth);
-    else if (a == "--threads") num(o.threads);
+    else if (a == "--threads") { num(o.threads); threads_set = true; }
     else if (a == "--cpu-threshold") num(o.threshold);
     else if (a == "--device") num(o.device);
     else if (a == "--streams") num(o.streams);
@@ -283,6 +283,10 @@ int main(int argc, char **argv) {
   (void)tile_set;
   if (o.width < 1 || o.height < 1 || o.tile < 1 || o.streams < 1) {
     std::fprintf(stderr, "invalid size, tile size or stream count\n");
+    return 2;
+  }
+  if (threads_set && o.threads < 1) {  // no CPU worker would render the CPU tiles
+    std::fprintf(stderr, "--threads must be at least 1\n");
     return 2;
   }
   if (o.threads < 0) {  // OMP_NUM_THREADS (the reference's CPU section is OpenMP), else the cores but one

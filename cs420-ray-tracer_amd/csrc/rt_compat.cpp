@@ -147,7 +147,14 @@ void launch_gpu_kernel(rt_float3 *d_framebuffer, rt_gpu_sphere *d_spheres, int n
   if (rc == RT_OK)
     rc = rt_render_tile(s->ctx, &c, image_width, image_height, max_depth, tile_x, tile_y, tile_width, tile_height,
                         RT_FB_F32X3, d_framebuffer);
-  t_status = rc;
+  // The caller owns its streams and may destroy them between calls (the
+  // reference's render_hybrid creates and destroys three per call,
+  // main_hybrid.cpp:407-409, 489-491): the context must not keep the handle.
+  // Switching back to its own stream orders that stream after the tile
+  // (rt_set_stream records an event on the caller's stream, which is still
+  // alive here), so a later call on any stream also waits for it.
+  const int rs = rt_set_stream(s->ctx, nullptr);
+  t_status = rc != RT_OK ? rc : rs;
 }
 
 int rt_compat_status(void) { return t_status; }

@@ -853,7 +853,8 @@ __host__ __device__ inline LdsLayout lds_layout(bool lds_geo, int n, int nl, int
   LdsLayout L;
   L.rad = lds_geo ? (size_t)n * sizeof(SphGeo) : 0;
   L.light = lds_geo ? (size_t)n * (sizeof(SphGeo) + sizeof(double)) : 0;
-  size_t e = (L.light + (size_t)nl * sizeof(LightD) + 15) & ~(size_t)15;
+  // lights: staged only with a staged scene (stage_scene); otherwise read with scalar loads
+  size_t e = (L.light + (lds_geo ? (size_t)nl * sizeof(LightD) : 0) + 15) & ~(size_t)15;
   const bool bvh = lds_geo && nnodes > 0;
   L.nodes = e;
   if (bvh) e += (size_t)nnodes * sizeof(BvhNode);

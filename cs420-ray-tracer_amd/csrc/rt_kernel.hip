@@ -36,6 +36,7 @@
 #include "rt_device.h"
 #include "rt_sched.h"
 
+#include <chrono>
 #include <cmath>
 #include <vector>
 
@@ -90,12 +91,15 @@ struct RenderArgs {
   StackEnt *gstack;
   unsigned long long *counters;
   int ntx, ntiles;
-  int nslots;                     // kStackGlobal with perm: launch slots (perm entries); ntiles otherwise
+  int nslots;                     // wave slots per frame: kStackMerge tile groups, kStackGlobal with perm
+                                  // the listed blocks, else ntiles
   const int *perm;
   unsigned long long *zero_next;  // counters of the next launch, zeroed by workgroup 0 (or nullptr)
   QRay *dq;                       // kStackMerge: deferred deep rays, [kShards][dq_cap] (render_deferred)
   int dq_cap;                     // entries per shard segment; 0 = no deferral
   int merge_q;                    // kStackMerge: LDS ray-queue entries per wave (16..64)
+  int nsingle;                    // kStackMerge: the first nsingle tile slots (heaviest class) get a wave each
+  int pix_off;                    // kStackMerge: LDS offset of the wave's finished pixels (flush_tiles)
   int defer_level;                // kStackMerge: rays of this reflection level and deeper are deferred
 };
 // the whole struct is the kernel's argument block (kernarg segment, at most 4 KiB)
@@ -500,25 +504,50 @@ constexpr int kDeferLevel = RT_DEFER_LEVEL;
 #define RT_DEFER_CAP_DIV 8  // deferred-queue room: 1 / RT_DEFER_CAP_DIV of the launch's pixels
 #endif
 constexpr int kDeferSlot = 7;
+constexpr size_t kPixbufBytes = (size_t)kMergeTiles * 64 * 3;  // merge_tiles' finished pixels, RGB8 (LDS)
 // u64 slot of a counter shard: the deferred kernels' next queue entry of that
 // shard segment (lanes take entries dynamically; zeroed with the launch's counters)
 constexpr int kFetchSlot = 24;
 constexpr long long kSchedMinTiles = 1024;  // launches with fewer 8x8 tiles keep scanline order
 
-// Stores a pixel's final colour (quantised as write_ppm, main.cpp:85) at out + 3 pix.
-__device__ __forceinline__ void store_px(uint8_t *out, unsigned pix, D3 c, bool img, unsigned &c_neg) {
-  int q0 = 0, q1 = 0, q2 = 0;  // padding rows of a shard: zeros
-  if (img) {
-    q0 = quantize(c.x), q1 = quantize(c.y), q2 = quantize(c.z);
-    c_neg += (q0 < 0) + (q1 < 0) + (q2 < 0);
-  }
-  uint8_t *px = out + (size_t)pix * 3;
-#if RT_ABL == 11  // ablation (wrong images): no pixel stores
-  if (q0 + q1 + q2 != -7) return;
+// A pixel's final colour quantised as write_ppm (main.cpp:85), packed r | g << 8 | b << 16.
+__device__ __forceinline__ unsigned pack_px(D3 c, unsigned &c_neg) {
+  const int q0 = quantize(c.x), q1 = quantize(c.y), q2 = quantize(c.z);
+  c_neg += (q0 < 0) + (q1 < 0) + (q2 < 0);
+  return (unsigned)(q0 < 0 ? 0 : q0) | (unsigned)(q1 < 0 ? 0 : q1) << 8 | (unsigned)(q2 < 0 ? 0 : q2) << 16;
+}
+
+// A deferred ray's pixel (render_deferred*): its 3 bytes at out + 3 pix are
+// OR-ed into the one or two dwords that hold them.  merge_tiles stored the
+// pixel's tile as dword rows with zero bytes in this pixel's place, and the
+// neighbours in those dwords may be other deferred pixels being OR-ed at the
+// same time: a dword atomic OR per covered dword, no byte stores.
+#ifndef RT_SINGLE
+#define RT_SINGLE 1
 #endif
-  px[0] = (uint8_t)(q0 < 0 ? 0 : q0);
-  px[1] = (uint8_t)(q1 < 0 ? 0 : q1);
-  px[2] = (uint8_t)(q2 < 0 ? 0 : q2);
+#ifndef RT_DEFER_PX_ATOMIC
+#define RT_DEFER_PX_ATOMIC 1
+#endif
+#ifndef RT_PX_STAGE
+#define RT_PX_STAGE 1
+#endif
+__device__ __forceinline__ void or_px(uint8_t *out, unsigned pix, unsigned v) {
+#if RT_ABL == 11  // ablation (wrong images): no pixel stores
+  if (v != 0x5a5a5a5au) return;
+#endif
+#if !RT_DEFER_PX_ATOMIC
+  uint8_t *px = out + (size_t)pix * 3;
+  px[0] = (uint8_t)v;
+  px[1] = (uint8_t)(v >> 8);
+  px[2] = (uint8_t)(v >> 16);
+  return;
+#endif
+  const uintptr_t a = reinterpret_cast<uintptr_t>(out) + (uintptr_t)pix * 3;
+  unsigned *d = reinterpret_cast<unsigned *>(a & ~(uintptr_t)3);
+  const unsigned sh = (unsigned)(a & 3) * 8;
+  const unsigned long long w = (unsigned long long)v << sh;  // bytes sh/8 .. sh/8 + 2 of a dword pair
+  if ((unsigned)w) atomicOr(d, (unsigned)w);
+  if (sh > 8 && (unsigned)(w >> 32)) atomicOr(d + 1, (unsigned)(w >> 32));
 }
 
 // kMergeTiles tiles of one frame for one wave (see kStackMerge).  Every lane
@@ -533,6 +562,69 @@ __device__ __forceinline__ void store_px(uint8_t *out, unsigned pix, D3 c, bool 
 //     lanes whose chain ended from the queue.
 // A chain that ends unwinds its pixel's stack (sbase[sidx + level * sstride],
 // innermost first, main.cpp:54) and stores the pixel.
+// One pixel's 3 bytes at p (any alignment) written with dword atomics: its
+// bytes of each covering dword cleared (AND), then set (OR); the other bytes,
+// other pixels', are untouched whoever writes them meanwhile.
+__device__ __forceinline__ void put_px(uint8_t *p, unsigned v) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  unsigned *d = reinterpret_cast<unsigned *>(a & ~(uintptr_t)3);
+  const unsigned sh = (unsigned)(a & 3) * 8;
+  const unsigned long long m = 0xFFFFFFull << sh, w = (unsigned long long)v << sh;
+  atomicAnd(d, ~(unsigned)m);
+  if ((unsigned)w) atomicOr(d, (unsigned)w);
+  if (sh > 8) {
+    atomicAnd(d + 1, ~(unsigned)(m >> 32));
+    if ((unsigned)(w >> 32)) atomicOr(d + 1, (unsigned)(w >> 32));
+  }
+}
+
+// The finished pixels of a merge_tiles group wait in LDS as RGB8 bytes laid
+// out like the tiles' rows (tile slot t, row y, pixel x at t * 192 + y * 24 +
+// x * 3) until the group is done, then go out as the tiles' 24-byte rows, one
+// dword per lane (flush_tiles); a deferred pixel's bytes stay 0 for
+// render_deferred's or_px.
+typedef __attribute__((address_space(3))) unsigned char LdsU8;
+typedef __attribute__((address_space(3))) unsigned LdsU32;
+__device__ __forceinline__ void flush_tiles(const RenderArgs &a, int base, int nt, int frame, const LdsU8 *pixbuf) {
+  const int lane = (int)(threadIdx.x & 63);
+  const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
+  const Rows &rows = kernarg_late<true, offsetof(RenderArgs, rows)>(a.rows);
+  const int W = kernarg_late<true, offsetof(RenderArgs, W)>(a.W);
+  const int ntx = kernarg_late<true, offsetof(RenderArgs, ntx)>(a.ntx);
+  const int *perm = kernarg_late<true, offsetof(RenderArgs, perm)>(a.perm);
+  uint8_t *out = static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride;
+  for (int t = 0; t < nt; ++t) {
+    const int tile = perm ? perm[base + t] : base + t;
+    const int x0 = (tile % ntx) * 8, ty = tile / ntx;
+    const LdsU8 *pb = pixbuf + t * 192;
+    // a row of 8 pixels is 24 bytes = 6 dwords when it is whole and dword aligned
+    auto row_at = [&](int r) { return out + ((size_t)(ty * 8 + r) * W + x0) * 3; };
+    auto whole = [&](int r) {
+      return ty * 8 + r < rows.count && x0 + 8 <= W && (reinterpret_cast<uintptr_t>(row_at(r)) & 3) == 0;
+    };
+    {
+      const int r = lane / 6, c = lane - 6 * (lane / 6);  // lanes 0..47: row r, dword c = LDS dword lane
+      if (lane < 48 && whole(r)) {
+        const unsigned v = reinterpret_cast<const LdsU32 *>(pb)[lane];
+#if RT_ABL == 11  // ablation (wrong images): no pixel stores
+        if (v == 0x5a5a5a5au)
+#endif
+        reinterpret_cast<unsigned *>(row_at(r))[c] = v;
+      }
+    }
+    {
+      // rows that are not whole (the image's right edge, odd widths): the
+      // lane's own pixel into the dwords it shares with its neighbours (which
+      // other waves may be writing): its bytes cleared and set by dword atomics
+      const int r = lane >> 3, x = x0 + (lane & 7);
+      if (!whole(r) && ty * 8 + r < rows.count && x < W) {
+        const LdsU8 *p = pb + lane * 3;
+        put_px(row_at(r) + (lane & 7) * 3, (unsigned)p[0] | (unsigned)p[1] << 8 | (unsigned)p[2] << 16);
+      }
+    }
+  }
+}
+
 template <bool kCull, bool kFast>
 __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                             const SphMat *__restrict__ mat, const LightD *__restrict__ slight,
@@ -541,6 +633,11 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
   const int lane = (int)(threadIdx.x & 63);
   const unsigned long long lt = (1ull << lane) - 1ull;
   unsigned c_prim = 0, c_shadow = 0, c_reflect = 0, c_neg = 0;
+  // the finished pixels (flush_tiles), at an LDS offset the host placed after the walk stacks
+  auto pixbuf = [&]() { return (LdsU8 *)rt_dyn_lds + kernarg_late<true, offsetof(RenderArgs, pix_off)>(a.pix_off); };
+#pragma unroll
+  for (int i = 0; i < (int)(kPixbufBytes / 256) && RT_PX_STAGE; ++i)  // padding, depth 0 and deferred pixels: 0
+    reinterpret_cast<LdsU32 *>(pixbuf())[i * 64 + lane] = 0u;
   const int depth = a.depth;
   const unsigned sstride = (unsigned)ca.npx;
   int qn = 0;        // queued rays q[0 .. qn), wave-uniform, < Q between passes
@@ -550,6 +647,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
   D3 o = mk(0.0, 0.0, 0.0), d = o;
   int key = -1, dleft = 0, lev = 0;
   unsigned pix = 0;
+  int lpos = 0;  // the pixel's place in pixbuf
   // pops queued rays into the lanes without one (lanes ranked by lane id)
   auto refill = [&](unsigned long long busy) {
     const int take = (64 - __popcll(busy)) < qn ? (64 - __popcll(busy)) : qn;
@@ -561,19 +659,25 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
       key = e.key;
       dleft = e.dleft;
       pix = (unsigned)e.pix;
+      lpos = e.orig;
       lev = 1;
       act = true;
     }
     qn -= take;
   };
   while (true) {
+    // the group's tile slots: [base, base + nt) -- one slot for the first nsingle
+    // groups (the heaviest tiles: their own reflection rays fill the wave, and
+    // a frame's critical path is its slowest wave), kMergeTiles after them
     const int ntiles = kernarg_late<true, offsetof(RenderArgs, ntiles)>(a.ntiles);
-    const int nt = ntiles - group * kMergeTiles < kMergeTiles ? ntiles - group * kMergeTiles : kMergeTiles;
+    const int ns = RT_SINGLE ? kernarg_late<true, offsetof(RenderArgs, nsingle)>(a.nsingle) : 0;
+    const int base = group < ns ? group : ns + (group - ns) * kMergeTiles;
+    const int nt = group < ns ? 1 : (ntiles - base < kMergeTiles ? ntiles - base : kMergeTiles);
     bool tile_pass = false;
     if (__ballot(act) == 0) {
       if (next < nt) {  // camera rays of the next tile: camera.h:17-25, main.cpp:151-154 (as trace_tile)
         const int *perm = kernarg_late<true, offsetof(RenderArgs, perm)>(a.perm);
-        const int slot = group * kMergeTiles + next;
+        const int slot = base + next;
         const int tile = perm ? perm[slot] : slot;
         const int ntx = kernarg_late<true, offsetof(RenderArgs, ntx)>(a.ntx);
         const int tx = tile % ntx, ty = tile / ntx;
@@ -600,14 +704,14 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
 #endif
         o = mk(cam.px, cam.py, cam.pz);
         pix = (unsigned)(k * W + x);
+        lpos = next * 192 + (lane >> 3) * 24 + (lane & 7) * 3;
         key = -1;
         dleft = depth;
         lev = 0;
         act = in_img && depth >= 1;
         c_prim += act ? 1u : 0u;
-        if (in_tile && !act)  // depth <= 0 -> black (main.cpp:17-18); padding rows -> zeros
-          store_px(static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride, pix, mk(0.0, 0.0, 0.0),
-                   in_img, c_neg);
+        // depth <= 0 -> black (main.cpp:17-18), padding rows -> zeros: pixbuf's 0
+        (void)od;
         ++next;
         tile_pass = true;
         if (__ballot(act) == 0) continue;
@@ -649,8 +753,24 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
           const StackEnt e = ca.gstack[sidx + (unsigned)lev * sstride];
           res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
         }
-        const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
-        store_px(static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride, pix, res, true, c_neg);
+#if RT_PX_STAGE
+        {
+          const unsigned v = pack_px(res, c_neg);
+          LdsU8 *p = pixbuf() + lpos;
+          p[0] = (unsigned char)v;
+          p[1] = (unsigned char)(v >> 8);
+          p[2] = (unsigned char)(v >> 16);
+        }
+#else
+        {
+          const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
+          const unsigned v = pack_px(res, c_neg);
+          uint8_t *px = static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride + (size_t)pix * 3;
+          px[0] = (uint8_t)v;
+          px[1] = (uint8_t)(v >> 8);
+          px[2] = (uint8_t)(v >> 16);
+        }
+#endif
         act = false;
       }
     }
@@ -679,12 +799,20 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     if (tile_pass && next < nt && __popcll(busy) + qn < Q) {
       // this tile's reflection rays wait for the next tiles' (queue < Q entries)
       if (act)
-        q[qn + (int)__popcll(busy & lt)] = QRay{o.x, o.y, o.z, d.x, d.y, d.z, 0, dleft, key, (int)pix};
+        q[qn + (int)__popcll(busy & lt)] = QRay{o.x, o.y, o.z, d.x, d.y, d.z, lpos, dleft, key, (int)pix};
       qn += __popcll(busy);
       act = false;
     } else if (qn > 0 && busy != ~0ull) {
       refill(busy);  // lanes without a ray take queued ones
     }
+  }
+  {
+    const int ntiles = kernarg_late<true, offsetof(RenderArgs, ntiles)>(a.ntiles);
+    const int ns = RT_SINGLE ? kernarg_late<true, offsetof(RenderArgs, nsingle)>(a.nsingle) : 0;
+    const int base = group < ns ? group : ns + (group - ns) * kMergeTiles;
+    if (RT_PX_STAGE)
+      flush_tiles(a, base, group < ns ? 1 : (ntiles - base < kMergeTiles ? ntiles - base : kMergeTiles), frame,
+                  pixbuf());
   }
   sums[0] += wave_sum(c_prim);
   sums[1] += wave_sum(c_shadow);
@@ -773,7 +901,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
   const int slot = nf > 1 ? b / nf : b, frame = nf > 1 ? b - slot * nf : 0;
   int tile = slot;
   if constexpr (kStack == kStackMerge) {
-    if (slot * kMergeTiles >= a.ntiles) return;  // slot = this wave's group of kMergeTiles tile slots
+    if (slot >= a.nslots) return;  // slot = this wave's group of tile slots (merge_tiles)
   } else {
     if (a.perm) {
       if (slot >= a.nslots) return;
@@ -817,7 +945,9 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
 #endif
   if constexpr (kStack == kStackMerge && !kLdsGeo && kSamples == 1) {
     // the wave's ray queue sits where trace_wave parks colours (launch_tiles)
-    QRay *q = reinterpret_cast<QRay *>(ca.park);
+    // the wave's ray queue sits where trace_wave parks colours, after the
+    // finished-pixel bytes (launch_tiles)
+    QRay *q = reinterpret_cast<QRay *>(reinterpret_cast<unsigned char *>(ca.park) + kPixbufBytes);
     merge_tiles<kCull, kFast>(g, rad, sm, slight, a, slot, frame, ca, q, work, sums);
   } else {
     trace_tile<kCull, kSamples, kStack, !kLdsGeo>(g, rad, sm, slight, a.n, a.nl, a.amb, kernarg_cam(frame), a.W, a.H,
@@ -926,8 +1056,8 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
           }
           const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
           const unsigned f = pixg / npx_frame;
-          store_px(static_cast<uint8_t *>(od.ptr) + (size_t)f * (size_t)od.fstride, pixg - f * npx_frame, res, true,
-                   c_neg);
+          or_px(static_cast<uint8_t *>(od.ptr) + (size_t)f * (size_t)od.fstride, pixg - f * npx_frame,
+                pack_px(res, c_neg));
           act = false;
         }
       }
@@ -1055,8 +1185,8 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
           }
           const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
           const unsigned f = pixg / npx_frame;
-          store_px(static_cast<uint8_t *>(od.ptr) + (size_t)f * (size_t)od.fstride, pixg - f * npx_frame, res, true,
-                   c_neg);
+          or_px(static_cast<uint8_t *>(od.ptr) + (size_t)f * (size_t)od.fstride, pixg - f * npx_frame,
+                pack_px(res, c_neg));
           act = false;
         }
       }
@@ -1171,7 +1301,7 @@ struct rt_ctx {
   bool defer = true;          // RT_HIP_DEFER: kStackMerge defers rays of level >= kDeferLevel to render_deferred
   bool defer_walk = true;     // RT_HIP_DEFER_WALK: deferred rays of a scene whose closest hits always walk the BVH use render_deferred_walk
   int merge_q = 64;           // kStackMerge: the launch's LDS queue entries per wave (launch_render4 picks it)
-  int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (16, 32 or 64)
+  int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (8, 16, 32 or 64)
   int defer_level = kDeferLevel;  // RT_HIP_DEFER_LEVEL (>= 1)
   QRay *dq_buf = nullptr;     // its queue, grow-only
   size_t dq_bytes = 0;
@@ -1200,8 +1330,28 @@ struct rt_ctx {
   unsigned long long perm_gen = ~0ull;
   int *d_perm = nullptr, *h_perm = nullptr;  // h_perm pinned
   size_t perm_cap = 0;
+  long long perm_cls[kSchedClasses] = {};  // tiles per class of the cached order
+  // kStackMerge: tiles of this class and above get a wave each (RT_HIP_SINGLE_CLASS
+  // for every launch; kSchedClasses = none).  Default: class >= 1 in one-frame
+  // launches, whose end is their slowest wave (synth200 0.534 -> 0.451 ms,
+  // complex 0.451 -> 0.388), none in multi-frame launches, where the other
+  // frames fill that tail and four tiles per wave share their reflection
+  // rays' passes (class >= 1 there: 0.2285 -> 0.2364 ms per frame;
+  // profiles/r3c/ab_single.log)
+  int single_class = -1;
+  // rt_get_info: host-side builds made by the render calls
+  bool cg_last = false;
+  int cg_last_n = 0;
+  unsigned long long cg_builds = 0, perm_builds = 0;
+  double cg_build_ms = 0.0, perm_build_ms = 0.0, upload_ms = 0.0;
   std::string err;
 };
+
+namespace {
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace
 
 namespace {
 
@@ -1316,6 +1466,7 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
   const bool cached = c->cg_gen == c->scene_gen && std::memcmp(c->cg_pos, pos, sizeof pos) == 0;
   if (!cached) {
     if (!(c->cg_mode == 2 || nf >= kCgMinFrames || repeat)) return RT_OK;
+    const auto t0 = std::chrono::steady_clock::now();
     const int N = c->cg_n_opt ? c->cg_n_opt : kCgN;
     double d2 = 0.0;
     for (int k = 0; k < 3; k++) {
@@ -1351,6 +1502,8 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
       c->cg_n = N;
       c->cg_ok = true;
     }
+    c->cg_builds++;
+    c->cg_build_ms += ms_since(t0);
   }
   if (c->cg_ok) out = CgArgs{c->d_cg_start, c->d_cg_ent, c->cg_n, 1};
   return RT_OK;
@@ -1376,8 +1529,10 @@ int tile_perm(rt_ctx *c, const Cam &cam, int W, int H, const Rows &rows, const O
     out = c->d_perm;
     return RT_OK;
   }
+  const auto t0 = std::chrono::steady_clock::now();
   std::vector<int> perm;
-  tile_order(v, c->h_refl, perm);
+  long long cls[kSchedClasses] = {};
+  tile_order(v, c->h_refl, perm, cls);
   if ((long long)perm.size() != ntiles) return RT_ERR_INVALID_ARG;
   const size_t bytes = perm.size() * sizeof(int);
   RT_TRY(c, hipStreamSynchronize(c->stream));  // the previous order may still be in flight from h_perm
@@ -1395,9 +1550,17 @@ int tile_perm(rt_ctx *c, const Cam &cam, int W, int H, const Rows &rows, const O
   RT_TRY(c, hipMemcpyAsync(c->d_perm, c->h_perm, bytes, hipMemcpyHostToDevice, c->stream));
   c->perm_view = v;
   c->perm_gen = c->scene_gen;
+  for (int k = 0; k < kSchedClasses; k++) c->perm_cls[k] = cls[k];
   out = c->d_perm;
+  c->perm_builds++;
+  c->perm_build_ms += ms_since(t0);
   return RT_OK;
 }
+
+// (Re-)records the launch's start event just before its first kernel: the
+// host-side builds a launch may make first (tile order, camera grid) are not
+// kernel time.  enqueue() has recorded it already for launches with no kernel.
+hipError_t mark_start(rt_ctx *c) { return hipEventRecord(c->ev0[(int)(c->launches % rt_ctx::kRing)], c->stream); }
 
 template <bool kLds, bool kCull, int kSamples, int kStack>
 int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth, const Rows &rows,
@@ -1425,7 +1588,9 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       std::vector<unsigned char> mark((size_t)ntiles, 0);
       for (int i = 0; i < c->req_n; i++) {
         const rt_tile &t = c->req_tiles[i];
-        const int x1 = std::min(W, t.x + t.width), j1 = std::min(H, t.y + t.height);
+        // in 64 bits: a caller's x + width near INT_MAX must still clip to the image
+        const int x1 = (int)std::min<long long>(W, (long long)t.x + t.width);
+        const int j1 = (int)std::min<long long>(H, (long long)t.y + t.height);
         if (t.x >= x1 || t.y >= j1) continue;
         // framebuffer rows j (0 = bottom) are PPM rows H-1-j
         const int y0 = H - j1, y1 = H - 1 - t.y;
@@ -1453,14 +1618,14 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       batch_perm = c->d_bperm;
     }
   }
-  const dim3 grid((unsigned)(nslots * nf));
   D3 amb{c->amb[0], c->amb[1], c->amb[2]};
   lds = (lds + 31) & ~(size_t)31;
   // the kernel places the ordered walk's stacks from these same arguments
   if (bv.ordered)
     lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
   if (!kLds && kStack == kStackGlobal) lds += (size_t)kWg * 64 * sizeof(D3);  // parked colours (trace_wave)
-  if (kStack == kStackMerge) lds += (size_t)c->merge_q * sizeof(QRay);         // the wave's ray queue (merge_tiles)
+  if (kStack == kStackMerge)  // the wave's ray queue and finished pixels (merge_tiles)
+    lds += (size_t)c->merge_q * sizeof(QRay) + kPixbufBytes;
   StackEnt *gstack = nullptr;
   if (depth > 1) {
     // the kernel indexes the stack with 32 bits: entry + level * npx < 2^32
@@ -1479,6 +1644,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     gstack = reinterpret_cast<StackEnt *>(c->cstack_buf);
   }
   const int *perm = nullptr;
+  int nsingle = 0;
   // The heavy-first order pays off when a launch has many more tiles than the
   // chip has wave slots; a small launch (a hybrid driver's 64x64 tile) keeps
   // scanline order and skips building and uploading one (which waits for the
@@ -1488,7 +1654,15 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   } else if (c->sched && ntiles >= kSchedMinTiles) {
     int rc = tile_perm(c, cam, W, H, rows, od, 8 * kWx, 8 * kWy, ntiles, perm);
     if (rc != RT_OK) return rc;
+    if (kStack == kStackMerge) {  // the heaviest classes lead the order: one wave per tile for them
+      const int sc = c->single_class >= 0 ? c->single_class : (nf == 1 ? 1 : kSchedClasses);
+      long long heavy = 0;
+      for (int k = sc; k < kSchedClasses; k++) heavy += c->perm_cls[k];
+      nsingle = (int)std::min<long long>(heavy, ntiles);
+      nslots = nsingle + (ntiles - nsingle + kMergeTiles - 1) / kMergeTiles;
+    }
   }
+  const dim3 grid((unsigned)(nslots * nf));
   RenderArgs ra{};
   ra.geo = c->d_geo;
   ra.radius = c->d_rad;
@@ -1520,6 +1694,10 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.dq = nullptr;
   ra.dq_cap = 0;
   ra.merge_q = c->merge_q;
+  ra.nsingle = nsingle;
+  // merge_tiles' pixel bytes: after the scene and the walk stacks, where render_kernel's park/queue region starts
+  ra.pix_off = (int)(((lds_layout(kLds, c->nsph, c->nlight, bv.nnodes).end + 31) & ~(size_t)31) +
+                     (bv.ordered ? (size_t)kWg * bv.odepth * 64 * sizeof(int2) : 0));
   ra.defer_level = c->defer_level;
   if (kStack == kStackMerge && c->defer && depth > c->defer_level) {
     // room for 1/8 of the launch's pixels (deferred rays are ~2 % on synth200); a ray
@@ -1548,6 +1726,9 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       const int rc = cam_grid(c, cam, nf, ra.cg);
       if (rc != RT_OK) return rc;
     }
+    c->cg_last = ra.cg.on != 0;
+    c->cg_last_n = ra.cg.on ? ra.cg.N : 0;
+    RT_TRY(c, mark_start(c));  // the launch's timing starts after the host-side builds
     if (fast)
       hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, true>), grid, dim3(64 * kWg), lds, c->stream, ra);
     else
@@ -1564,6 +1745,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
         hipLaunchKernelGGL((render_deferred<kCull>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
     }
   } else {
+    RT_TRY(c, mark_start(c));
     hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
     if constexpr (kStack == kStackMerge) {
       if (ra.dq_cap > 0)
@@ -1585,8 +1767,8 @@ int launch_render4(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dept
       const BvhArgs bv = bvh_args(c, cam);
       const size_t stacks = bv.ordered ? (size_t)bv.odepth * 64 * sizeof(int2) : 0;
       if (od.fmt == RT_FB_RGB8 && !od.full && od.x0 == 0 && od.xw == W)
-        for (int q = c->merge_q_max; q >= 16; q /= 2)  // the longest queue that keeps 12 waves per CU
-          if (12 * (stacks + (size_t)q * sizeof(QRay) + ((lds + 31) & ~(size_t)31)) <= 160 * 1024) {
+        for (int q = c->merge_q_max; q >= 8; q /= 2)  // the longest queue that keeps 12 waves per CU
+          if (12 * (stacks + (size_t)q * sizeof(QRay) + kPixbufBytes + ((lds + 31) & ~(size_t)31)) <= 160 * 1024) {
             c->merge_q = q;
             return launch_tiles<kLds, kCull, 1, kStackMerge>(c, lds, cam, W, H, depth, rows, od);
           }
@@ -1632,6 +1814,8 @@ int enqueue(rt_ctx *c, const rt_camera *cm, int W, int H, int depth, const Rows 
   c->zero_pending = false;
   const int slot = (int)(c->launches % rt_ctx::kRing);
   RT_TRY(c, hipEventRecord(c->ev0[slot], c->stream));
+  c->cg_last = false;
+  c->cg_last_n = 0;
   if (r.count > 0) {
     const Cam cam = to_cam(*cm);
     // the scene and its BVH are staged in LDS when they fit (lds_layout)
@@ -1687,10 +1871,12 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_WALK")) c->defer_walk = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_LEVEL")) c->defer_level = std::max(1, std::min(RT_MAX_DEPTH, std::atoi(e)));
-  if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(16, std::min(64, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(8, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_CAM_GRID")) c->cg_mode = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_CAM_GRID_N")) c->cg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_SINGLE_CLASS"))
+    c->single_class = std::max(0, std::min(kSchedClasses, std::atoi(e)));
   auto bail = [&](int rc) {
     rt_destroy(c);
     return rc;
@@ -1774,6 +1960,7 @@ int rt_set_culling(rt_ctx *c, int enable) {
 int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
   if (!c || !s || s->num_spheres < 0 || s->num_lights < 0) return RT_ERR_INVALID_ARG;
   if ((s->num_spheres > 0 && !s->spheres) || (s->num_lights > 0 && !s->lights)) return RT_ERR_INVALID_ARG;
+  const auto t_upload = std::chrono::steady_clock::now();
   RT_TRY(c, hipSetDevice(c->device));
   RT_TRY(c, hipStreamSynchronize(c->stream));
   free_scene(c);
@@ -1933,6 +2120,7 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     c->scene_gen++;
     for (int q = 0; q < 3; q++) c->amb[q] = s->ambient[q];
     c->has_scene = true;
+    c->upload_ms = ms_since(t_upload);
   }
   delete[] hg;
   delete[] hr;
@@ -2056,7 +2244,8 @@ int rt_render_tile(rt_ctx *c, const rt_camera *cam, int W, int H, int depth, int
   if (!c->has_scene) return RT_ERR_NO_SCENE;
   if (depth > RT_MAX_DEPTH) return RT_ERR_DEPTH;
   // the reference kernel clips the tile to the image (kernel.cu:103)
-  const int xe = std::min(W, tile_x + tile_w), ye = std::min(H, tile_y + tile_h);
+  const int xe = (int)std::min<long long>(W, (long long)tile_x + tile_w);  // 64-bit: no overflow near INT_MAX
+  const int ye = (int)std::min<long long>(H, (long long)tile_y + tile_h);
   const int xw = std::max(0, xe - tile_x), th = std::max(0, ye - tile_y);
   // framebuffer rows j = tile_y .. ye-1 (j = 0 the bottom row) are PPM rows H-ye .. H-1-tile_y
   const Rows r{1, H - ye, 1, xw > 0 ? th : 0};
@@ -2096,6 +2285,20 @@ int rt_kernel_times(rt_ctx *c, double *ms_out, int max_n, int *n_out) {
   }
   *n_out = (int)avail;
   c->hist_begin = c->launches;
+  return RT_OK;
+}
+
+int rt_get_info(rt_ctx *c, rt_info *out) {
+  if (!c || !out) return RT_ERR_INVALID_ARG;
+  *out = rt_info{};
+  out->cam_grid_last = c->cg_last ? 1 : 0;
+  out->cam_grid_n = c->cg_last_n;
+  out->cam_grid_builds = c->cg_builds;
+  out->cam_grid_build_ms = c->cg_build_ms;
+  out->tile_order_builds = c->perm_builds;
+  out->tile_order_build_ms = c->perm_build_ms;
+  out->upload_ms = c->upload_ms;
+  out->launches = (uint64_t)c->launches;
   return RT_OK;
 }
 

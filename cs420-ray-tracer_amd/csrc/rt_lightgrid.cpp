@@ -2,6 +2,7 @@
 #include "rt_lightgrid.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -259,6 +260,11 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
   constexpr int kThreads = 8;
   std::vector<Rec> recs[kThreads];
   bool over[kThreads] = {};
+  // records of all workers together: a worker stops (and the build is
+  // refused) as soon as the total passes max_entries, so the host memory held
+  // is bounded by max_entries records plus one disk per worker, not
+  // kThreads * max_entries
+  std::atomic<size_t> total_recs{(size_t)cells * global.size()};
   auto build_slice = [&](int w) {
     std::vector<Rec> &out = recs[w];
     const size_t pairs = disks.size() / 2, lo = pairs * w / kThreads, hi = pairs * (w + 1) / kThreads;
@@ -266,8 +272,9 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
       const Disk &k = disks[di];
       const Dir &v = k.v;
       const double ca = k.ca, sa = k.sa, alpha = k.alpha;
+      const size_t before = out.size();
       G.for_cells(v, ca, sa, alpha, [&](size_t c) { out.push_back(Rec{(int32_t)c, k.tlo, k.s}); });
-      if (out.size() > max_entries) {
+      if (total_recs.fetch_add(out.size() - before, std::memory_order_relaxed) + (out.size() - before) > max_entries) {
         over[w] = true;
         return;
       }

@@ -12,7 +12,7 @@ namespace rtk {
 
 namespace {
 
-constexpr int kClasses = 4;  // 0 .. 3 reflective spheres over a tile (capped)
+constexpr int kClasses = kSchedClasses;
 
 // Image position of point (qx,qy,qz) for the reference camera: the ray
 // P + t (f + r su + u sv) through it has su = (w.r)/(w.f), sv = (w.u)/(w.f)
@@ -32,7 +32,8 @@ bool project(const SchedView &v, double qx, double qy, double qz, double &x, dou
 
 }  // namespace
 
-void tile_order(const SchedView &v, const std::vector<SchedSphere> &refl, std::vector<int> &perm) {
+void tile_order(const SchedView &v, const std::vector<SchedSphere> &refl, std::vector<int> &perm,
+                long long *class_count) {
   const int ntx = (v.xw + v.tw - 1) / v.tw, nty = (v.count + v.th - 1) / v.th;
   const long long ntiles = (long long)ntx * nty;
   perm.resize((size_t)ntiles);
@@ -115,6 +116,8 @@ void tile_order(const SchedView &v, const std::vector<SchedSphere> &refl, std::v
 #endif
   long long start[kClasses + 1] = {};
   for (long long t = 0; t < ntiles; ++t) ++start[kClasses - 1 - cls[(size_t)t] + 1];
+  if (class_count)
+    for (int k = 0; k < kClasses; ++k) class_count[k] = start[kClasses - k];
   for (int k = 0; k < kClasses; ++k) start[k + 1] += start[k];
   for (const int t : order) perm[(size_t)start[kClasses - 1 - cls[(size_t)t]]++] = t;
 }

@@ -30,6 +30,10 @@ struct SchedView {
 
 // perm[b] = tile index (ty * ntx + tx) dispatched b-th; ntx = ceil(xw / tw),
 // nty = ceil(count / th).  `refl` holds the reflective spheres only.
-void tile_order(const SchedView &v, const std::vector<SchedSphere> &refl, std::vector<int> &perm);
+// class_count (optional, kSchedClasses entries): tiles per class; perm lists
+// class kSchedClasses-1 first, then the lower classes in turn.
+constexpr int kSchedClasses = 4;  // 0 .. 3 reflective spheres over a tile (capped)
+void tile_order(const SchedView &v, const std::vector<SchedSphere> &refl, std::vector<int> &perm,
+                long long *class_count = nullptr);
 
 }  // namespace rtk

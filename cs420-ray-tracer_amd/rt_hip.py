@@ -22,7 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(HERE, "librt_hip.so")
 
 RT_MAX_DEPTH = 64
-ABI_VERSION = 6  # RT_HIP_ABI_VERSION in include/rt_hip.h
+ABI_VERSION = 7  # RT_HIP_ABI_VERSION in include/rt_hip.h
 MAX_FRAMES = 32  # RT_MAX_FRAMES
 
 
@@ -52,6 +52,15 @@ class rt_scene(C.Structure):
 class rt_camera(C.Structure):
     _fields_ = [("position", C.c_double * 3), ("forward", C.c_double * 3), ("right", C.c_double * 3),
                 ("up", C.c_double * 3), ("scale", C.c_double)]
+
+
+class rt_info(C.Structure):
+    _fields_ = [("cam_grid_last", C.c_int32), ("cam_grid_n", C.c_int32), ("cam_grid_builds", C.c_uint64),
+                ("cam_grid_build_ms", C.c_double), ("tile_order_builds", C.c_uint64),
+                ("tile_order_build_ms", C.c_double), ("upload_ms", C.c_double), ("launches", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class rt_tile(C.Structure):
@@ -108,6 +117,7 @@ SIGNATURES = {
     "rt_render_tiles": (C.c_int, [_P, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int, C.POINTER(rt_tile), C.c_int,
                                   C.c_int, _P]),
     "rt_set_antialias": (C.c_int, [_P, C.c_int]),
+    "rt_get_info": (C.c_int, [_P, C.POINTER(rt_info)]),
 }
 
 # include/rt_hip_compat.h: the reference's hybrid interface (src/kernel.cu:185-207),
@@ -329,6 +339,12 @@ class Renderer:
         st = rt_stats()
         _check(lib().rt_render_stats(self._ctx, C.byref(st)), "rt_render_stats", self._ctx)
         return st
+
+    def info(self) -> rt_info:
+        """rt_get_info: the host-side builds the render calls made (camera grid, tile order)."""
+        inf = rt_info()
+        _check(lib().rt_get_info(self._ctx, C.byref(inf)), "rt_get_info", self._ctx)
+        return inf
 
     def kernel_times(self, max_n: int = 256) -> list[float]:
         """Per-launch kernel durations (ms) since the previous call (syncs the stream)."""

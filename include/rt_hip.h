@@ -25,6 +25,8 @@
  *                                      y = tile_y + ..., fb[y*W + x], kernel.cu:99-112), as main_hybrid.cpp:457-470
  *                                      calls it; float3 / Vec3 / RGB8 framebuffers
  *   rt_set_antialias                <- the `-a` flag of ray_gpu, src/main_gpu.cu:249-333, 363-370
+ *   rt_get_info                     <- (new) the host-side builds the render calls made (camera grid,
+ *                                      tile launch order) and their cost
  *   launch_gpu_kernel, upload_lights_and_ambience (include/rt_hip_compat.h)
  *                                   <- the same symbols of src/kernel.cu:185-207, link-compatible
  *
@@ -50,8 +52,8 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 6  /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
-                                   6: rt_render_tiles */
+#define RT_HIP_ABI_VERSION 7  /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
+                                   6: rt_render_tiles; 7: rt_get_info */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -177,9 +179,17 @@ int rt_upload_scene(rt_ctx *ctx, const rt_scene *scene);
  * stats may be NULL. */
 int rt_render(rt_ctx *ctx, const rt_camera *cam, int width, int height, int depth, const rt_rows *rows,
               uint8_t *rgb_out, int out_on_device, rt_stats *stats);
-/* Asynchronous render into DEVICE memory on the context's stream; nothing is
- * synchronised.  rt_render_stats() waits for the stream and returns the stats
- * of the most recent rt_render_async. */
+/* Asynchronous render into DEVICE memory on the context's stream.  The kernels
+ * are only enqueued, but two host-side builds can happen inside the call and
+ * then wait for the context's stream first (work in flight may still read the
+ * buffer being replaced):
+ *   - the tile launch order (rt_sched), rebuilt when the view, the image or
+ *     shard geometry or the scene changed since the previous launch (~1 ms);
+ *   - the camera grid (closest hits of camera rays), built per camera position
+ *     for a launch of >= 8 frames sharing one position or a position repeated
+ *     from the previous launch (50-180 ms; a moving camera never builds one).
+ * rt_get_info() reports both.  rt_render_stats() waits for the stream and
+ * returns the stats of the most recent rt_render_async. */
 int rt_render_async(rt_ctx *ctx, const rt_camera *cam, int width, int height, int depth, const rt_rows *rows,
                     uint8_t *rgb_out_device);
 int rt_render_stats(rt_ctx *ctx, rt_stats *stats);
@@ -246,6 +256,19 @@ int rt_render_tiles(rt_ctx *ctx, const rt_camera *cam, int image_width, int imag
  * v = y/(H-1); the 4 colours summed in that order and scaled by 1/4, all in
  * the serial fp64 semantics).  Ray counts include every sample. */
 int rt_set_antialias(rt_ctx *ctx, int samples);
+
+/* Host-side work of the render calls since rt_create (see rt_render_async). */
+typedef struct rt_info {
+    int32_t cam_grid_last;       /* 1: the most recent launch traced its camera rays on a camera grid */
+    int32_t cam_grid_n;          /* its cells per cube-map face edge (0: none) */
+    uint64_t cam_grid_builds;    /* camera grids built */
+    double cam_grid_build_ms;    /* host wall time of those builds (incl. the stream wait and the upload) */
+    uint64_t tile_order_builds;  /* tile launch orders built */
+    double tile_order_build_ms;  /* host wall time of those builds */
+    double upload_ms;            /* host wall time of the most recent rt_upload_scene (BVH, light grids, copies) */
+    uint64_t launches;           /* render launches enqueued */
+} rt_info;
+int rt_get_info(rt_ctx *ctx, rt_info *out);
 
 /* Reassemble G shards gathered rank-major ([G][rows_per_rank][W][3], rank r
  * rendered with rt_rows{band, r, G, rows_per_rank}) into a PPM-ordered

@@ -1,5 +1,6 @@
 """Randomised parity sweep (a design/validation tool, not a test): random
-scenes -- 1 to 1,500 spheres (so both the cull sweeps and the always-BVH
+scenes -- whole or fractional shininess (40 % of scenes: int_pow and dd_pow),
+1 to 1,500 spheres (so both the cull sweeps and the always-BVH
 paths, render_deferred and render_deferred_walk), tiny to huge radii, mirror
 clouds, 0 to 6 lights, cameras inside spheres -- rendered on cuda:0 through
 the C-ABI at small sizes and random depths, against the oracle byte for byte
@@ -22,13 +23,20 @@ def scene(rng):
     n = rng.choice([1, 2, 5, 30, 200, 700, 1100, 1500])
     spread = rng.choice([0.5, 5.0, 20.0, 1000.0])
     mirror = rng.random() < 0.3
+    frac = rng.random() < 0.4  # fractional shininess: dd_pow (rt_pow.h) instead of int_pow
+
+    def shin():
+        if frac and rng.random() < 0.8:
+            return "%.4f" % rng.choice([0.5, 7.5, 33.3, 1500.25, rng.uniform(0.01, 2000.0)])
+        return "%d" % rng.choice([0, 1, 5, 20, 100, 200])
+
     lines = []
     for _ in range(n):
         r = rng.choice([1e-3, 0.05, 0.3, 1.0, 4.0]) * rng.uniform(0.5, 1.5) * spread / 10
         refl = rng.choice([0.8, 0.9, 1.0]) if mirror else rng.choice([0.0, 0.0, 0.3, 0.7, 1.0])
         lines.append("sphere %.9g %.9g %.9g %.9g %.3f %.3f %.3f %.2f 0.5 %d" % (
             rng.uniform(-spread, spread), rng.uniform(-spread, spread), rng.uniform(-3 * spread, spread), r,
-            rng.random(), rng.random(), rng.random(), refl, rng.choice([0, 1, 5, 20, 100, 200])))
+            rng.random(), rng.random(), rng.random(), refl, shin()))
     for _ in range(rng.randint(0, 6)):
         lines.append("light %.6g %.6g %.6g %.3f %.3f %.3f 1" % (
             rng.uniform(-2 * spread, 2 * spread), rng.uniform(-spread, 3 * spread), rng.uniform(-3 * spread, spread),

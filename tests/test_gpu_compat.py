@@ -137,3 +137,66 @@ def test_hybrid_interface_errors_never_exit():
     assert L.rt_compat_status() == 0
     s.synchronize()
     assert (fb == 7.0).all()
+
+
+def _hip_runtime():
+    """The HIP runtime torch loaded (the one librt_hip.so is bound to), for raw
+    hipStreamCreate / hipStreamDestroy calls."""
+    with open("/proc/self/maps") as f:
+        paths = {line.split()[-1] for line in f if "libamdhip64" in line}
+    assert paths, "no HIP runtime loaded"
+    hip = C.CDLL(sorted(paths)[0])
+    hip.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [C.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [C.c_void_p]
+    return hip
+
+
+def test_hybrid_interface_streams_destroyed_between_calls():
+    """render_hybrid creates three streams per call and destroys them at its end
+    (main_hybrid.cpp:407-409, 489-491; COMPARE_MODES calls it twice, :817): the
+    per-device default context must not keep a destroyed stream.  Two rounds of
+    launch_gpu_kernel over the tiles on raw HIP streams, destroyed after each
+    round, the second with moved spheres (the re-upload waits for the context's
+    stream): both framebuffers bit-identical to rt_render_tile's."""
+    import rt_hip
+    import torch
+
+    hip = _hip_runtime()
+    L = rt_hip.lib()
+    for rnd, shift in enumerate((0.0, 0.5)):
+        text = SCENE.replace("sphere 0 0 -5 1 ", "sphere %g 0 -5 1 " % shift)
+        sc = rt_hip.Scene.parse(text)
+        n, nl = sc.num_spheres, sc.num_lights
+        d_sph, d_cam, lights = _gpu_scene(rt_hip, torch, sc)
+        L.upload_lights_and_ambience(lights, nl, rt_hip.rt_float3(0.125, 0.125, 0.125))
+        assert L.rt_compat_status() == 0
+        fb = torch.full((H * W * 3,), float("nan"), dtype=torch.float32, device="cuda:0")
+        torch.cuda.synchronize()
+        raw = [C.c_void_p() for _ in range(3)]
+        for s in raw:
+            assert hip.hipStreamCreate(C.byref(s)) == 0
+        k = 0
+        for ty in range(0, H, TILE):
+            for tx in range(0, W, TILE):
+                L.launch_gpu_kernel(C.cast(fb.data_ptr(), C.POINTER(rt_hip.rt_float3)),
+                                    C.cast(d_sph.data_ptr(), C.POINTER(rt_hip.rt_gpu_sphere)), n, nl,
+                                    C.cast(d_cam.data_ptr(), C.POINTER(rt_hip.rt_gpu_camera)), tx, ty, TILE, TILE,
+                                    W, H, D, raw[k % 3])
+                k += 1
+                assert L.rt_compat_status() == 0, (rnd, rt_hip.status_string(L.rt_compat_status()))
+        for s in raw:
+            assert hip.hipStreamSynchronize(s) == 0
+            assert hip.hipStreamDestroy(s) == 0
+        r = rt_hip.Renderer(0)
+        try:
+            r.upload(sc)
+            f2 = torch.full((H * W * 3,), float("nan"), dtype=torch.float32, device="cuda:0")
+            torch.cuda.synchronize()
+            for ty in range(0, H, TILE):
+                for tx in range(0, W, TILE):
+                    r.render_tile(sc.camera(), W, H, D, tx, ty, TILE, TILE, rt_hip.RT_FB_F32X3, f2.data_ptr())
+            r.stats()
+            assert torch.equal(fb, f2), rnd
+        finally:
+            r.close()
