@@ -99,7 +99,8 @@ struct RenderArgs {
   int dq_cap;                     // entries per shard segment; 0 = no deferral
   int merge_q;                    // kStackMerge: LDS ray-queue entries per wave (16..64)
   int nsingle;                    // kStackMerge: the first nsingle tile slots (heaviest class) get a wave each
-  int pix_off;                    // kStackMerge: LDS offset of the wave's finished pixels (flush_tiles)
+  int pix_off;                    // kStackMerge: LDS offset of the wave's finished pixels (flush_tile)
+  int rows_dword;                 // kStackMerge: every 8-pixel tile row starts dword aligned (flush_tile)
   int defer_level;                // kStackMerge: rays of this reflection level and deeper are deferred
 };
 // the whole struct is the kernel's argument block (kernarg segment, at most 4 KiB)
@@ -504,7 +505,9 @@ constexpr int kDeferLevel = RT_DEFER_LEVEL;
 #define RT_DEFER_CAP_DIV 8  // deferred-queue room: 1 / RT_DEFER_CAP_DIV of the launch's pixels
 #endif
 constexpr int kDeferSlot = 7;
-constexpr size_t kPixbufBytes = (size_t)kMergeTiles * 64 * 3;  // merge_tiles' finished pixels, RGB8 (LDS)
+// merge_tiles' LDS: the finished pixels (RGB8, 192 B per tile), then the tile ids
+constexpr size_t kPixbufIds = (size_t)kMergeTiles * 64 * 3;
+constexpr size_t kPixbufBytes = kPixbufIds + (size_t)kMergeTiles * 8;  // + (tile id, row-0 offset) per tile
 // u64 slot of a counter shard: the deferred kernels' next queue entry of that
 // shard segment (lanes take entries dynamically; zeroed with the launch's counters)
 constexpr int kFetchSlot = 24;
@@ -522,25 +525,9 @@ __device__ __forceinline__ unsigned pack_px(D3 c, unsigned &c_neg) {
 // pixel's tile as dword rows with zero bytes in this pixel's place, and the
 // neighbours in those dwords may be other deferred pixels being OR-ed at the
 // same time: a dword atomic OR per covered dword, no byte stores.
-#ifndef RT_SINGLE
-#define RT_SINGLE 1
-#endif
-#ifndef RT_DEFER_PX_ATOMIC
-#define RT_DEFER_PX_ATOMIC 1
-#endif
-#ifndef RT_PX_STAGE
-#define RT_PX_STAGE 1
-#endif
 __device__ __forceinline__ void or_px(uint8_t *out, unsigned pix, unsigned v) {
 #if RT_ABL == 11  // ablation (wrong images): no pixel stores
   if (v != 0x5a5a5a5au) return;
-#endif
-#if !RT_DEFER_PX_ATOMIC
-  uint8_t *px = out + (size_t)pix * 3;
-  px[0] = (uint8_t)v;
-  px[1] = (uint8_t)(v >> 8);
-  px[2] = (uint8_t)(v >> 16);
-  return;
 #endif
   const uintptr_t a = reinterpret_cast<uintptr_t>(out) + (uintptr_t)pix * 3;
   unsigned *d = reinterpret_cast<unsigned *>(a & ~(uintptr_t)3);
@@ -580,47 +567,48 @@ __device__ __forceinline__ void put_px(uint8_t *p, unsigned v) {
 
 // The finished pixels of a merge_tiles group wait in LDS as RGB8 bytes laid
 // out like the tiles' rows (tile slot t, row y, pixel x at t * 192 + y * 24 +
-// x * 3) until the group is done, then go out as the tiles' 24-byte rows, one
-// dword per lane (flush_tiles); a deferred pixel's bytes stay 0 for
-// render_deferred's or_px.
+// x * 3) until every pixel of their tile is final, then go out as the tile's
+// 24-byte rows, one dword per lane (flush_tile); a deferred pixel's bytes stay
+// 0 for render_deferred's or_px.
 typedef __attribute__((address_space(3))) unsigned char LdsU8;
 typedef __attribute__((address_space(3))) unsigned LdsU32;
-__device__ __forceinline__ void flush_tiles(const RenderArgs &a, int base, int nt, int frame, const LdsU8 *pixbuf) {
+__device__ __forceinline__ void flush_tile(const RenderArgs &a, int tile, int frame, const LdsU8 *pb) {
   const int lane = (int)(threadIdx.x & 63);
   const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
   const Rows &rows = kernarg_late<true, offsetof(RenderArgs, rows)>(a.rows);
   const int W = kernarg_late<true, offsetof(RenderArgs, W)>(a.W);
   const int ntx = kernarg_late<true, offsetof(RenderArgs, ntx)>(a.ntx);
-  const int *perm = kernarg_late<true, offsetof(RenderArgs, perm)>(a.perm);
+  const int rows_dword = kernarg_late<true, offsetof(RenderArgs, rows_dword)>(a.rows_dword);
   uint8_t *out = static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride;
-  for (int t = 0; t < nt; ++t) {
-    const int tile = perm ? perm[base + t] : base + t;
-    const int x0 = (tile % ntx) * 8, ty = tile / ntx;
-    const LdsU8 *pb = pixbuf + t * 192;
-    // a row of 8 pixels is 24 bytes = 6 dwords when it is whole and dword aligned
-    auto row_at = [&](int r) { return out + ((size_t)(ty * 8 + r) * W + x0) * 3; };
-    auto whole = [&](int r) {
-      return ty * 8 + r < rows.count && x0 + 8 <= W && (reinterpret_cast<uintptr_t>(row_at(r)) & 3) == 0;
-    };
-    {
-      const int r = lane / 6, c = lane - 6 * (lane / 6);  // lanes 0..47: row r, dword c = LDS dword lane
-      if (lane < 48 && whole(r)) {
-        const unsigned v = reinterpret_cast<const LdsU32 *>(pb)[lane];
+  const int x0 = (tile % ntx) * 8, ty = tile / ntx;
+  // a row of 8 pixels is 24 bytes = 6 dwords when it is whole and dword aligned
+  auto row_at = [&](int r) { return out + ((size_t)(ty * 8 + r) * W + x0) * 3; };
+  if (rows_dword && x0 + 8 <= W && ty * 8 + 8 <= rows.count) {  // wave-uniform: the usual case
+    if (lane < 48) {  // lane: row lane / 6, dword lane % 6 = LDS dword lane
+      const unsigned v = reinterpret_cast<const LdsU32 *>(pb)[lane];
 #if RT_ABL == 11  // ablation (wrong images): no pixel stores
-        if (v == 0x5a5a5a5au)
+      if (v == 0x5a5a5a5au)
 #endif
-        reinterpret_cast<unsigned *>(row_at(r))[c] = v;
-      }
+      *reinterpret_cast<unsigned *>(row_at(0) + (unsigned)(lane / 6) * (unsigned)W * 3u +
+                                    4u * (unsigned)(lane - 6 * (lane / 6))) = v;
     }
-    {
-      // rows that are not whole (the image's right edge, odd widths): the
-      // lane's own pixel into the dwords it shares with its neighbours (which
-      // other waves may be writing): its bytes cleared and set by dword atomics
-      const int r = lane >> 3, x = x0 + (lane & 7);
-      if (!whole(r) && ty * 8 + r < rows.count && x < W) {
-        const LdsU8 *p = pb + lane * 3;
-        put_px(row_at(r) + (lane & 7) * 3, (unsigned)p[0] | (unsigned)p[1] << 8 | (unsigned)p[2] << 16);
-      }
+    return;
+  }
+  auto whole = [&](int r) {
+    return ty * 8 + r < rows.count && x0 + 8 <= W && (reinterpret_cast<uintptr_t>(row_at(r)) & 3) == 0;
+  };
+  {
+    const int r = lane / 6, c = lane - 6 * (lane / 6);  // lanes 0..47: row r, dword c = LDS dword lane
+    if (lane < 48 && whole(r)) reinterpret_cast<unsigned *>(row_at(r))[c] = reinterpret_cast<const LdsU32 *>(pb)[lane];
+  }
+  {
+    // rows that are not whole (the image's right edge, odd widths): the
+    // lane's own pixel into the dwords it shares with its neighbours (which
+    // other waves may be writing): its bytes cleared and set by dword atomics
+    const int r = lane >> 3, x = x0 + (lane & 7);
+    if (!whole(r) && ty * 8 + r < rows.count && x < W) {
+      const LdsU8 *p = pb + lane * 3;
+      put_px(row_at(r) + (lane & 7) * 3, (unsigned)p[0] | (unsigned)p[1] << 8 | (unsigned)p[2] << 16);
     }
   }
 }
@@ -633,10 +621,10 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
   const int lane = (int)(threadIdx.x & 63);
   const unsigned long long lt = (1ull << lane) - 1ull;
   unsigned c_prim = 0, c_shadow = 0, c_reflect = 0, c_neg = 0;
-  // the finished pixels (flush_tiles), at an LDS offset the host placed after the walk stacks
+  // the finished pixels (flush_tile), at an LDS offset the host placed after the walk stacks
   auto pixbuf = [&]() { return (LdsU8 *)rt_dyn_lds + kernarg_late<true, offsetof(RenderArgs, pix_off)>(a.pix_off); };
 #pragma unroll
-  for (int i = 0; i < (int)(kPixbufBytes / 256) && RT_PX_STAGE; ++i)  // padding, depth 0 and deferred pixels: 0
+  for (int i = 0; i < (int)(kPixbufBytes / 256); ++i)  // padding, depth 0 and deferred pixels: 0
     reinterpret_cast<LdsU32 *>(pixbuf())[i * 64 + lane] = 0u;
   const int depth = a.depth;
   const unsigned sstride = (unsigned)ca.npx;
@@ -647,7 +635,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
   D3 o = mk(0.0, 0.0, 0.0), d = o;
   int key = -1, dleft = 0, lev = 0;
   unsigned pix = 0;
-  int lpos = 0;  // the pixel's place in pixbuf
+  int lidx = 0;  // the pixel's place in the group: tile slot * 64 + y * 8 + x (pixbuf byte 3 * lidx)
   // pops queued rays into the lanes without one (lanes ranked by lane id)
   auto refill = [&](unsigned long long busy) {
     const int take = (64 - __popcll(busy)) < qn ? (64 - __popcll(busy)) : qn;
@@ -659,7 +647,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
       key = e.key;
       dleft = e.dleft;
       pix = (unsigned)e.pix;
-      lpos = e.orig;
+      lidx = e.orig;
       lev = 1;
       act = true;
     }
@@ -670,7 +658,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     // groups (the heaviest tiles: their own reflection rays fill the wave, and
     // a frame's critical path is its slowest wave), kMergeTiles after them
     const int ntiles = kernarg_late<true, offsetof(RenderArgs, ntiles)>(a.ntiles);
-    const int ns = RT_SINGLE ? kernarg_late<true, offsetof(RenderArgs, nsingle)>(a.nsingle) : 0;
+    const int ns = kernarg_late<true, offsetof(RenderArgs, nsingle)>(a.nsingle);
     const int base = group < ns ? group : ns + (group - ns) * kMergeTiles;
     const int nt = group < ns ? 1 : (ntiles - base < kMergeTiles ? ntiles - base : kMergeTiles);
     bool tile_pass = false;
@@ -704,7 +692,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
 #endif
         o = mk(cam.px, cam.py, cam.pz);
         pix = (unsigned)(k * W + x);
-        lpos = next * 192 + (lane >> 3) * 24 + (lane & 7) * 3;
+        lidx = next * 64 + lane;
         key = -1;
         dleft = depth;
         lev = 0;
@@ -712,6 +700,17 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         c_prim += act ? 1u : 0u;
         // depth <= 0 -> black (main.cpp:17-18), padding rows -> zeros: pixbuf's 0
         (void)od;
+        // for the flush at the group's end: the tile id and, when the tile is
+        // whole and its rows dword aligned, the byte offset of its first row in
+        // the frame (else ~0: flush_tile's general path)
+        if (lane == 0) {
+          const size_t off = ((size_t)ty * 8 * W + (size_t)tx * 8) * 3;
+          const bool whole = kernarg_late<true, offsetof(RenderArgs, rows_dword)>(a.rows_dword) && tx * 8 + 8 <= W &&
+                             ty * 8 + 8 <= rows.count && off < 0xFFFFFFFFull;
+          LdsU32 *ids = reinterpret_cast<LdsU32 *>(pixbuf() + kPixbufIds);
+          ids[2 * next] = (unsigned)tile;
+          ids[2 * next + 1] = whole ? (unsigned)off : 0xFFFFFFFFu;
+        }
         ++next;
         tile_pass = true;
         if (__ballot(act) == 0) continue;
@@ -753,24 +752,13 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
           const StackEnt e = ca.gstack[sidx + (unsigned)lev * sstride];
           res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
         }
-#if RT_PX_STAGE
         {
           const unsigned v = pack_px(res, c_neg);
-          LdsU8 *p = pixbuf() + lpos;
+          LdsU8 *p = pixbuf() + 3 * lidx;
           p[0] = (unsigned char)v;
           p[1] = (unsigned char)(v >> 8);
           p[2] = (unsigned char)(v >> 16);
         }
-#else
-        {
-          const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
-          const unsigned v = pack_px(res, c_neg);
-          uint8_t *px = static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride + (size_t)pix * 3;
-          px[0] = (uint8_t)v;
-          px[1] = (uint8_t)(v >> 8);
-          px[2] = (uint8_t)(v >> 16);
-        }
-#endif
         act = false;
       }
     }
@@ -799,20 +787,37 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     if (tile_pass && next < nt && __popcll(busy) + qn < Q) {
       // this tile's reflection rays wait for the next tiles' (queue < Q entries)
       if (act)
-        q[qn + (int)__popcll(busy & lt)] = QRay{o.x, o.y, o.z, d.x, d.y, d.z, lpos, dleft, key, (int)pix};
+        q[qn + (int)__popcll(busy & lt)] = QRay{o.x, o.y, o.z, d.x, d.y, d.z, lidx, dleft, key, (int)pix};
       qn += __popcll(busy);
       act = false;
     } else if (qn > 0 && busy != ~0ull) {
       refill(busy);  // lanes without a ray take queued ones
     }
   }
+  // every pixel of the group is final (or deferred, 0 bytes): its tiles go
+  // out, a whole aligned tile as 48 dword stores at its recorded offset
   {
-    const int ntiles = kernarg_late<true, offsetof(RenderArgs, ntiles)>(a.ntiles);
-    const int ns = RT_SINGLE ? kernarg_late<true, offsetof(RenderArgs, nsingle)>(a.nsingle) : 0;
-    const int base = group < ns ? group : ns + (group - ns) * kMergeTiles;
-    if (RT_PX_STAGE)
-      flush_tiles(a, base, group < ns ? 1 : (ntiles - base < kMergeTiles ? ntiles - base : kMergeTiles), frame,
-                  pixbuf());
+    const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
+    const int W = kernarg_late<true, offsetof(RenderArgs, W)>(a.W);
+    uint8_t *out = static_cast<uint8_t *>(od.ptr) + (size_t)frame * (size_t)od.fstride;
+    const unsigned roff = (unsigned)(lane / 6) * (unsigned)W * 3u + 4u * (unsigned)(lane - 6 * (lane / 6));
+    const LdsU32 *ids = reinterpret_cast<const LdsU32 *>(pixbuf() + kPixbufIds);
+#pragma unroll
+    for (int t = 0; t < kMergeTiles; ++t) {
+      if (t >= next) break;
+      const unsigned off = __builtin_amdgcn_readfirstlane(ids[2 * t + 1]);
+      if (off != 0xFFFFFFFFu) {
+        if (lane < 48) {
+          const unsigned v = reinterpret_cast<const LdsU32 *>(pixbuf() + 192 * t)[lane];
+#if RT_ABL == 11  // ablation (wrong images): no pixel stores
+          if (v == 0x5a5a5a5au)
+#endif
+          *reinterpret_cast<unsigned *>(out + off + roff) = v;
+        }
+      } else {
+        flush_tile(a, (int)__builtin_amdgcn_readfirstlane(ids[2 * t]), frame, pixbuf() + 192 * t);
+      }
+    }
   }
   sums[0] += wave_sum(c_prim);
   sums[1] += wave_sum(c_shadow);
@@ -944,7 +949,6 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
   const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
   if constexpr (kStack == kStackMerge && !kLdsGeo && kSamples == 1) {
-    // the wave's ray queue sits where trace_wave parks colours (launch_tiles)
     // the wave's ray queue sits where trace_wave parks colours, after the
     // finished-pixel bytes (launch_tiles)
     QRay *q = reinterpret_cast<QRay *>(reinterpret_cast<unsigned char *>(ca.park) + kPixbufBytes);
@@ -1698,6 +1702,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   // merge_tiles' pixel bytes: after the scene and the walk stacks, where render_kernel's park/queue region starts
   ra.pix_off = (int)(((lds_layout(kLds, c->nsph, c->nlight, bv.nnodes).end + 31) & ~(size_t)31) +
                      (bv.ordered ? (size_t)kWg * bv.odepth * 64 * sizeof(int2) : 0));
+  // row k of frame f starts at ptr + f fstride + 3 (k W + x): dword aligned for every k, f and x = 8i
+  ra.rows_dword = ((reinterpret_cast<uintptr_t>(od.ptr) | (uintptr_t)(3 * (size_t)W) | (uintptr_t)od.fstride) & 3) == 0;
   ra.defer_level = c->defer_level;
   if (kStack == kStackMerge && c->defer && depth > c->defer_level) {
     // room for 1/8 of the launch's pixels (deferred rays are ~2 % on synth200); a ray

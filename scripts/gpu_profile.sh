@@ -14,14 +14,19 @@ cd /tmp
 timeout -k 10 300 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail -5 "$OUT/bench.err"; exit 1; }
 echo "bench: $(head -c 300 "$OUT/bench.json")"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 "$ROOT/bench.py" --no-cpu-baseline --no-also > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err" || { echo "trace failed"; tail -5 "$OUT/trace_bench.err"; exit 1; }
+  python3 "$ROOT/bench.py" --no-cpu-baseline --no-also --no-extras > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err" || { echo "trace failed"; tail -5 "$OUT/trace_bench.err"; exit 1; }
 echo "trace ok"
+# PMC passes: one-wave heavy tiles off (RT_HIP_SINGLE_CLASS=4), so the
+# bench's one-frame stats launch has the per-frame grid of its multi-frame
+# launches (make_pmc_json.py counts frames by grid size); it changes nothing
+# in multi-frame launches
+export RT_HIP_SINGLE_CLASS=4
 for w in $WORKLOADS; do
   i=0; mkdir -p "$OUT/pmc_$w"
   while IFS= read -r counters; do
     [ -z "$counters" ] && continue
     timeout -s KILL 120 rocprofv3 --pmc $counters --output-format csv -d "$OUT/pmc_$w/p$i" -o run -- \
-      python3 "$ROOT/bench.py" --no-cpu-baseline --no-also --workload "$w" --steps 32 --warmup 16 \
+      python3 "$ROOT/bench.py" --no-cpu-baseline --no-also --no-extras --workload "$w" --steps 32 --warmup 16 \
       > "$OUT/pmc_$w/p$i.log" 2>&1 || { echo "pmc $w pass $i failed"; tail -5 "$OUT/pmc_$w/p$i.log"; exit 1; }
     i=$((i+1))
   done < "$ROOT/scripts/pmc_r2_passes.txt"
