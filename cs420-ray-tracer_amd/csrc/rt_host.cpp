@@ -196,13 +196,18 @@ int rt_write_ppm(const char *path, const uint8_t *rgb, int width, int height, in
   if (binary) {
     if (std::fwrite(rgb, 1, n * 3, f) != n * 3) rc = RT_ERR_IO;
   } else {
-    static char tab[256][4];
-    static unsigned char len[256];
-    static bool init = false;
-    if (!init) {
-      for (int v = 0; v < 256; v++) len[v] = (unsigned char)std::snprintf(tab[v], 4, "%d", v);
-      init = true;
-    }
+    // "0".."255" and their lengths, built once (a function-local static: safe
+    // when several threads write images at the same time)
+    struct Tab {
+      char s[256][4];
+      unsigned char n[256];
+      Tab() {
+        for (int v = 0; v < 256; v++) n[v] = (unsigned char)std::snprintf(s[v], 4, "%d", v);
+      }
+    };
+    static const Tab T;
+    const auto &tab = T.s;
+    const auto &len = T.n;
     const size_t chunk_px = 1 << 16;
     std::vector<char> buf(chunk_px * 12);
     for (size_t p0 = 0; p0 < n && rc == RT_OK; p0 += chunk_px) {

@@ -1302,7 +1302,13 @@ struct rt_ctx {
   size_t tmp_bytes = 0;
   int samples = 1;  // 4: the antialias mode (rt_set_antialias)
   int stack_mode = 4;  // RT_HIP_STACK: 4 merged reflection levels (default), 1 per-pixel global stack (one tile per wave)
-  bool defer = true;          // RT_HIP_DEFER: kStackMerge defers rays of level >= kDeferLevel to render_deferred
+  // RT_HIP_DEFER: kStackMerge defers rays of level >= kDeferLevel to render_deferred
+  // (-1, default: in multi-frame launches only; 0 never; 1 always).  A one-frame
+  // launch ends on its slowest chains either way, and the second kernel's own
+  // ramp and tail come after them (synth200 single frame 0.455 -> 0.384 ms
+  // without it, profiles/r3n/ab_knobs.log; 32-frame launches are 13 % slower
+  // per frame without it)
+  int defer = -1;
   bool defer_walk = true;     // RT_HIP_DEFER_WALK: deferred rays of a scene whose closest hits always walk the BVH use render_deferred_walk
   int merge_q = 64;           // kStackMerge: the launch's LDS queue entries per wave (launch_render4 picks it)
   int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (8, 16, 32 or 64)
@@ -1336,12 +1342,13 @@ struct rt_ctx {
   size_t perm_cap = 0;
   long long perm_cls[kSchedClasses] = {};  // tiles per class of the cached order
   // kStackMerge: tiles of this class and above get a wave each (RT_HIP_SINGLE_CLASS
-  // for every launch; kSchedClasses = none).  Default: class >= 1 in one-frame
-  // launches, whose end is their slowest wave (synth200 0.534 -> 0.451 ms,
-  // complex 0.451 -> 0.388), none in multi-frame launches, where the other
-  // frames fill that tail and four tiles per wave share their reflection
-  // rays' passes (class >= 1 there: 0.2285 -> 0.2364 ms per frame;
-  // profiles/r3c/ab_single.log)
+  // for every launch; kSchedClasses = none).  Default: every tile (class >= 0)
+  // in one-frame launches, whose end is their slowest wave -- with no deferred
+  // kernel after them (defer, below): synth200 0.780 -> 0.372 ms, complex
+  // 0.652 -> 0.332 ms (profiles/r3r/ab_knobs.log); none in multi-frame
+  // launches, where the other frames fill that tail and four tiles per wave
+  // share their reflection rays' passes (class >= 1 there: 0.2285 -> 0.2364 ms
+  // per frame, profiles/r3c/ab_single.log)
   int single_class = -1;
   // rt_get_info: host-side builds made by the render calls
   bool cg_last = false;
@@ -1659,7 +1666,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     int rc = tile_perm(c, cam, W, H, rows, od, 8 * kWx, 8 * kWy, ntiles, perm);
     if (rc != RT_OK) return rc;
     if (kStack == kStackMerge) {  // the heaviest classes lead the order: one wave per tile for them
-      const int sc = c->single_class >= 0 ? c->single_class : (nf == 1 ? 1 : kSchedClasses);
+      const int sc = c->single_class >= 0 ? c->single_class : (nf == 1 ? 0 : kSchedClasses);
       long long heavy = 0;
       for (int k = sc; k < kSchedClasses; k++) heavy += c->perm_cls[k];
       nsingle = (int)std::min<long long>(heavy, ntiles);
@@ -1705,7 +1712,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   // row k of frame f starts at ptr + f fstride + 3 (k W + x): dword aligned for every k, f and x = 8i
   ra.rows_dword = ((reinterpret_cast<uintptr_t>(od.ptr) | (uintptr_t)(3 * (size_t)W) | (uintptr_t)od.fstride) & 3) == 0;
   ra.defer_level = c->defer_level;
-  if (kStack == kStackMerge && c->defer && depth > c->defer_level) {
+  if (kStack == kStackMerge && (c->defer > 0 || (c->defer < 0 && nf > 1)) && depth > c->defer_level) {
     // room for 1/8 of the launch's pixels (deferred rays are ~2 % on synth200); a ray
     // that finds its shard segment full simply continues in its merge_tiles lane
     const size_t npx = (size_t)rows.count * od.xw * nf;
@@ -1874,7 +1881,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH_ORDERED")) c->bvh_ordered = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH4")) c->bvh_wide = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
-  if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0 ? 1 : 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_WALK")) c->defer_walk = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_LEVEL")) c->defer_level = std::max(1, std::min(RT_MAX_DEPTH, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(8, std::min(64, std::atoi(e)));

@@ -320,19 +320,25 @@ def test_fractional_shininess_scenes_vs_oracle(gpu_renderer, seed):
 
 
 @pytest.mark.parametrize("n", [400, 1300], ids=["render_deferred", "render_deferred_walk"])
-def test_fractional_shininess_mirror_cloud_vs_oracle(gpu_renderer, n):
+def test_fractional_shininess_mirror_cloud_vs_oracle(monkeypatch, n):
     """A camera inside a cloud of mirrors with fractional shininess: every
-    reflection level (merged megakernel, render_deferred / render_deferred_walk)
-    shades with dd_pow.  +-1 per channel, identical ray counts."""
+    reflection level (merged megakernel, render_deferred / render_deferred_walk:
+    RT_HIP_DEFER=1 defers in this one-frame render too) shades with dd_pow.
+    +-1 per channel, identical ray counts."""
     import orc
     import rt_hip
 
     W, H, D = 192, 144, 6
     text = _mirror_cloud(11, n, frac=True)
     sc = rt_hip.Scene.parse(text)
-    gpu_renderer.upload(sc)
+    monkeypatch.setenv("RT_HIP_DEFER", "1")
+    r = rt_hip.Renderer(0)
+    r.upload(sc)
     ref, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=8)
-    rgb, st = gpu_renderer.render(sc.camera(), W, H, D)
+    try:
+        rgb, st = r.render(sc.camera(), W, H, D)
+    finally:
+        r.close()
     nd = _pm1(bytes(rgb), ref)
     print(f"fractional shininess mirror cloud n={n}: {nd} of {len(ref)} channels differ")
     assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
@@ -411,17 +417,24 @@ def test_bvh_far_from_origin(bvh_renderer):
 
 @pytest.fixture(params=[{"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_SCHED": "0"}, {"RT_HIP_STACK": "1"},
                         {"RT_HIP_STACK": "1", "RT_HIP_SCHED": "0"}, {"RT_HIP_STACK": "4", "RT_HIP_LDS_SCENE": "1"},
-                        {"RT_HIP_MERGE_Q": "16"}, {"RT_HIP_DEFER": "0"}, {"RT_HIP_DEFER_LEVEL": "1"},
-                        {"RT_HIP_DEFER_LEVEL": "3"}, {"RT_HIP_DEFER_WALK": "0"}],
+                        {"RT_HIP_MERGE_Q": "16"}, {"RT_HIP_DEFER": "0"}, {"RT_HIP_DEFER": "1"},
+                        {"RT_HIP_DEFER": "1", "RT_HIP_DEFER_LEVEL": "1"},
+                        {"RT_HIP_DEFER": "1", "RT_HIP_DEFER_LEVEL": "3"},
+                        {"RT_HIP_DEFER": "1", "RT_HIP_DEFER_WALK": "0"}, {"RT_HIP_MERGE_Q": "8"},
+                        {"RT_HIP_SINGLE_CLASS": "0"}, {"RT_HIP_SINGLE_CLASS": "4"}],
                 ids=["lds-scene", "scanline-order", "global-stack", "global-stack-scanline", "merge-lds-scene",
-                     "merge-queue-16", "no-defer", "defer-level-1", "defer-level-3", "defer-walk-off"])
+                     "merge-queue-16", "no-defer", "defer-one-frame", "defer-level-1", "defer-level-3",
+                     "defer-walk-off", "merge-queue-8", "one-tile-waves-all", "one-tile-waves-none"])
 def stack_renderer(request, monkeypatch):
     """Non-default kernel layouts (RT_HIP_STACK=1: one tile per wave with the
     per-pixel global stack instead of merged levels; RT_HIP_LDS_SCENE=1:
     scenes that fit staged in LDS with 4-wave workgroups; RT_HIP_SCHED=0: tiles
     launched in scanline order instead of heaviest-predicted first;
     RT_HIP_MERGE_Q / RT_HIP_DEFER / RT_HIP_DEFER_LEVEL: merge-queue size and
-    the deferred-ray kernel; RT_HIP_DEFER_WALK=0: large scenes' deferred rays
+    the deferred-ray kernel (these single-frame renders defer only with
+    RT_HIP_DEFER=1: by default one-frame launches keep every level in the
+    megakernel); RT_HIP_SINGLE_CLASS: which tiles get a wave each in one-frame
+    launches; RT_HIP_DEFER_WALK=0: large scenes' deferred rays
     through render_deferred instead of render_deferred_walk)."""
     import rt_hip
 
@@ -463,9 +476,11 @@ def test_stack_modes_depth_edges(stack_renderer, depth):
             assert np.array_equal(got[k], want[y])
 
 
-@pytest.mark.parametrize("walk", [{}, {"RT_HIP_BVH4": "0"}, {"RT_HIP_BVH_ORDERED": "0"},
-                                  {"RT_HIP_DEFER_WALK": "0"}, {"RT_HIP_DEFER_LEVEL": "1"}],
-                         ids=["ordered4", "ordered2", "stackless", "defer-walk-off", "defer-walk-level-1"])
+@pytest.mark.parametrize("walk", [{}, {"RT_HIP_DEFER": "1"}, {"RT_HIP_BVH4": "0"}, {"RT_HIP_BVH_ORDERED": "0"},
+                                  {"RT_HIP_DEFER_WALK": "0", "RT_HIP_DEFER": "1"},
+                                  {"RT_HIP_DEFER_LEVEL": "1", "RT_HIP_DEFER": "1"}],
+                         ids=["ordered4", "ordered4-defer", "ordered2", "stackless", "defer-walk-off",
+                              "defer-walk-level-1"])
 @pytest.mark.parametrize("seed,count", [(101, 700), (102, 1100), (103, 1600)])
 def test_large_scenes_global_memory_paths(monkeypatch, walk, seed, count):
     """Scenes read through L2 with the BVH fallback: the ordered 4-wide walk
@@ -520,7 +535,8 @@ def test_deferred_queue_overflow_vs_oracle(n):
     the merged megakernel. Checked: the level-2 ray count exceeds the room; the
     image and ray counts equal a render without deferral (RT_HIP_DEFER=0); every
     31st row equals the oracle's.  n = 1300 takes the walk kernel
-    (render_deferred_walk), n = 400 render_deferred."""
+    (render_deferred_walk), n = 400 render_deferred.  These one-frame renders
+    defer with RT_HIP_DEFER=1 (one-frame launches do not by default)."""
     import os
 
     import orc
@@ -529,7 +545,15 @@ def test_deferred_queue_overflow_vs_oracle(n):
     W, H, D = 512, 384, 6
     text = _mirror_cloud(7, n)
     sc = rt_hip.Scene.parse(text)
-    r = rt_hip.Renderer(0)
+    old1 = os.environ.get("RT_HIP_DEFER")
+    os.environ["RT_HIP_DEFER"] = "1"
+    try:
+        r = rt_hip.Renderer(0)
+    finally:
+        if old1 is None:
+            del os.environ["RT_HIP_DEFER"]
+        else:
+            os.environ["RT_HIP_DEFER"] = old1
     try:
         r.upload(sc)
         _, st2 = r.render(sc.camera(), W, H, 2)
