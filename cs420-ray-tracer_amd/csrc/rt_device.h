@@ -1341,8 +1341,12 @@ struct CgArgs {
   int N;
   int on;  // the launch's frames all share the grid's camera position
 };
-__device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d,
-                                           const CgArgs &cg, double &best_t, Work &work) {
+// The scan of one grid's cell list for the closest hit; this lane's grid
+// starts at start + sbase (camera grid: sbase = 0; sphere grids: the grid of
+// the sphere the ray leaves).
+__device__ __forceinline__ int grid_closest(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d,
+                                            const int32_t *__restrict__ start, const int2 *__restrict__ ent, int N,
+                                            int sbase, double &best_t, Work &work) {
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
   double bt = kInf, bn = __builtin_inf();
@@ -1351,27 +1355,51 @@ __device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, 
   int cb = 0, len = 0;
   bool all = false;
   if (act) {
-    const int c = lg_cell_rcp((float)d.x, (float)d.y, (float)d.z, cg.N);
+    const int c = lg_cell_rcp((float)d.x, (float)d.y, (float)d.z, N);
     if (c < 0) {
       all = true;
       len = n;
     } else {
-      cb = cg.start[c];
-      len = cg.start[c + 1] - cb;
+      cb = start[sbase + c];
+      len = start[sbase + c + 1] - cb;
     }
   }
   int k = 0;
-  int2 e = (len > 0 && !all) ? cg.ent[cb] : make_int2(0, (int)0xff800000u);  // -inf
+  int2 e = (len > 0 && !all) ? ent[cb] : make_int2(0, (int)0xff800000u);  // -inf
   while (k < len) {
     const int i = all ? k : e.x;
     if ((double)__int_as_float(e.y) > bt) break;
     ++k;
-    if (k < len && !all) e = cg.ent[cb + k];  // the next entry, loaded during this test
+    if (k < len && !all) e = ent[cb + k];  // the next entry, loaded during this test
     work.exact += 1;
     closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi);
   }
   best_t = bt;
   return bi;
+}
+__device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d,
+                                           const CgArgs &cg, double &best_t, Work &work) {
+  return grid_closest(g, n, act, o, d, cg.start, cg.ent, cg.N, 0, best_t, work);
+}
+
+// Closest hit of reflection rays through the sphere grids (rt_lightgrid.h
+// build_sphere_grids): a ray leaving sphere `key` whose origin lies in the
+// ball the grid of `key` was built for (|o - C|^2 <= rho2[key]: checked here
+// per ray; rho2 < 0 where there is no grid) scans that grid's cell of d as the
+// camera rays scan theirs -- the candidate set holds every sphere the
+// reference's test can report for such a ray, with a lower bound of its t.
+struct SgArgs {
+  const int32_t *start;  // [n][6N^2 + 1]
+  const int2 *ent;       // (sphere, tlo bits)
+  const double *rho2;    // [n] squared origin-ball radius, < 0: no grid
+  int N;
+  int on;
+};
+__device__ __forceinline__ bool sg_usable(const SphGeo *__restrict__ g, const SgArgs &sg, bool act, D3 o, int key) {
+  if (!act || key < 0) return false;
+  const SphGeo s = g[key];
+  const double ox = o.x - s.cx, oy = o.y - s.cy, oz = o.z - s.cz;
+  return (ox * ox + oy * oy) + oz * oz <= sg.rho2[key];
 }
 
 struct Cam {

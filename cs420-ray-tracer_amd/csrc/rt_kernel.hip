@@ -87,6 +87,7 @@ struct RenderArgs {
   BvhArgs bv;
   LgArgs lg;
   CgArgs cg;  // camera grid of the launch's (shared) camera position; cg.on = 0: none
+  SgArgs sg;  // sphere grids (reflection rays); sg.on = 0: none
   OutDesc od;
   StackEnt *gstack;
   unsigned long long *counters;
@@ -293,11 +294,43 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
     if (cam_pass) {
       bi = cam_closest(g, n, alive, o, d, kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{}), bt, work);
       swept = true;
+    } else if (kernarg_late<true, offsetof(RenderArgs, sg)>(SgArgs{}).on) {
+      // reflection rays through the sphere grid of the sphere they leave; the
+      // lanes whose origin fails the grid's check sweep as before
+      bool grid;
+      {
+        const SgArgs &sg = kernarg_late<true, offsetof(RenderArgs, sg)>(SgArgs{});
+        grid = sg_usable(g, sg, alive, o, key);
+      }
+      if (__ballot(grid)) {
+        const SgArgs &sg = kernarg_late<true, offsetof(RenderArgs, sg)>(SgArgs{});
+        bi = grid_closest(g, n, grid, o, d, sg.start, sg.ent, sg.N, grid ? key * (6 * sg.N * sg.N + 1) : 0, bt,
+                          work);
+      }
+      const bool rest = alive && !grid;
+      if (__ballot(rest)) {
+        double bt2 = kInf;
+        const int bi2 = sweep_closest<kCull, kFast>(g, rad, n, rest, o, d, key,
+                                                    kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt2, work);
+        if (rest) {
+          bi = bi2;
+          bt = bt2;
+        }
+      }
+      swept = true;
     }
   }
   if (!swept)
     bi = sweep_closest<kCull, kFast>(g, rad, n, alive, o, d, key, kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv),
                                      bt, work);
+#if RT_ABL == 20  // ablation (diagnostic builds only): the reflection rays' closest-hit search done twice
+  if (!swept) {
+    double bt2 = kInf;
+    const int bi2 = sweep_closest<kCull, kFast>(g, rad, n, alive, o, d, key,
+                                                kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt2, work);
+    asm volatile("" ::"v"(bi2), "v"(bt2));
+  }
+#endif
   RT_ACC(work, 8, t_cl);
   shade_hit<kCull, kArgMem, kFast>(g, rad, mat, slight, n, nl, amb, bv, lg_arg, alive, o, d, key, dleft, bi, bt, work,
                                    c_shadow, outcome, color, refl, no, nd, nkey);
@@ -1270,6 +1303,18 @@ struct rt_ctx {
   double last_pos[3] = {0, 0, 0};      // the previous launch's camera position
   bool have_last = false;
   std::vector<double> h_sx, h_sy, h_sz, h_sr;  // sphere centres and radii (grid builds)
+  // sphere grids (rt_lightgrid.h build_sphere_grids): the closest hit of
+  // reflection rays in the kFast kernels, built at upload for the reflective
+  // spheres
+  int sg_mode = -1;  // RT_HIP_SPHERE_GRID: -1 auto (scenes of up to kSgMaxSpheres spheres), 0 off, 1 on
+  int sg_n_opt = 0;  // RT_HIP_SPHERE_GRID_N; 0 = kSgN
+  int32_t *d_sg_start = nullptr;
+  int2 *d_sg_ent = nullptr;
+  double *d_sg_rho2 = nullptr;
+  int sg_n = 0, sg_grids = 0;
+  bool sg_ok = false;
+  size_t sg_entries = 0;
+  double sg_build_ms = 0.0;
   double c0[3] = {0, 0, 0};
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
   double rmax = 0;
@@ -1395,6 +1440,15 @@ void free_scene(rt_ctx *c) {
   c->d_lg_start = c->d_lg_ids = nullptr;
   c->cg_ok = false;
   c->cg_gen = ~0ull;
+  if (c->d_sg_start) (void)hipFree(c->d_sg_start);
+  if (c->d_sg_ent) (void)hipFree(c->d_sg_ent);
+  if (c->d_sg_rho2) (void)hipFree(c->d_sg_rho2);
+  c->d_sg_start = nullptr;
+  c->d_sg_ent = nullptr;
+  c->d_sg_rho2 = nullptr;
+  c->sg_ok = false;
+  c->sg_grids = 0;
+  c->sg_entries = 0;
   c->d_bvh = nullptr;
   c->d_prims = nullptr;
   c->bvh_nodes = 0;
@@ -1517,6 +1571,56 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
     c->cg_build_ms += ms_since(t0);
   }
   if (c->cg_ok) out = CgArgs{c->d_cg_start, c->d_cg_ent, c->cg_n, 1};
+  return RT_OK;
+}
+
+constexpr int kSgN = 16;               // sphere grid cells per cube-map face edge
+constexpr int kSgMaxSpheres = 2048;     // RT_HIP_SPHERE_GRID=-1: larger scenes keep the BVH walks
+constexpr int kSgMaxGlobal = 32;        // spheres overlapping an origin ball (on every list of its grid)
+constexpr size_t kSgMaxEntries = size_t(64) << 20;
+
+// Sphere grids for the reflective spheres of the scene being uploaded (the
+// origins of reflection rays, main.cpp:46, lie within |r| + 0.001 of their
+// sphere's centre up to the rounding of the hit point; the ball is grown by a
+// relative 1e-6 and the device checks every ray against it).  No grids (and
+// RT_OK) when disabled, too large, or refused.
+int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
+  const int n = s->num_spheres;
+  if (c->sg_mode == 0 || (c->sg_mode < 0 && n > kSgMaxSpheres) || n == 0 || !std::isfinite(diam)) return RT_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<double> rho((size_t)n, -1.0);
+  for (int i = 0; i < n; i++) {
+    const rt_sphere &sp = s->spheres[i];
+    const double r = std::fabs(sp.radius);
+    const double mag = std::fabs(sp.center[0]) + std::fabs(sp.center[1]) + std::fabs(sp.center[2]);
+    if (sp.reflectivity > 0.0 && std::isfinite(r) && std::isfinite(mag))  // main.cpp:43
+      rho[(size_t)i] = (r + kEps) * (1.0 + 1e-6) + 1e-12 * mag + 1e-9 * diam;
+  }
+  const int N = c->sg_n_opt ? c->sg_n_opt : kSgN;
+  std::vector<int32_t> start, ent;
+  std::vector<uint8_t> ok;
+  const size_t entries = build_sphere_grids(c->h_sx.data(), c->h_sy.data(), c->h_sz.data(), c->h_sr.data(), n,
+                                            rho.data(), diam, N, kSgMaxGlobal, kSgMaxEntries, start, ent, ok);
+  std::vector<double> rho2((size_t)n);
+  int grids = 0;
+  for (int i = 0; i < n; i++) {
+    rho2[(size_t)i] = ok[(size_t)i] ? rho[(size_t)i] * rho[(size_t)i] : -1.0;
+    grids += ok[(size_t)i] ? 1 : 0;
+  }
+  if (grids > 0) {
+    RT_TRY(c, hipMalloc(&c->d_sg_start, sizeof(int32_t) * start.size()));
+    RT_TRY(c, hipMalloc(&c->d_sg_ent, sizeof(int32_t) * ent.size() + sizeof(int2)));
+    RT_TRY(c, hipMalloc(&c->d_sg_rho2, sizeof(double) * (size_t)n));
+    RT_TRY(c, hipMemcpy(c->d_sg_start, start.data(), sizeof(int32_t) * start.size(), hipMemcpyHostToDevice));
+    if (!ent.empty())
+      RT_TRY(c, hipMemcpy(c->d_sg_ent, ent.data(), sizeof(int32_t) * ent.size(), hipMemcpyHostToDevice));
+    RT_TRY(c, hipMemcpy(c->d_sg_rho2, rho2.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
+    c->sg_n = N;
+    c->sg_ok = true;
+  }
+  c->sg_grids = grids;
+  c->sg_entries = entries;
+  c->sg_build_ms = ms_since(t0);
   return RT_OK;
 }
 
@@ -1739,6 +1843,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       const int rc = cam_grid(c, cam, nf, ra.cg);
       if (rc != RT_OK) return rc;
     }
+    if (fast && kCull && c->sg_ok) ra.sg = SgArgs{c->d_sg_start, c->d_sg_ent, c->d_sg_rho2, c->sg_n, 1};
     c->cg_last = ra.cg.on != 0;
     c->cg_last_n = ra.cg.on ? ra.cg.N : 0;
     RT_TRY(c, mark_start(c));  // the launch's timing starts after the host-side builds
@@ -1888,6 +1993,8 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_CAM_GRID")) c->cg_mode = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_CAM_GRID_N")) c->cg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_SPHERE_GRID")) c->sg_mode = std::max(-1, std::min(1, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_SPHERE_GRID_N")) c->sg_n_opt = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SINGLE_CLASS"))
     c->single_class = std::max(0, std::min(kSchedClasses, std::atoi(e)));
   auto bail = [&](int rc) {
@@ -2105,6 +2212,14 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
       delete[] hl;
       return rc;
     }
+    if ((rc = sphere_grids(c, s, diam)) != RT_OK) {
+      free_scene(c);
+      delete[] hg;
+      delete[] hr;
+      delete[] hm;
+      delete[] hl;
+      return rc;
+    }
   }
   for (int k = 0; k < 3; k++) {
     c->c0[k] = c0[k];
@@ -2312,6 +2427,10 @@ int rt_get_info(rt_ctx *c, rt_info *out) {
   out->tile_order_build_ms = c->perm_build_ms;
   out->upload_ms = c->upload_ms;
   out->launches = (uint64_t)c->launches;
+  out->sphere_grids = c->sg_ok ? c->sg_grids : 0;
+  out->sphere_grid_n = c->sg_ok ? c->sg_n : 0;
+  out->sphere_grid_entries = c->sg_ok ? (uint64_t)c->sg_entries : 0;
+  out->sphere_grid_build_ms = c->sg_build_ms;
   return RT_OK;
 }
 

@@ -204,15 +204,23 @@ void build_light_grid(const double *cx, const double *cy, const double *cz, cons
   }
 }
 
-bool build_point_grid(const double *cx, const double *cy, const double *cz, const double *r, int n, double px,
-                      double py, double pz, double diam, int N, int max_global, size_t max_entries,
-                      std::vector<int32_t> &start, std::vector<int32_t> &ent) {
+namespace {
+
+// build_point_grid for origins anywhere in the ball B(P, rho) (rho = 0: the
+// point itself), its disk-binning spread over `nthreads` workers;
+// `total_recs` (shared by concurrent builds) counts the records of all of
+// them against max_entries.
+bool point_grid(const CubeGrid &G, const double *cx, const double *cy, const double *cz, const double *r, int n,
+                double px, double py, double pz, double rho, double diam, int max_global, size_t max_entries,
+                int nthreads, std::atomic<size_t> &total_recs, std::vector<int32_t> &start,
+                std::vector<int32_t> &ent) {
   start.clear();
   ent.clear();
-  if (N < 1 || N > 4096 || !std::isfinite(px) || !std::isfinite(py) || !std::isfinite(pz) || !std::isfinite(diam))
+  const int N = G.N;
+  if (!std::isfinite(px) || !std::isfinite(py) || !std::isfinite(pz) || !std::isfinite(diam) || !std::isfinite(rho) ||
+      !(rho >= 0.0))
     return false;
   const int cells = 6 * N * N;
-  const CubeGrid G(N);
   // records (cell, tlo, sphere)
   struct Rec {
     int32_t cell;
@@ -237,8 +245,11 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
   for (int s = 0; s < n; s++) {
     const double vx = cx[s] - px, vy = cy[s] - py, vz = cz[s] - pz;
     const double D = std::sqrt(vx * vx + vy * vy + vz * vz);
-    // the light grid's radius: >= |r| + the rounding of the reference's test
-    const double R = std::fabs(r[s]) * (1.0 + 1e-6) + 1e-6 * (D + diam);
+    // the light grid's radius: >= |r| + the rounding of the reference's test,
+    // grown by rho: a ray from any origin p in B(P, rho) that meets the
+    // sphere has its direction in the disk of B(C - P, R) (the Minkowski sum)
+    // and every root at least D - R from p
+    const double R = std::fabs(r[s]) * (1.0 + 1e-6) + 1e-6 * (D + diam) + rho;
     if (!std::isfinite(D) || !std::isfinite(R) || !(D > R)) {
       global.push_back(s);  // contains (or nearly) P, or non-finite: every direction, tlo = -inf
       if ((int)global.size() > max_global) return false;
@@ -257,14 +268,14 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
   // kThreads workers over slices of the spheres, records per worker.  A
   // sphere whose two disks (very wide ones) both meet a cell is listed there
   // twice: the second test of it changes nothing (same t, same index)
-  constexpr int kThreads = 8;
-  std::vector<Rec> recs[kThreads];
-  bool over[kThreads] = {};
+  const int kThreads = nthreads;
+  std::vector<std::vector<Rec>> recs((size_t)kThreads);
+  std::unique_ptr<bool[]> over(new bool[(size_t)kThreads]());
   // records of all workers together: a worker stops (and the build is
   // refused) as soon as the total passes max_entries, so the host memory held
   // is bounded by max_entries records plus one disk per worker, not
   // kThreads * max_entries
-  std::atomic<size_t> total_recs{(size_t)cells * global.size()};
+  if (total_recs.fetch_add((size_t)cells * global.size()) + (size_t)cells * global.size() > max_entries) return false;
   auto build_slice = [&](int w) {
     std::vector<Rec> &out = recs[w];
     const size_t pairs = disks.size() / 2, lo = pairs * w / kThreads, hi = pairs * (w + 1) / kThreads;
@@ -321,13 +332,89 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
       }
     }
   };
-  {
+  if (kThreads == 1) {  // one worker: no face threads either (concurrent builds run one per thread)
+    for (int f = 0; f < 6; f++) emit_face(f);
+  } else {
     std::vector<std::thread> th;
     for (int f = 1; f < 6; f++) th.emplace_back(emit_face, f);
     emit_face(0);
     for (auto &t : th) t.join();
   }
   return true;
+}
+
+}  // namespace
+
+bool build_point_grid(const double *cx, const double *cy, const double *cz, const double *r, int n, double px,
+                      double py, double pz, double diam, int N, int max_global, size_t max_entries,
+                      std::vector<int32_t> &start, std::vector<int32_t> &ent) {
+  start.clear();
+  ent.clear();
+  if (N < 1 || N > 4096) return false;
+  const CubeGrid G(N);
+  std::atomic<size_t> total{0};
+  return point_grid(G, cx, cy, cz, r, n, px, py, pz, 0.0, diam, max_global, max_entries, 8, total, start, ent);
+}
+
+size_t build_sphere_grids(const double *cx, const double *cy, const double *cz, const double *r, int n,
+                          const double *rho, double diam, int N, int max_global, size_t max_entries,
+                          std::vector<int32_t> &start, std::vector<int32_t> &ent, std::vector<uint8_t> &ok) {
+  start.clear();
+  ent.clear();
+  ok.assign((size_t)std::max(n, 0), 0);
+  if (N < 1 || N > 1024 || n <= 0) return 0;
+  const int cells = 6 * N * N;
+  const size_t stride = (size_t)cells + 1;
+  const CubeGrid G(N);
+  std::vector<std::vector<int32_t>> st((size_t)n), en((size_t)n);
+  std::atomic<size_t> total{0};
+  std::atomic<int> next{0};
+  std::atomic<bool> over{false};
+  // one sphere's grid per worker at a time (single-threaded builds)
+  auto worker = [&]() {
+    for (int s; (s = next.fetch_add(1)) < n && !over.load(std::memory_order_relaxed);) {
+      ok[(size_t)s] = point_grid(G, cx, cy, cz, r, n, cx[s], cy[s], cz[s], rho[s], diam, max_global, max_entries, 1,
+                                 total, st[(size_t)s], en[(size_t)s])
+                          ? 1
+                          : 0;
+      if (total.load(std::memory_order_relaxed) > max_entries) over = true;
+    }
+  };
+  {
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int nw = (int)std::max(1u, std::min(8u, hw ? hw : 1u));
+    std::vector<std::thread> th;
+    for (int w = 1; w < nw; w++) th.emplace_back(worker);
+    worker();
+    for (auto &t : th) t.join();
+  }
+  if (over) {
+    ok.assign((size_t)n, 0);
+    return 0;
+  }
+  size_t entries = 0;
+  for (int s = 0; s < n; s++)
+    if (ok[(size_t)s]) entries += en[(size_t)s].size() / 2;
+  if (entries > (size_t)INT32_MAX) {
+    ok.assign((size_t)n, 0);
+    return 0;
+  }
+  start.assign(stride * (size_t)n, 0);
+  ent.resize(2 * entries);
+  size_t base = 0;
+  for (int s = 0; s < n; s++) {
+    int32_t *so = start.data() + stride * (size_t)s;
+    if (!ok[(size_t)s]) {  // refused (too many spheres overlap its origin ball): empty lists, never used
+      for (size_t c = 0; c < stride; c++) so[c] = (int32_t)base;
+      continue;
+    }
+    for (size_t c = 0; c < stride; c++) so[c] = (int32_t)(base + (size_t)st[(size_t)s][c]);
+    std::memcpy(ent.data() + 2 * base, en[(size_t)s].data(), en[(size_t)s].size() * sizeof(int32_t));
+    base += en[(size_t)s].size() / 2;
+    std::vector<int32_t>().swap(st[(size_t)s]);
+    std::vector<int32_t>().swap(en[(size_t)s]);
+  }
+  return entries;
 }
 
 }  // namespace rtk

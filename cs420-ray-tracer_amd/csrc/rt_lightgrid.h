@@ -83,4 +83,20 @@ bool build_point_grid(const double *cx, const double *cy, const double *cz, cons
                       double py, double pz, double diam, int N, int max_global, size_t max_entries,
                       std::vector<int32_t> &start, std::vector<int32_t> &ent);
 
+// Sphere grids: one such grid per sphere s, for the closest hit of rays that
+// leave s (reflection rays, main.cpp:46: origin hit point + normal * 0.001),
+// built for origins anywhere in the ball B(C_s, rho[s]): every disk grows by
+// rho (the directions from B(C_s, rho) to a sphere of radius R around C are
+// those of B(C - C_s, R + rho)) and every bound by rho (tlo = D - R - rho
+// ahead, -(D + R + rho) behind); s itself and the spheres within R + rho of
+// C_s are on every list.  The device uses grid s only for a ray whose origin
+// it has checked to lie in B(C_s, rho[s]).  Sphere s's cell c is
+// ent[2k], ent[2k + 1] for k in [start[s * (6N^2 + 1) + c], start[... + c + 1]);
+// ok[s] = 0 where that grid was refused (more than max_global spheres overlap
+// the ball; its lists are empty).  Returns the number of entries, 0 (and
+// every ok[s] = 0) when they would exceed max_entries.
+size_t build_sphere_grids(const double *cx, const double *cy, const double *cz, const double *r, int n,
+                          const double *rho, double diam, int N, int max_global, size_t max_entries,
+                          std::vector<int32_t> &start, std::vector<int32_t> &ent, std::vector<uint8_t> &ok);
+
 }  // namespace rtk

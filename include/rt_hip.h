@@ -52,8 +52,8 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 7  /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
-                                   6: rt_render_tiles; 7: rt_get_info */
+#define RT_HIP_ABI_VERSION 8  /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
+                                   6: rt_render_tiles; 7: rt_get_info; 8: rt_info sphere-grid fields */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -267,6 +267,10 @@ typedef struct rt_info {
     double tile_order_build_ms;  /* host wall time of those builds */
     double upload_ms;            /* host wall time of the most recent rt_upload_scene (BVH, light grids, copies) */
     uint64_t launches;           /* render launches enqueued */
+    int32_t sphere_grids;        /* spheres with a sphere grid (reflection rays' closest hit; 0: none) */
+    int32_t sphere_grid_n;       /* their cells per cube-map face edge */
+    uint64_t sphere_grid_entries;  /* list entries of all sphere grids (8 bytes each) */
+    double sphere_grid_build_ms; /* host wall time of their build, part of upload_ms */
 } rt_info;
 int rt_get_info(rt_ctx *ctx, rt_info *out);
 

@@ -208,3 +208,95 @@ def test_camera_grid_goldens(monkeypatch):
             assert bytes(rgb) == want, (name, diff_summary(bytes(rgb), want))
     finally:
         r.close()
+
+
+def test_sphere_grid_lists_and_scan(tmp_path):
+    """Sphere grids (rt_lightgrid.h build_sphere_grids, rt_device.h
+    grid_closest): for reflection rays built as the renderer builds them
+    (origin hit point + normal * 0.001, the reflected direction) and rays from
+    those origins aimed at silhouettes ahead and behind, whose origin passes
+    the device's ball check, every sphere the reference's test reports a hit
+    for (t of either sign) is on the looked-up cell's list of the grid of the
+    sphere the ray leaves with tlo <= t, and the early-exit scan returns
+    find_intersection's (t, index) -- random scenes at scales 0.1..1000, far
+    from the origin, negative and tiny radii, a ground sphere
+    (tests/native/sg_check.cpp)."""
+    exe = tmp_path / "sg_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-o", str(exe),
+                    os.path.join(REPO, "tests", "native", "sg_check.cpp"), os.path.join(CSRC, "rt_lightgrid.cpp"),
+                    "-lpthread"], check=True)
+    out = subprocess.run([str(exe), "40"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    w = out.stdout.split()
+    assert w[0] == "checked" and int(w[1]) > 100000 and int(w[2]) > 200000, out.stdout
+    # the origin check passes for every renderer-built ray; missed = wrong = 0
+    assert int(w[4]) <= int(w[1]) // 1000 and w[6] == "0" and w[8] == "0", out.stdout
+
+
+@pytest.fixture(params=["16", "4", "1", "off"], ids=lambda n: "spheregrid" + n)
+def spheregrid_renderer(request, monkeypatch):
+    import rt_hip
+
+    if request.param == "off":
+        monkeypatch.setenv("RT_HIP_SPHERE_GRID", "0")
+    else:
+        monkeypatch.setenv("RT_HIP_SPHERE_GRID", "1")
+        monkeypatch.setenv("RT_HIP_SPHERE_GRID_N", request.param)
+    r = rt_hip.Renderer(0)
+    yield r, request.param
+    r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CAM_SCENES))
+def test_sphere_grid_scenes_vs_oracle(spheregrid_renderer, name):
+    """Reflection rays through the sphere grids (single and 8-frame launches,
+    the latter with the deferred kernel) against the oracle."""
+    import orc
+    import rt_hip
+
+    import torch
+
+    r, mode = spheregrid_renderer
+    text = CAM_SCENES[name]
+    W, H, D = 96, 72, 6
+    sc = rt_hip.Scene.parse(text)
+    r.upload(sc)
+    info = r.info().as_dict()
+    assert (info["sphere_grids"] > 0) == (mode != "off"), info  # every scene here has mirrors
+    ref, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=4)
+    rgb, st = r.render(sc.camera(), W, H, D)
+    assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
+    assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
+                                                                   counts["reflect"])
+    buf = torch.zeros((8, H, W, 3), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    r.render_frames_async([sc.camera()] * 8, W, H, D, None, buf.data_ptr(), H * W * 3)
+    r.stats()  # waits for the launch
+    for f in range(8):
+        got = bytes(buf[f].cpu().numpy().tobytes())
+        assert got == ref, (f, diff_summary(got, ref))
+
+
+@pytest.mark.gpu
+def test_sphere_grid_goldens(monkeypatch):
+    """Every golden fixture with the sphere grids forced on, at two N, is
+    byte-identical (the default turns them on up to 2,048 spheres)."""
+    import rt_hip
+    from conftest import golden_rgb, manifest, scene_path
+
+    for n in ("16", "3"):
+        monkeypatch.setenv("RT_HIP_SPHERE_GRID", "1")
+        monkeypatch.setenv("RT_HIP_SPHERE_GRID_N", n)
+        r = rt_hip.Renderer(0)
+        try:
+            for name, m in sorted(manifest().items()):
+                sc = rt_hip.Scene.load(scene_path(m["scene"]))
+                r.upload(sc)
+                # above 2,048 spheres even a forced build gives up (the entry cap)
+                assert r.info().sphere_grids > 0 or sc.num_spheres > 2048, name
+                rgb, st = r.render(sc.camera(), m["width"], m["height"], m["depth"])
+                want = golden_rgb(name)
+                assert bytes(rgb) == want, (name, n, diff_summary(bytes(rgb), want))
+        finally:
+            r.close()
