@@ -360,6 +360,11 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
                    "build_ms_total": round(info_warm.cam_grid_build_ms, 2),
                    "tile_order_builds_in_timed_region": info_timed.tile_order_builds - info_warm.tile_order_builds,
                    "upload_ms": round(info_timed.upload_ms, 2)}
+    # sphere grids (reflection rays' closest hit), built by rt_upload_scene (in upload_ms)
+    sphere_grids = {"grids": getattr(info_timed, "sphere_grids", None),
+                    "cells_per_face_edge": getattr(info_timed, "sphere_grid_n", None),
+                    "entries": getattr(info_timed, "sphere_grid_entries", None),
+                    "build_ms": round(getattr(info_timed, "sphere_grid_build_ms", 0.0), 2)}
     extra = {}
     if extras and not dist_on:
         extra["single_frame"] = single_frame(rt_hip, r, cam, W, H, D, rows, shards[0][0].data_ptr())
@@ -386,7 +391,7 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
             "tests_cull": tests_cull, "cull": cull, "gather_ms_per_batch": gather_ms,
             "rank_kernel_ms_per_frame": rank_kernel_ms, "world_size_seen": seen_world,
             "warmup_frames_rendered": max(warmup, F), "launch_frames": rt_frames.batch_sizes(steps, F),
-            "camera_grid": camera_grid, **extra}
+            "camera_grid": camera_grid, "sphere_grids": sphere_grids, **extra}
 
 
 def main():
@@ -517,7 +522,7 @@ def main():
                        # view): the camera grid for that position is built once, in warmup (its cost below);
                        # single_frame / moving_camera are the rates without that assumption
                        "view": "static camera: every frame the scene file's view",
-                       "camera_grid": m["camera_grid"]},
+                       "camera_grid": m["camera_grid"], "sphere_grids": m["sphere_grids"]},
             # achieved = the fp64 FLOPs the render kernels EXECUTE per frame
             # (rocprofv3 PMC, 64 x (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions,
             # profiles/pmc_traffic.json taken with these kernel sources) over the
