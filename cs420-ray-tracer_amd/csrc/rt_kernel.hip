@@ -173,8 +173,9 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
     col = mul(amb, mk(m0.cr, m0.cg, m0.cb));                   // scene.h:91
   }
     // scene.h:94-120: per light in file order, the shadow query then (if lit)
-    // the Phong terms with the same ldir
-    {
+    // the Phong terms with the same ldir -- skipped by a wave (or the active
+    // lanes of one) whose rays all left the scene
+    if (__ballot(hit)) {
       const SphGeo sg = g[hi];
       const SphMat m = mat[hi];
       const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
@@ -222,8 +223,13 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
 #else
           const D3 so = add(hp, scale(ldir, kEps)), sd = renormalized(ldir);
 #endif
-          if constexpr (kFast)
+          if constexpr (kFast) {
             occ = shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi);
+#if RT_ABL == 21  // ablation (diagnostic builds only): every shadow query done twice
+            const bool occ2 = shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi);
+            asm volatile("" ::"v"(occ2));
+#endif
+          }
           else
             occ = lg.on ? shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi)
                         : sweep_shadow<kCull>(g, rad, n, need, so, sd, lp, hi, dist,
@@ -293,6 +299,13 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
   if constexpr (kFast && kArgMem) {
     if (cam_pass) {
       bi = cam_closest(g, n, alive, o, d, kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{}), bt, work);
+#if RT_ABL == 23  // ablation (diagnostic builds only): the camera rays' closest hit done twice
+      {
+        double bt2 = kInf;
+        const int bi2 = cam_closest(g, n, alive, o, d, kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{}), bt2, work);
+        asm volatile("" ::"v"(bi2), "v"(bt2));
+      }
+#endif
       swept = true;
     } else if (kernarg_late<true, offsetof(RenderArgs, sg)>(SgArgs{}).on) {
       // reflection rays through the sphere grid of the sphere they leave; the
@@ -306,6 +319,12 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
         const SgArgs &sg = kernarg_late<true, offsetof(RenderArgs, sg)>(SgArgs{});
         bi = grid_closest(g, n, grid, o, d, sg.start, sg.ent, sg.N, grid ? key * (6 * sg.N * sg.N + 1) : 0, bt,
                           work);
+#if RT_ABL == 20
+        double bt2 = kInf;
+        const int bi2 = grid_closest(g, n, grid, o, d, sg.start, sg.ent, sg.N, grid ? key * (6 * sg.N * sg.N + 1) : 0,
+                                     bt2, work);
+        asm volatile("" ::"v"(bi2), "v"(bt2));
+#endif
       }
       const bool rest = alive && !grid;
       if (__ballot(rest)) {
