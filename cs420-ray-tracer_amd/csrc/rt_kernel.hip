@@ -144,6 +144,7 @@ __device__ __forceinline__ const T &kernarg_late(const T &x) {
 // when no depth is left) or kSpawned (colour = shade*(1-refl), refl, and the
 // reflection ray no/nd leaving sphere nkey).  Wave-uniform control flow.
 enum { kEnded = 1, kSpawned = 2 };
+
 // kArgMem: bv and lg are the kernel's own arguments (kernarg segment), so they
 // are re-read where needed (kernarg_late) instead of held in SGPRs throughout.
 // kFast: only the default paths (ordered 4-wide BVH walk, light-grid shadow
@@ -284,12 +285,12 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
   }
 }
 
+// The closest hit of bounce() (scene.h:41-61) for the `alive` lanes: sphere
+// index (-1: none) and t.  Wave-uniform control flow.
 template <bool kCull, bool kArgMem = false, bool kFast = false>
-__device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const double *__restrict__ rad,
-                                       const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
-                                       int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o, D3 d,
-                                       int key, int dleft, Work &work, unsigned &c_shadow, int &outcome, D3 &color,
-                                       double &refl, D3 &no, D3 &nd, int &nkey, bool cam_pass = false) {
+__device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
+                                           const BvhArgs &bv, bool alive, D3 o, D3 d, int key, Work &work,
+                                           double &bt_out, bool cam_pass = false) {
   double bt = kInf;
   RT_T0(t_cl);
   int bi = -1;
@@ -351,6 +352,18 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
   }
 #endif
   RT_ACC(work, 8, t_cl);
+  bt_out = bt;
+  return bi;
+}
+
+template <bool kCull, bool kArgMem = false, bool kFast = false>
+__device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                       const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
+                                       int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o, D3 d,
+                                       int key, int dleft, Work &work, unsigned &c_shadow, int &outcome, D3 &color,
+                                       double &refl, D3 &no, D3 &nd, int &nkey, bool cam_pass = false) {
+  double bt;
+  const int bi = closest_hit<kCull, kArgMem, kFast>(g, rad, n, bv, alive, o, d, key, work, bt, cam_pass);
   shade_hit<kCull, kArgMem, kFast>(g, rad, mat, slight, n, nl, amb, bv, lg_arg, alive, o, d, key, dleft, bi, bt, work,
                                    c_shadow, outcome, color, refl, no, nd, nkey);
 }
@@ -775,9 +788,11 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     int outcome = 0, nkey = 0;
     D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
     double refl = 0.0;
-    bounce<kCull, true, kFast>(g, rad, mat, slight, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft, work,
-                               c_shadow, outcome, color, refl, no, nd, nkey,
-                               kFast && tile_pass && kernarg_late<true, offsetof(RenderArgs, cg)>(a.cg).on);
+    double bt;
+    const int bi = closest_hit<kCull, true, kFast>(g, rad, a.n, a.bv, act, o, d, key, work, bt,
+                                             kFast && tile_pass && kernarg_late<true, offsetof(RenderArgs, cg)>(a.cg).on);
+    shade_hit<kCull, true, kFast>(g, rad, mat, slight, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft, bi, bt,
+                                  work, c_shadow, outcome, color, refl, no, nd, nkey);
     const unsigned sidx = pix + ca.fpx;
     bool defer = false;
     if (act) {
