@@ -669,7 +669,11 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
         const float az = (nd->loz[k] - lz) * iz, bz = (nd->hiz[k] - hz) * iz;
         const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
         const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+#ifdef RT_EXPERIMENT_FWD  // diagnostic only (not exact): skip boxes wholly behind the origin
+        const bool h = tn <= tf && !(tn > tmf) && tf >= 0.0f;
+#else
         const bool h = tn <= tf && !(tn > tmf);  // NaN (unused slot) -> false
+#endif
         hits += h ? 1 : 0;
         // sort key: a hit sorts below every miss (fminf keeps it finite-or-below-inf)
         t[k] = h ? fminf(tn, 3.0e38f) : __builtin_inff();
@@ -769,7 +773,11 @@ __device__ __forceinline__ bool walk4_step(const BvhArgs &bv, const Walk4Ray &r,
       const float az = (nd->loz[k] - r.lz) * r.iz, bz = (nd->hiz[k] - r.hz) * r.iz;
       const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
       const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+#ifdef RT_EXPERIMENT_FWD
+      const bool h = tn <= tf && !(tn > tmf) && tf >= 0.0f;
+#else
       const bool h = tn <= tf && !(tn > tmf);
+#endif
       hits += h ? 1 : 0;
       t[k] = h ? fminf(tn, 3.0e38f) : __builtin_inff();
       c[k] = nd->c[k];

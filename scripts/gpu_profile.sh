@@ -21,6 +21,9 @@ echo "trace ok"
 # launches (make_pmc_json.py counts frames by grid size); it changes nothing
 # in multi-frame launches
 export RT_HIP_SINGLE_CLASS=4
+# and the deferred kernel in every launch (one-frame launches skip it by
+# default), so that stats launch also has the multi-frame launches' kernel split
+export RT_HIP_DEFER=1
 for w in $WORKLOADS; do
   i=0; mkdir -p "$OUT/pmc_$w"
   while IFS= read -r counters; do
