@@ -365,6 +365,12 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
                     "cells_per_face_edge": getattr(info_timed, "sphere_grid_n", None),
                     "entries": getattr(info_timed, "sphere_grid_entries", None),
                     "build_ms": round(getattr(info_timed, "sphere_grid_build_ms", 0.0), 2)}
+    # behind grid (the backward half of the BVH walks' closest-hit lines), built by rt_upload_scene
+    behind_grid = {"built": bool(getattr(info_timed, "behind_grid", 0)),
+                   "used_by_timed_launches": bool(getattr(info_timed, "behind_grid_last", 0)),
+                   "cells": getattr(info_timed, "behind_grid_cells", None),
+                   "entries": getattr(info_timed, "behind_grid_entries", None),
+                   "build_ms": round(getattr(info_timed, "behind_grid_build_ms", 0.0), 2)}
     extra = {}
     if extras and not dist_on:
         extra["single_frame"] = single_frame(rt_hip, r, cam, W, H, D, rows, shards[0][0].data_ptr())
@@ -391,7 +397,7 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
             "tests_cull": tests_cull, "cull": cull, "gather_ms_per_batch": gather_ms,
             "rank_kernel_ms_per_frame": rank_kernel_ms, "world_size_seen": seen_world,
             "warmup_frames_rendered": max(warmup, F), "launch_frames": rt_frames.batch_sizes(steps, F),
-            "camera_grid": camera_grid, "sphere_grids": sphere_grids, **extra}
+            "camera_grid": camera_grid, "sphere_grids": sphere_grids, "behind_grid": behind_grid, **extra}
 
 
 def main():
@@ -522,7 +528,8 @@ def main():
                        # view): the camera grid for that position is built once, in warmup (its cost below);
                        # single_frame / moving_camera are the rates without that assumption
                        "view": "static camera: every frame the scene file's view",
-                       "camera_grid": m["camera_grid"], "sphere_grids": m["sphere_grids"]},
+                       "camera_grid": m["camera_grid"], "sphere_grids": m["sphere_grids"],
+                       "behind_grid": m["behind_grid"]},
             # achieved = the fp64 FLOPs the render kernels EXECUTE per frame
             # (rocprofv3 PMC, 64 x (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions,
             # profiles/pmc_traffic.json taken with these kernel sources) over the

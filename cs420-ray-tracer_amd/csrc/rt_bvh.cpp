@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstddef>
+#include <cstring>
 
 namespace rtk {
 namespace {
@@ -244,6 +246,150 @@ int32_t build_bvh4(const std::vector<BvhNode> &nodes, std::vector<BvhNode4> &out
   }
   stack = need[0];
   return 0;
+}
+
+bool build_ugrid(const double *cx, const double *cy, const double *cz, const double *r, int n, size_t max_entries,
+                 UgridHost &out, double cells_per_sphere) {
+  out = UgridHost{};
+  if (n <= 0) return false;
+  double clo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, chi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+  for (int i = 0; i < n; i++) {
+    const double c[3] = {cx[i], cy[i], cz[i]};
+    if (!std::isfinite(c[0]) || !std::isfinite(c[1]) || !std::isfinite(c[2]) || !std::isfinite(r[i])) return false;
+    for (int k = 0; k < 3; k++) {
+      clo[k] = std::min(clo[k], c[k]);
+      chi[k] = std::max(chi[k], c[k]);
+    }
+  }
+  // first cell size from the centres' box (two cells per sphere); spheres
+  // wider than two such cells are global
+  const double cps = std::isfinite(cells_per_sphere) && cells_per_sphere > 1e-3 ? cells_per_sphere : 2.0;
+  auto cell_for = [cps](const double *lo, const double *hi, int m) {
+    double vol = 1.0, emax = 0.0;
+    for (int k = 0; k < 3; k++) emax = std::max(emax, hi[k] - lo[k]);
+    const double floor_e = std::max(emax * 1e-3, 1e-9);
+    for (int k = 0; k < 3; k++) vol *= std::max(hi[k] - lo[k], floor_e);
+    return std::cbrt(vol / (cps * std::max(1, m)));
+  };
+  const double cs0 = cell_for(clo, chi, n);
+  std::vector<int32_t> small;
+  small.reserve((size_t)n);
+  for (int i = 0; i < n; i++) {
+    if (std::fabs(r[i]) > 2.0 * cs0) out.glob.push_back(i);
+    else small.push_back(i);
+  }
+  if (out.glob.size() > 64) return false;  // every line would test them all
+  if (small.empty()) {  // only global spheres: one empty cell
+    out.cs = 1.0f;
+    out.nx = out.ny = out.nz = 1;
+    out.reg_margin = FLT_MAX;
+    out.start.assign(2, 0);
+    out.rec.assign(4, UgRec{0.0f, 0.0f, 0.0f, -1.0f});
+    out.rid.assign(4, 0);
+    out.q.assign(1, UgRec{0.0f, 0.0f, 0.0f, -1.0f});
+    return true;
+  }
+  double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+  for (int i : small) {
+    const double c[3] = {cx[i], cy[i], cz[i]}, a = std::fabs(r[i]);
+    for (int k = 0; k < 3; k++) {
+      lo[k] = std::min(lo[k], c[k] - a);
+      hi[k] = std::max(hi[k], c[k] + a);
+    }
+  }
+  double E = 0.0;
+  for (int k = 0; k < 3; k++) E = std::max(E, hi[k] - lo[k]);
+  double cs = cell_for(lo, hi, (int)small.size());
+  // listing margin: the device's prefilter margin plus the DDA's fp32 error
+  // (both checked against it per launch, rt_kernel.hip bvh_args)
+  const double mg = 1e-3 * cs + 2e-4 * E;
+  for (int k = 0; k < 3; k++) {
+    lo[k] -= mg;
+    hi[k] += mg;
+  }
+  E += 2.0 * mg;
+  int dim[3];
+  for (int it = 0; it < 2; it++) {  // at most 512 cells per axis and 16 M cells
+    double cells = 1.0;
+    for (int k = 0; k < 3; k++) {
+      dim[k] = (int)std::min(512.0, std::max(1.0, std::ceil((hi[k] - lo[k]) / cs)));
+      cells *= dim[k];
+    }
+    if (cells <= 16.0 * (1 << 20)) break;
+    cs *= std::cbrt(cells / (16.0 * (1 << 20))) * 1.01;
+  }
+  for (int k = 0; k < 3; k++) cs = std::max(cs, (hi[k] - lo[k]) / dim[k] * (1.0 + 1e-6));
+  if (!(cs > 0.0) || !std::isfinite(cs)) return false;
+  // fp32 origin and cell size, rounded so that the fp32 grid still covers [lo, hi]
+  out.gx = round_down(lo[0]);
+  out.gy = round_down(lo[1]);
+  out.gz = round_down(lo[2]);
+  out.cs = round_up(cs);
+  out.nx = dim[0];
+  out.ny = dim[1];
+  out.nz = dim[2];
+  out.reg_margin = round_down(mg);
+  out.extent = round_up(E);
+  const double g0[3] = {out.gx, out.gy, out.gz}, fcs = out.cs;
+  const size_t ncell = (size_t)dim[0] * dim[1] * dim[2];
+  std::vector<uint32_t> count(ncell + 1, 0u);
+  auto range = [&](int i, int (&a)[3], int (&b)[3]) {
+    const double c[3] = {cx[i], cy[i], cz[i]}, rr = std::fabs(r[i]) + mg;
+    for (int k = 0; k < 3; k++) {
+      a[k] = std::max(0, std::min(dim[k] - 1, (int)std::floor((c[k] - rr - g0[k]) / fcs)));
+      b[k] = std::max(0, std::min(dim[k] - 1, (int)std::floor((c[k] + rr - g0[k]) / fcs)));
+    }
+  };
+  size_t total = 0;
+  for (int i : small) {
+    int a[3], b[3];
+    range(i, a, b);
+    total += (size_t)(b[0] - a[0] + 1) * (b[1] - a[1] + 1) * (b[2] - a[2] + 1);
+    if (total > max_entries) return false;
+    for (int z = a[2]; z <= b[2]; z++)
+      for (int y = a[1]; y <= b[1]; y++)
+        for (int x = a[0]; x <= b[0]; x++) count[((size_t)z * dim[1] + y) * dim[0] + x]++;
+  }
+  out.start.assign(ncell + 1, 0);
+  for (size_t c = 0; c < ncell; c++) out.start[c + 1] = out.start[c] + (int32_t)count[c];
+  out.ids.assign(total, 0);
+  std::vector<int32_t> fill(out.start.begin(), out.start.end() - 1);
+  for (int i : small) {  // ascending sphere index within every cell
+    int a[3], b[3];
+    range(i, a, b);
+    for (int z = a[2]; z <= b[2]; z++)
+      for (int y = a[1]; y <= b[1]; y++)
+        for (int x = a[0]; x <= b[0]; x++) out.ids[(size_t)fill[((size_t)z * dim[1] + y) * dim[0] + x]++] = i;
+  }
+  // the device records: slot data (centre - c0 and |radius| rounded up, fp32)
+  out.q.resize(total + 1);
+  for (size_t k = 0; k < total; k++) {
+    const int i = out.ids[k];
+    float rr = (float)std::fabs(r[i]);
+    if ((double)rr < std::fabs(r[i])) rr = std::nextafter(rr, INFINITY);
+    out.q[k] = UgRec{(float)cx[i], (float)cy[i], (float)cz[i], rr};
+  }
+  out.q[total] = UgRec{0.0f, 0.0f, 0.0f, -1.0f};
+  out.rec.assign(ncell * 4, UgRec{0.0f, 0.0f, 0.0f, -1.0f});
+  out.rid.assign(ncell * 4, 0);
+  for (size_t c = 0; c < ncell; c++) {
+    const int32_t k0 = out.start[c], k1 = out.start[c + 1];
+    const int m = k1 - k0;
+    const int inl = m <= 4 ? m : 3;
+    for (int j = 0; j < inl; j++) {
+      out.rec[4 * c + j] = out.q[(size_t)k0 + j];
+      out.rid[4 * c + j] = out.ids[(size_t)k0 + j];
+    }
+    if (m > 4) {
+      UgRec o{};
+      const int32_t a0 = k0 + 3;
+      std::memcpy(&o.x, &a0, sizeof(float));
+      std::memcpy(&o.y, &k1, sizeof(float));
+      o.w = -2.0f;
+      out.rec[4 * c + 3] = o;
+    }
+  }
+  return true;
 }
 
 }  // namespace rtk

@@ -7,6 +7,7 @@
 // the traversal adds a scene-scale margin at run time (see rt_device.h), so a
 // box test never rejects a sphere the reference's fp64 test could report.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -54,5 +55,42 @@ int32_t build_bvh4(const std::vector<BvhNode> &nodes, std::vector<BvhNode4> &out
 // spheres; depth is unlimited (the traversal is stackless).
 void build_bvh(const double *cx, const double *cy, const double *cz, const double *r, int n, int max_leaf,
                std::vector<BvhNode> &nodes, std::vector<int32_t> &prims);
+
+// Behind grid: a uniform grid of sphere lists for the part of a closest-hit
+// line BEHIND the ray origin.  There the reference's test (sphere.h:26-59) can
+// only report the negative tangent root (disc == 0, sphere.h:43-47) -- any
+// other root of a sphere wholly behind the origin is negative and discarded --
+// so the ordered walks skip boxes wholly behind the origin when this grid
+// exists, and the device visits the cells along the backward half-line instead
+// (rt_device.h behind_cells), testing every listed sphere exactly.  Cells are
+// cubes of edge cs from the origin (gx, gy, gz) (coordinates relative to the
+// BVH centre c0, fp32); a sphere is listed in every cell its box grown by
+// reg_margin meets.  Spheres of radius above 2 cells (a ground sphere) are not
+// listed but in `glob`, tested for every line.  Cell (x, y, z) = k in
+// [start[c], start[c + 1]), c = (z * ny + y) * nx + x.
+// The device reads a cell as one 64-B record of four slots (UgRec: centre -
+// c0 and |radius| rounded up, fp32; w = -1: no further entry; a cell with more
+// than four entries keeps three and, in slot 3, w = -2 and the bit patterns
+// of [k0, k1): its remaining entries q[k], ids[k] of the overflow list); rid
+// holds the slots' sphere ids.
+struct UgRec {
+  float x, y, z, w;
+};
+struct UgridHost {
+  float gx = 0, gy = 0, gz = 0, cs = 0;
+  int nx = 0, ny = 0, nz = 0;
+  float reg_margin = 0;  // listing margin (>= the device's prefilter margin + DDA error, checked per launch)
+  float extent = 0;      // largest edge of the grid (the DDA error scale)
+  std::vector<int32_t> start, ids, glob;  // CSR lists (ids: every entry, in cell order)
+  std::vector<UgRec> rec;                  // [cell][4]
+  std::vector<int32_t> rid;                // [cell][4]
+  std::vector<UgRec> q;                    // per CSR entry (the overflow lists index it)
+};
+// Builds the grid over spheres (centres relative to c0, radii r), about
+// cells_per_sphere cells per listed sphere; false (no grid) for an empty
+// scene, non-finite values, more than 64 global spheres or more than
+// max_entries list entries.
+bool build_ugrid(const double *cx, const double *cy, const double *cz, const double *r, int n, size_t max_entries,
+                 UgridHost &out, double cells_per_sphere = 2.0);
 
 }  // namespace rtk

@@ -437,6 +437,23 @@ __device__ __forceinline__ unsigned long long rt_stamp() {
 // the cull proof above needs, and far above the fp32 rounding (~1e-7 of the
 // diameter) of the slab arithmetic.  Closest-hit prunes a box only when its
 // entry t exceeds the current best by a margin; any-hit prunes beyond T.
+// The uniform grid (rt_bvh.h UgridHost) on the device: on = 1 when this
+// launch may use it (the host checked its listing margin against pmargin and
+// the DDA error bound).  A record slot or overflow entry q = centre - c0
+// (fp32) and |radius| rounded up.
+struct UgArgs {
+  const float4 *rec;   // [cell][4] list records (grid_line)
+  const int32_t *rid;  // [cell][4] their sphere ids
+  const float4 *q;     // overflow lists: q[k], ids[k]
+  const int32_t *ids;
+  const int32_t *glob;
+  int nglob;
+  int nx, ny, nz;
+  float gx, gy, gz, cs;
+  int on;
+  int closest;  // 1: closest hits walk the grid along the whole line (grid_closest_line) instead of the BVH
+  float tol;    // 1e-4 * the grid's extent: the DDA's error bound, with room to spare
+};
 struct BvhArgs {
   const BvhNode *nodes;
   const int32_t *prims;
@@ -463,6 +480,11 @@ struct BvhArgs {
   int odepth;   // stack entries per lane (the tree depth)
   int2 *ostk;
   int ostk_off;  // ostk == nullptr: the stacks sit at this byte offset of dynamic LDS ([wave][entry][lane]); -1 none
+  // the ordered 4-wide closest-hit walks enter a box only if its (grown) exit
+  // t is >= tf_min: 0 with the behind grid (ug.on; boxes wholly behind the
+  // origin are then behind_cells' part), -inf without it
+  float tf_min;
+  UgArgs ug;
 };
 constexpr int kOrderedStack = 24;  // pending far children; the host requires depth <= this
 
@@ -640,6 +662,7 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
   // which costs a visit, never a result); NaNs keep boxes either way.
   auto tmax_f = [&] { return float_up(tmax_fn()); };
   float tmf = tmax_f();
+  const float tfm = bv.tf_min;
   {
     const BvhNode &r0 = bv.nodes[0];
     const float ax = (r0.lo[0] - lx) * ix, bx = (r0.hi[0] - hx) * ix;
@@ -669,11 +692,7 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
         const float az = (nd->loz[k] - lz) * iz, bz = (nd->hiz[k] - hz) * iz;
         const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
         const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-#ifdef RT_EXPERIMENT_FWD  // diagnostic only (not exact): skip boxes wholly behind the origin
-        const bool h = tn <= tf && !(tn > tmf) && tf >= 0.0f;
-#else
-        const bool h = tn <= tf && !(tn > tmf);  // NaN (unused slot) -> false
-#endif
+        const bool h = tn <= tf && !(tn > tmf) && tf >= tfm;  // NaN (unused slot) -> false
         hits += h ? 1 : 0;
         // sort key: a hit sorts below every miss (fminf keeps it finite-or-below-inf)
         t[k] = h ? fminf(tn, 3.0e38f) : __builtin_inff();
@@ -731,7 +750,7 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
 // hit is the same.  The fp32 form of the ray (walk4_ray) is recomputed
 // wherever a kernel resumes walks, so it is not live across other work.
 struct Walk4Ray {
-  float ox, oy, oz, dx, dy, dz, ix, iy, iz, dd, lx, ly, lz, hx, hy, hz;
+  float ox, oy, oz, dx, dy, dz, ix, iy, iz, dd, lx, ly, lz, hx, hy, hz, tfm;
 };
 __device__ __forceinline__ Walk4Ray walk4_ray(const BvhArgs &bv, D3 o, D3 d) {
   Walk4Ray r;
@@ -741,6 +760,7 @@ __device__ __forceinline__ Walk4Ray walk4_ray(const BvhArgs &bv, D3 o, D3 d) {
   r.dd = (r.dx * r.dx + r.dy * r.dy + r.dz * r.dz) * (1.0f + 1e-5f);
   const float m = bv.margin;
   r.lx = r.ox + m, r.ly = r.oy + m, r.lz = r.oz + m, r.hx = r.ox - m, r.hy = r.oy - m, r.hz = r.oz - m;
+  r.tfm = bv.tf_min;
   return r;
 }
 __device__ __forceinline__ bool walk4_begin(const BvhArgs &bv, const Walk4Ray &r, float tmf, int &ref, int &sp) {
@@ -773,11 +793,7 @@ __device__ __forceinline__ bool walk4_step(const BvhArgs &bv, const Walk4Ray &r,
       const float az = (nd->loz[k] - r.lz) * r.iz, bz = (nd->hiz[k] - r.hz) * r.iz;
       const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
       const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-#ifdef RT_EXPERIMENT_FWD
-      const bool h = tn <= tf && !(tn > tmf) && tf >= 0.0f;
-#else
-      const bool h = tn <= tf && !(tn > tmf);
-#endif
+      const bool h = tn <= tf && !(tn > tmf) && tf >= r.tfm;
       hits += h ? 1 : 0;
       t[k] = h ? fminf(tn, 3.0e38f) : __builtin_inff();
       c[k] = nd->c[k];
@@ -846,6 +862,170 @@ __device__ __forceinline__ void closest_test(const SphGeo &s, int i, D3 o, D3 d,
       bi = i;
     }
   }
+}
+
+// The grid walks (bv.ug, the uniform grid of rt_bvh.h UgridHost): a 3-D DDA
+// in fp32 along a closest-hit line, visiting its cells in order and handing
+// every sphere listed there that the line passes near to test_fn (which folds
+// it into the lexicographic (t, index) minimum, so a sphere tested twice is
+// harmless).  Two uses:
+//
+// behind_cells -- the part of the line BEHIND its origin, when the ordered
+// walks skipped the boxes wholly behind it (bv.tf_min = 0).  A box whose
+// grown exit t is < 0 in the walk's fp32 slab test (error ~2^-23 of the
+// diameter, far inside the 1e-6 margin) holds only spheres all of whose
+// points lie at t < 0.  For such a sphere the reference's test
+// (sphere.h:26-59) reports a hit only through its disc == 0 branch (the
+// tangent root -b/2a, kept whatever its sign, sphere.h:43-47): with disc > 0
+// both roots are negative by more than their rounding (|oc| 2^-50 << the
+// margin), so max(t1, t2) < 0 is a miss; and disc == 0 needs the line within
+// ~2e-8 of the diameter of the sphere's surface (the cull proof's bound,
+// above).  So it suffices to test every sphere whose surface the backward
+// half-line {o + t d, t <= 0} passes within the prefilter margin of.
+//
+// grid_closest_line -- the whole closest hit (bv.ug.closest, instead of the
+// BVH walk): the line from where it enters the grid, in order along +d; the
+// walk stops after the first cell whose exit t is beyond the best t + tol: a
+// sphere with a root t* below the best has that root's point on its surface,
+// inside a cell entered at t <= t* that the DDA has visited.
+//
+// Coverage: the global spheres (listed in no cell) are tested first; every
+// other sphere is listed in every cell its box grown by reg_margin meets, and
+// reg_margin >= pmargin + tol, tol = 1e-4 * the grid's extent (the host's
+// per-launch check): every line point within R + pmargin of a listed centre
+// lies within reg_margin - tol of that sphere's cells, and the visited cells
+// miss no line point by more than the DDA's fp32 error (a few ulps of the
+// extent, << tol).  Prefilter (fp32, as the BVH walks' leaves): a sphere is
+// skipped when the line misses it grown by pmargin, and -- in cells wholly
+// behind the origin -- when the line runs deep inside it (disc > 0 there,
+// both roots negative; a root ahead lies in a cell ahead, where the sphere
+// is listed too and tested).  NaN lines return at once (the reference's
+// test never records a NaN t).
+//
+// A cell's list is one 64-B record of four float4 slots (centre - c0, |r|
+// rounded up; w = -1: no more entries; w = -2 in slot 3: entries x..y of the
+// overflow list continue the cell), so a cell is one 64-B load, issued one
+// cell ahead; sphere ids are read only for the spheres that pass.
+template <bool kWhole, typename F, typename B>
+__host__ __device__ __forceinline__ void grid_line(const BvhArgs &bv, D3 o, D3 d, Work &work, F &&test_fn,
+                                                   B &&best_fn) {
+  const UgArgs &ug = bv.ug;
+  for (int k = 0; k < ug.nglob; ++k) {
+    work.exact += 1;
+    test_fn((int)ug.glob[k]);
+  }
+  const float ox = (float)(o.x - bv.c0x), oy = (float)(o.y - bv.c0y), oz = (float)(o.z - bv.c0z);
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float d2 = dx * dx + dy * dy + dz * dz;
+  const float dd_hi = d2 * (1.0f + 1e-5f), dd_lo = d2 * (1.0f - 1e-5f);
+  const float pm = bv.pmargin;
+  const float cs = ug.cs;
+  const float p0 = ox - ug.gx, p1 = oy - ug.gy, p2 = oz - ug.gz;  // the origin in grid coordinates
+  // walk direction: +d for the whole line, -d behind the origin (then s = -t)
+  const float v0 = kWhole ? dx : -dx, v1 = kWhole ? dy : -dy, v2 = kWhole ? dz : -dz;
+  const float i0 = 1.0f / v0, i1 = 1.0f / v1, i2 = 1.0f / v2;  // +-inf for a zero component
+  // the walked part inside the grid box [0, n cs]^3: s in [s0, s1]
+  float s0 = kWhole ? -__builtin_inff() : 0.0f, s1 = __builtin_inff();
+  auto clip = [&](float p, float iv, int n) {
+    const float ta = (0.0f - p) * iv, tb = ((float)n * cs - p) * iv;  // a zero component: +-inf or NaN
+    if (iv == __builtin_inff() || iv == -__builtin_inff()) {
+      if (!(p >= 0.0f && p <= (float)n * cs)) s1 = -__builtin_inff();  // parallel to the slab and outside it
+    } else {
+      s0 = fmaxf(s0, fminf(ta, tb));
+      s1 = fminf(s1, fmaxf(ta, tb));
+    }
+  };
+  clip(p0, i0, ug.nx);
+  clip(p1, i1, ug.ny);
+  clip(p2, i2, ug.nz);
+  if (!(s0 <= s1)) return;  // misses the grid (or NaN)
+  const float ics = 1.0f / cs;
+  auto cell_of = [&](float p, float v, int n) {
+    const int c = (int)floorf((p + v * s0) * ics);
+    return c < 0 ? 0 : (c >= n ? n - 1 : c);
+  };
+  int c0 = cell_of(p0, v0, ug.nx), c1 = cell_of(p1, v1, ug.ny), c2 = cell_of(p2, v2, ug.nz);
+  const int st0 = v0 > 0.0f ? 1 : -1, st1 = v1 > 0.0f ? 1 : -1, st2 = v2 > 0.0f ? 1 : -1;
+  // the exit s of the current cell along each axis (re-derived per step, not accumulated)
+  auto exit_s = [&](int c, float p, float iv, int st) {
+    return (iv == __builtin_inff() || iv == -__builtin_inff()) ? __builtin_inff()
+                                                              : ((float)(c + (st > 0 ? 1 : 0)) * cs - p) * iv;
+  };
+  int ci = (c2 * ug.ny + c1) * ug.nx + c0;
+  float4 r0 = ug.rec[4 * ci], r1 = ug.rec[4 * ci + 1], r2 = ug.rec[4 * ci + 2], r3 = ug.rec[4 * ci + 3];
+  int guard = ug.nx + ug.ny + ug.nz + 2;  // every step leaves the cell along one axis for good
+  int last = -1;                          // the sphere tested last (spheres span neighbouring cells)
+  while (true) {
+    // the next cell first, so its record is in flight while this one's slots are tested
+    const float e0 = exit_s(c0, p0, i0, st0), e1 = exit_s(c1, p1, i1, st1), e2 = exit_s(c2, p2, i2, st2);
+    const float ex = fminf(e0, fminf(e1, e2));  // this cell's exit
+    bool more = false;
+    if (--guard > 0) {
+      if (e0 <= e1 && e0 <= e2) {
+        c0 += st0;
+        more = e0 <= s1 && c0 >= 0 && c0 < ug.nx;
+      } else if (e1 <= e2) {
+        c1 += st1;
+        more = e1 <= s1 && c1 >= 0 && c1 < ug.ny;
+      } else {
+        c2 += st2;
+        more = e2 <= s1 && c2 >= 0 && c2 < ug.nz;
+      }
+    }
+    const int cur = ci;
+    float4 n0 = r0, n1 = r1, n2 = r2, n3 = r3;
+    if (more) {
+      ci = (c2 * ug.ny + c1) * ug.nx + c0;
+      n0 = ug.rec[4 * ci];
+      n1 = ug.rec[4 * ci + 1];
+      n2 = ug.rec[4 * ci + 2];
+      n3 = ug.rec[4 * ci + 3];
+    }
+    work.cull += 1;
+    // cells wholly behind the origin: the deep-inside skip applies
+    const bool behind = kWhole ? ex < 0.0f : true;
+    auto one = [&](const float4 &q, int id_at, const int32_t *ids) {
+      const float wx = q.x - ox, wy = q.y - oy, wz = q.z - oz;
+      const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
+      const float x2 = cx * cx + cy * cy + cz * cz;  // (distance to the line)^2 |d|^2
+      const float ro = q.w + pm, ri = q.w * (1.0f - 0x1p-22f) - pm;
+      if (x2 > ro * ro * dd_hi) return;                          // misses the grown sphere
+      if (behind && ri > 0.0f && x2 < ri * ri * dd_lo) return;  // runs deep inside it
+      const int id = (int)ids[id_at];
+      if (id == last) return;
+      last = id;
+      work.exact += 1;
+      test_fn(id);
+    };
+    // false: no slot after this one
+    auto slot = [&](const float4 &q, int j) {
+      if (q.w >= 0.0f) {
+        one(q, 4 * cur + j, ug.rid);
+        return true;
+      }
+      if (q.w == -2.0f)  // the cell continues in the overflow list
+        for (int k = __builtin_bit_cast(int, q.x), ke = __builtin_bit_cast(int, q.y); k < ke; ++k) one(ug.q[k], k, ug.ids);
+      return false;
+    };
+    if (slot(r0, 0) && slot(r1, 1) && slot(r2, 2)) slot(r3, 3);
+    if (!more) break;
+    if (kWhole && (double)ex > best_fn() + (double)ug.tol) break;
+    r0 = n0;
+    r1 = n1;
+    r2 = n2;
+    r3 = n3;
+  }
+}
+
+// Host-callable too (tests/native/ug_check.cpp runs this same code on the CPU).
+template <typename F>
+__host__ __device__ __forceinline__ void behind_cells(const BvhArgs &bv, D3 o, D3 d, Work &work, F &&test_fn) {
+  grid_line<false>(bv, o, d, work, test_fn, [] { return 0.0; });
+}
+template <typename F, typename B>
+__host__ __device__ __forceinline__ void grid_closest_line(const BvhArgs &bv, D3 o, D3 d, Work &work, F &&test_fn,
+                                                           B &&best_fn) {
+  grid_line<true>(bv, o, d, work, test_fn, best_fn);
 }
 
 // LDS layout of a staged scene: sphere geometry, radii, lights and, when the
@@ -1052,11 +1232,21 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       return true;
     };
     if constexpr (kFast) {
-      bvh_walk_ordered4<true>(bv, o, d, tmax, work, leaf);
+      if (bv.ug.on && bv.ug.closest) {
+        grid_closest_line(bv, o, d, work, test, [&] { return bt; });
+      } else {
+        bvh_walk_ordered4<true>(bv, o, d, tmax, work, leaf);
+        if (bv.ug.on) behind_cells(bv, o, d, work, test);
+      }
     } else {
-      if (has_ordered_stack(bv) && bv.wide) bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
-      else if (has_ordered_stack(bv)) bvh_walk_ordered(bv, o, d, tmax, work, leaf);
-      else bvh_walk(bv, o, d, tmax, work, leaf);
+      if (has_ordered_stack(bv) && bv.wide) {
+        bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
+        if (bv.ug.on) behind_cells(bv, o, d, work, test);
+      } else if (has_ordered_stack(bv)) {
+        bvh_walk_ordered(bv, o, d, tmax, work, leaf);
+      } else {
+        bvh_walk(bv, o, d, tmax, work, leaf);
+      }
     }
   }
 #ifdef RT_STAMPS

@@ -1230,6 +1230,16 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
     }
     const bool ready = act && !walking;
     if (__ballot(ready)) {
+      {
+        // the line's part behind its origin (the walk skipped boxes wholly behind it)
+        const BvhArgs &bv = kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv);
+        if (bv.ug.on && ready) {
+          const double a4 = 4.0 * dot(d, d), a2 = 0.5 * a4;
+          const bool fast = a2_ok(a2);
+          const SphGeo *__restrict__ g = a.geo;
+          behind_cells(bv, o, d, work, [&](int i) { closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi); });
+        }
+      }
       int outcome = 0, nkey = 0;
       D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
       double refl = 0.0;
@@ -1299,6 +1309,7 @@ __global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__rest
 using namespace rtk;
 
 constexpr int kBvhAlwaysAbove = 1024;
+constexpr size_t kUgMaxEntries = size_t(64) << 20;  // behind-grid list entries (20 B each)
 
 struct rt_ctx {
   int device = 0;
@@ -1349,6 +1360,23 @@ struct rt_ctx {
   bool sg_ok = false;
   size_t sg_entries = 0;
   double sg_build_ms = 0.0;
+  // behind grid (rt_bvh.h build_ugrid): the backward half of the ordered
+  // walks' closest-hit lines (rt_device.h behind_cells), built at upload
+  int ug_mode = -1;  // RT_HIP_BEHIND_GRID: -1 auto (scenes above kBvhAlwaysAbove spheres), 0 off, 1 on
+  // RT_HIP_GRID_CLOSEST: 1 (default) = with the grid, closest hits walk it along the whole line instead of the
+  // BVH (rt_device.h grid_closest_line; synth10k 3.03 -> 2.93 ms per frame, profiles/r3u); 0 = the ordered BVH
+  // walk ahead of the origin + behind_cells behind it (3.15 ms: the grid walk behind the origin costs more than
+  // the BVH boxes it replaces)
+  int ug_closest = 1;
+  int32_t *d_ug_rid = nullptr, *d_ug_ids = nullptr, *d_ug_glob = nullptr;
+  UgRec *d_ug_rec = nullptr, *d_ug_q = nullptr;
+  double ug_cells = 2.0;  // RT_HIP_GRID_CELLS: cells per listed sphere
+  UgArgs ug{};        // its device arguments (on = 0 until a launch allows it)
+  float ug_reg_margin = 0.0f, ug_extent = 0.0f;
+  bool ug_ok = false;
+  bool ug_last = false;  // the most recent launch used it
+  size_t ug_entries = 0;
+  double ug_build_ms = 0.0;
   double c0[3] = {0, 0, 0};
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // bounds of spheres and lights
   double rmax = 0;
@@ -1483,6 +1511,16 @@ void free_scene(rt_ctx *c) {
   c->sg_ok = false;
   c->sg_grids = 0;
   c->sg_entries = 0;
+  if (c->d_ug_rec) (void)hipFree(c->d_ug_rec);
+  if (c->d_ug_rid) (void)hipFree(c->d_ug_rid);
+  if (c->d_ug_ids) (void)hipFree(c->d_ug_ids);
+  if (c->d_ug_glob) (void)hipFree(c->d_ug_glob);
+  if (c->d_ug_q) (void)hipFree(c->d_ug_q);
+  c->d_ug_rid = c->d_ug_ids = c->d_ug_glob = nullptr;
+  c->d_ug_rec = c->d_ug_q = nullptr;
+  c->ug = UgArgs{};
+  c->ug_ok = false;
+  c->ug_entries = 0;
   c->d_bvh = nullptr;
   c->d_prims = nullptr;
   c->bvh_nodes = 0;
@@ -1528,6 +1566,18 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   b.min_cands = c->bvh_min;
   b.always = c->bvh_always >= 0 ? c->bvh_always : (c->nsph > kBvhAlwaysAbove ? 1 : 0);
   b.max_groups = c->bvh_groups;
+  // the behind grid, when its listing margin covers this view's prefilter
+  // margin plus the DDA's error bound (rt_device.h behind_cells); the ordered
+  // walks then skip boxes wholly behind the origin
+  b.tf_min = -INFINITY;
+  b.ug = UgArgs{};
+  if (c->ug_ok && b.nnodes > 0 && b.ordered && b.wide && std::isfinite(b.pmargin) &&
+      (double)b.pmargin + 1e-4 * (double)c->ug_extent <= (double)c->ug_reg_margin) {
+    b.ug = c->ug;
+    b.ug.on = 1;
+    b.ug.closest = c->ug_closest;
+    b.tf_min = 0.0f;
+  }
   return b;
 }
 
@@ -1831,6 +1881,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.depth = depth;
   ra.rows = rows;
   ra.bv = bv;
+  c->ug_last = bv.ug.on != 0;
   ra.lg = lg;
   ra.od = od;
   ra.gstack = gstack;
@@ -1892,7 +1943,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       // the walk kernel where every closest hit walks the BVH anyway (large
       // scenes: synth10k 12.2 -> 11.0 ms per 8-frame launch); small scenes keep
       // the cull sweeps (synth200 1 % slower on the walk kernel)
-      if (kCull && fast && c->defer_walk && bv.nnodes > 0 && bv.always)
+      if (kCull && fast && c->defer_walk && bv.nnodes > 0 && bv.always && !(bv.ug.on && bv.ug.closest))
         hipLaunchKernelGGL(render_deferred_walk, dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
       else if (fast)
         hipLaunchKernelGGL((render_deferred<kCull, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
@@ -2032,6 +2083,9 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_CAM_GRID_N")) c->cg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID")) c->sg_mode = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID_N")) c->sg_n_opt = std::max(1, std::min(256, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_BEHIND_GRID")) c->ug_mode = std::max(-1, std::min(1, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_GRID_CLOSEST")) c->ug_closest = std::atoi(e) != 0 ? 1 : 0;  // (see ug_closest)
+  if (const char *e = std::getenv("RT_HIP_GRID_CELLS")) c->ug_cells = std::max(0.05, std::min(64.0, std::atof(e)));
   if (const char *e = std::getenv("RT_HIP_SINGLE_CLASS"))
     c->single_class = std::max(0, std::min(kSchedClasses, std::atoi(e)));
   auto bail = [&](int rc) {
@@ -2206,6 +2260,42 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     delete[] hm;
     delete[] hl;
     return rc;
+  }
+  if (c->ug_mode > 0 || (c->ug_mode < 0 && big)) {
+    const auto t_ug = std::chrono::steady_clock::now();
+    UgridHost ug;
+    if (build_ugrid(bx.data(), by.data(), bz.data(), br.data(), n, kUgMaxEntries, ug, c->ug_cells)) {
+      if ((e = hipMalloc(&c->d_ug_rec, sizeof(UgRec) * ug.rec.size())) != hipSuccess ||
+          (e = hipMalloc(&c->d_ug_rid, sizeof(int32_t) * ug.rid.size())) != hipSuccess ||
+          (e = hipMalloc(&c->d_ug_q, sizeof(UgRec) * ug.q.size())) != hipSuccess ||
+          (e = hipMalloc(&c->d_ug_ids, sizeof(int32_t) * (ug.ids.size() + 1))) != hipSuccess ||
+          (e = hipMalloc(&c->d_ug_glob, sizeof(int32_t) * (ug.glob.size() + 1))) != hipSuccess ||
+          (e = hipMemcpy(c->d_ug_rec, ug.rec.data(), sizeof(UgRec) * ug.rec.size(), hipMemcpyHostToDevice)) !=
+              hipSuccess ||
+          (e = hipMemcpy(c->d_ug_rid, ug.rid.data(), sizeof(int32_t) * ug.rid.size(), hipMemcpyHostToDevice)) !=
+              hipSuccess ||
+          (e = hipMemcpy(c->d_ug_q, ug.q.data(), sizeof(UgRec) * ug.q.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+          (!ug.ids.empty() && (e = hipMemcpy(c->d_ug_ids, ug.ids.data(), sizeof(int32_t) * ug.ids.size(),
+                                             hipMemcpyHostToDevice)) != hipSuccess) ||
+          (!ug.glob.empty() && (e = hipMemcpy(c->d_ug_glob, ug.glob.data(), sizeof(int32_t) * ug.glob.size(),
+                                              hipMemcpyHostToDevice)) != hipSuccess)) {
+        rc = fail(c, e, "rt_upload_scene(uniform grid)");
+        free_scene(c);
+        delete[] hg;
+        delete[] hr;
+        delete[] hm;
+        delete[] hl;
+        return rc;
+      }
+      c->ug = UgArgs{reinterpret_cast<const float4 *>(c->d_ug_rec), c->d_ug_rid,
+                     reinterpret_cast<const float4 *>(c->d_ug_q), c->d_ug_ids, c->d_ug_glob, (int)ug.glob.size(),
+                     ug.nx, ug.ny, ug.nz, ug.gx, ug.gy, ug.gz, ug.cs, 0, 0, (float)(1e-4 * (double)ug.extent)};
+      c->ug_reg_margin = ug.reg_margin;
+      c->ug_extent = ug.extent;
+      c->ug_entries = ug.ids.size();
+      c->ug_ok = true;
+    }
+    c->ug_build_ms = ms_since(t_ug);
   }
   c->bvh_nodes = (int)nodes.size();
   c->bvh2_root = root2;
@@ -2468,6 +2558,11 @@ int rt_get_info(rt_ctx *c, rt_info *out) {
   out->sphere_grid_n = c->sg_ok ? c->sg_n : 0;
   out->sphere_grid_entries = c->sg_ok ? (uint64_t)c->sg_entries : 0;
   out->sphere_grid_build_ms = c->sg_build_ms;
+  out->behind_grid = c->ug_ok ? 1 : 0;
+  out->behind_grid_last = c->ug_last ? 1 : 0;
+  out->behind_grid_cells = c->ug_ok ? (uint64_t)c->ug.nx * (uint64_t)c->ug.ny * (uint64_t)c->ug.nz : 0;
+  out->behind_grid_entries = c->ug_ok ? (uint64_t)c->ug_entries : 0;
+  out->behind_grid_build_ms = c->ug_build_ms;
   return RT_OK;
 }
 

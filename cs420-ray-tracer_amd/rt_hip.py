@@ -22,7 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(HERE, "librt_hip.so")
 
 RT_MAX_DEPTH = 64
-ABI_VERSION = 8  # RT_HIP_ABI_VERSION in include/rt_hip.h
+ABI_VERSION = 9  # RT_HIP_ABI_VERSION in include/rt_hip.h
 MAX_FRAMES = 32  # RT_MAX_FRAMES
 
 
@@ -59,7 +59,9 @@ class rt_info(C.Structure):
                 ("cam_grid_build_ms", C.c_double), ("tile_order_builds", C.c_uint64),
                 ("tile_order_build_ms", C.c_double), ("upload_ms", C.c_double), ("launches", C.c_uint64),
                 ("sphere_grids", C.c_int32), ("sphere_grid_n", C.c_int32), ("sphere_grid_entries", C.c_uint64),
-                ("sphere_grid_build_ms", C.c_double)]
+                ("sphere_grid_build_ms", C.c_double), ("behind_grid", C.c_int32), ("behind_grid_last", C.c_int32),
+                ("behind_grid_cells", C.c_uint64), ("behind_grid_entries", C.c_uint64),
+                ("behind_grid_build_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

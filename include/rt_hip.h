@@ -52,8 +52,9 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 8  /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
-                                   6: rt_render_tiles; 7: rt_get_info; 8: rt_info sphere-grid fields */
+#define RT_HIP_ABI_VERSION 9  /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
+                                   6: rt_render_tiles; 7: rt_get_info; 8: rt_info sphere-grid fields;
+                                   9: rt_info behind-grid fields */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -271,6 +272,11 @@ typedef struct rt_info {
     int32_t sphere_grid_n;       /* their cells per cube-map face edge */
     uint64_t sphere_grid_entries;  /* list entries of all sphere grids (8 bytes each) */
     double sphere_grid_build_ms; /* host wall time of their build, part of upload_ms */
+    int32_t behind_grid;         /* 1: the scene has a behind grid (closest-hit lines' part behind their origin) */
+    int32_t behind_grid_last;    /* 1: the most recent launch's BVH walks used it */
+    uint64_t behind_grid_cells;  /* its cells */
+    uint64_t behind_grid_entries;  /* its list entries (20 bytes each) */
+    double behind_grid_build_ms; /* host wall time of its build, part of upload_ms */
 } rt_info;
 int rt_get_info(rt_ctx *ctx, rt_info *out);
 
