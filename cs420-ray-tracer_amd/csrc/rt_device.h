@@ -955,21 +955,25 @@ __host__ __device__ __forceinline__ void grid_line(const BvhArgs &bv, D3 o, D3 d
   float4 r0 = ug.rec[4 * ci], r1 = ug.rec[4 * ci + 1], r2 = ug.rec[4 * ci + 2], r3 = ug.rec[4 * ci + 3];
   int guard = ug.nx + ug.ny + ug.nz + 2;  // every step leaves the cell along one axis for good
   int last = -1;                          // the sphere tested last (spheres span neighbouring cells)
+  // the current cell's exit s per axis; a step re-derives only the stepped axis's
+  float e0 = exit_s(c0, p0, i0, st0), e1 = exit_s(c1, p1, i1, st1), e2 = exit_s(c2, p2, i2, st2);
   while (true) {
     // the next cell first, so its record is in flight while this one's slots are tested
-    const float e0 = exit_s(c0, p0, i0, st0), e1 = exit_s(c1, p1, i1, st1), e2 = exit_s(c2, p2, i2, st2);
     const float ex = fminf(e0, fminf(e1, e2));  // this cell's exit
     bool more = false;
     if (--guard > 0) {
       if (e0 <= e1 && e0 <= e2) {
         c0 += st0;
         more = e0 <= s1 && c0 >= 0 && c0 < ug.nx;
+        e0 = exit_s(c0, p0, i0, st0);
       } else if (e1 <= e2) {
         c1 += st1;
         more = e1 <= s1 && c1 >= 0 && c1 < ug.ny;
+        e1 = exit_s(c1, p1, i1, st1);
       } else {
         c2 += st2;
         more = e2 <= s1 && c2 >= 0 && c2 < ug.nz;
+        e2 = exit_s(c2, p2, i2, st2);
       }
     }
     const int cur = ci;
@@ -1239,7 +1243,9 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
         if (bv.ug.on) behind_cells(bv, o, d, work, test);
       }
     } else {
-      if (has_ordered_stack(bv) && bv.wide) {
+      if (bv.ug.on && bv.ug.closest) {
+        grid_closest_line(bv, o, d, work, test, [&] { return bt; });
+      } else if (has_ordered_stack(bv) && bv.wide) {
         bvh_walk_ordered4(bv, o, d, tmax, work, leaf);
         if (bv.ug.on) behind_cells(bv, o, d, work, test);
       } else if (has_ordered_stack(bv)) {

@@ -1577,6 +1577,10 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
     b.ug.on = 1;
     b.ug.closest = c->ug_closest;
     b.tf_min = 0.0f;
+    // no closest hit walks the BVH then (the shadow queries use the light
+    // grids or the stackless walk): no LDS stacks for the ordered walk, so
+    // merge_tiles keeps its longest ray queue
+    if (b.ug.closest) b.odepth = 0;
   }
   return b;
 }
