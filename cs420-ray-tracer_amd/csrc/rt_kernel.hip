@@ -103,6 +103,7 @@ struct RenderArgs {
   int pix_off;                    // kStackMerge: LDS offset of the wave's finished pixels (flush_tile)
   int rows_dword;                 // kStackMerge: every 8-pixel tile row starts dword aligned (flush_tile)
   int defer_level;                // kStackMerge: rays of this reflection level and deeper are deferred
+  int xcd_frames;                 // multi-frame launches: every frame of a tile group on one XCD (render_kernel)
 };
 // the whole struct is the kernel's argument block (kernarg segment, at most 4 KiB)
 static_assert(sizeof(RenderArgs) <= 4096, "RenderArgs exceeds the kernel-argument segment");
@@ -967,10 +968,25 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
   const int b = blockIdx.x;
   if (b == 0 && a.zero_next)
     for (int i = (int)threadIdx.x; i < kShards * kShardStride; i += (int)blockDim.x) a.zero_next[i] = 0ull;
-  // the frames of a multi-frame launch share the tile order: slots b of one
-  // tile slot are adjacent, so every frame's copy of a heavy tile starts early
+  // the frames of a multi-frame launch share the tile order, so every frame's
+  // copy of a heavy tile starts early.  Workgroups are dealt to the 8 XCDs
+  // round robin (b % 8); with xcd_frames the k-th workgroup of XCD x renders
+  // frame k % F of tile group 8 (k / F) + x, so all F copies of a group run on
+  // the XCD whose L2 holds that group's scene lists and nodes (the grid is
+  // padded to a multiple of 8 groups; the padding exits); otherwise the F
+  // copies of a group are adjacent (b / F, b % F) and spread over the XCDs
   const int nf = a.frames;
-  const int slot = nf > 1 ? b / nf : b, frame = nf > 1 ? b - slot * nf : 0;
+  int slot = b, frame = 0;
+  if (nf > 1) {
+    if (a.xcd_frames) {
+      const int k = b >> 3;
+      slot = (k / nf) * 8 + (b & 7);
+      frame = k - (k / nf) * nf;
+    } else {
+      slot = b / nf;
+      frame = b - slot * nf;
+    }
+  }
   int tile = slot;
   if constexpr (kStack == kStackMerge) {
     if (slot >= a.nslots) return;  // slot = this wave's group of tile slots (merge_tiles)
@@ -1029,7 +1045,8 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
   }
   RT_ACC(work, 5, t_wave);
 #ifdef RT_STAMPS
-  record_timeline(tile * kWg + wave, t_real0, work);
+  // merged kernels: one entry per workgroup of the launch (slot b = group b / F of frame b % F)
+  record_timeline(kStack == kStackMerge ? (unsigned)blockIdx.x : (unsigned)(tile * kWg + wave), t_real0, work);
 #endif
   flush_counts(kernarg_late<!kLdsGeo, offsetof(RenderArgs, counters)>(a.counters), sums, work);
 }
@@ -1457,6 +1474,12 @@ struct rt_ctx {
   // share their reflection rays' passes (class >= 1 there: 0.2285 -> 0.2364 ms
   // per frame, profiles/r3c/ab_single.log)
   int single_class = -1;
+  // RT_HIP_XCD_FRAMES: multi-frame launches put every frame of a tile group on
+  // one XCD (render_kernel).  -1 (default): for scenes with the uniform grid
+  // (large scenes, whose lists and nodes outgrow an XCD's L2: synth10k 2.58 ->
+  // 2.49 ms per frame); synth200 keeps the adjacent order (0.1943 vs 0.1958
+  // ms per frame at 32 frames, equal at 20; profiles/r3u/ab_xcd_frames.log)
+  int xcd_frames = -1;
   // rt_get_info: host-side builds made by the render calls
   bool cg_last = false;
   int cg_last_n = 0;
@@ -1868,7 +1891,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       nslots = nsingle + (ntiles - nsingle + kMergeTiles - 1) / kMergeTiles;
     }
   }
-  const dim3 grid((unsigned)(nslots * nf));
+  const bool xcd_frames = nf > 1 && (c->xcd_frames > 0 || (c->xcd_frames < 0 && bv.ug.on));
+  const dim3 grid((unsigned)((xcd_frames ? (nslots + 7) / 8 * 8 : nslots) * nf));
   RenderArgs ra{};
   ra.geo = c->d_geo;
   ra.radius = c->d_rad;
@@ -1908,6 +1932,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   // row k of frame f starts at ptr + f fstride + 3 (k W + x): dword aligned for every k, f and x = 8i
   ra.rows_dword = ((reinterpret_cast<uintptr_t>(od.ptr) | (uintptr_t)(3 * (size_t)W) | (uintptr_t)od.fstride) & 3) == 0;
   ra.defer_level = c->defer_level;
+  ra.xcd_frames = xcd_frames ? 1 : 0;
   if (kStack == kStackMerge && (c->defer > 0 || (c->defer < 0 && nf > 1)) && depth > c->defer_level) {
     // room for 1/8 of the launch's pixels (deferred rays are ~2 % on synth200); a ray
     // that finds its shard segment full simply continues in its merge_tiles lane
@@ -2089,6 +2114,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID_N")) c->sg_n_opt = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_BEHIND_GRID")) c->ug_mode = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_GRID_CLOSEST")) c->ug_closest = std::atoi(e) != 0 ? 1 : 0;  // (see ug_closest)
+  if (const char *e = std::getenv("RT_HIP_XCD_FRAMES")) c->xcd_frames = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_GRID_CELLS")) c->ug_cells = std::max(0.05, std::min(64.0, std::atof(e)));
   if (const char *e = std::getenv("RT_HIP_SINGLE_CLASS"))
     c->single_class = std::max(0, std::min(kSchedClasses, std::atoi(e)));
