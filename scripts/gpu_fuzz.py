@@ -4,8 +4,13 @@ scenes -- whole or fractional shininess (40 % of scenes: int_pow and dd_pow),
 paths, render_deferred and render_deferred_walk), tiny to huge radii, mirror
 clouds, 0 to 6 lights, cameras inside spheres -- rendered on cuda:0 through
 the C-ABI at small sizes and random depths, against the oracle byte for byte
-and ray count for ray count.  Prints one line per scene and a summary; exits
-non-zero on the first mismatch.
+and ray count for ray count; every third scene is also rendered as three
+frames of one launch (rt_render_frames_async: the deferred kernel and, for
+scenes with the uniform grid, the XCD frame mapping), each frame against the
+same oracle image.  Knobs (RT_HIP_*) apply as set in the environment, e.g.
+RT_HIP_BEHIND_GRID=1 RT_HIP_BVH_ALWAYS=1 puts every scene on the uniform
+grid.  Prints one line per scene and a summary; exits non-zero on the first
+mismatch.
   python scripts/gpu_fuzz.py [SECONDS] [SEED]"""
 import os
 import random
@@ -15,6 +20,7 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "cs420-ray-tracer_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
+import torch  # noqa: E402  (torch's HIP runtime first; frame buffers)
 import orc  # noqa: E402  (the checker)
 import rt_hip  # noqa: E402
 
@@ -52,7 +58,7 @@ def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 300.0
     rng = random.Random(int(sys.argv[2]) if len(sys.argv) > 2 else 20261016)
     r = rt_hip.Renderer(0)
-    t0, k, px = time.time(), 0, 0
+    t0, k, px, frames = time.time(), 0, 0, 0
     try:
         while time.time() - t0 < budget:
             text = scene(rng)
@@ -63,6 +69,15 @@ def main():
             ref, cnt, _ = orc.OracleScene(text=text).render(W, H, D, threads=16)
             ok = bytes(rgb) == ref and (st.rays_primary, st.rays_shadow, st.rays_reflect) == (
                 cnt["primary"], cnt["shadow"], cnt["reflect"])
+            if ok and k % 3 == 2:  # three frames in one launch
+                F, stride = 3, W * H * 3
+                buf = torch.full((F * stride,), 77, dtype=torch.uint8, device="cuda:0")
+                torch.cuda.synchronize()
+                r.render_frames_async([sc.camera()] * F, W, H, D, None, buf.data_ptr(), stride)
+                r.stats()
+                host = bytes(buf.cpu().numpy())
+                ok = all(host[f * stride:(f + 1) * stride] == ref for f in range(F))
+                frames += F
             k += 1
             px += W * H
             if not ok:
@@ -76,7 +91,8 @@ def main():
                 print("%d scenes ok (%d pixels), %.0f s" % (k, px, time.time() - t0), flush=True)
     finally:
         r.close()
-    print("fuzz: %d scenes, %d pixels, all byte-identical to the oracle" % (k, px))
+    print("fuzz: %d scenes, %d pixels (+ %d frames of 3-frame launches), all byte-identical to the oracle"
+          % (k, px, frames))
     return 0
 
 

@@ -140,6 +140,51 @@ void bvh_case(int n) {
   }
 }
 
+// The uniform grid (rt_bvh.h build_ugrid): CSR, cell records and overflow
+// entries consistent, for spreads 1e-3 .. 1e6, duplicate centres, zero /
+// negative / non-finite radii and a few huge spheres.
+void ugrid_case(int n) {
+  std::vector<double> cx(n), cy(n), cz(n), r(n);
+  const double spread = std::pow(10.0, uni(-3, 6));
+  const bool flat = irand(0, 3) == 0;  // every centre in one plane
+  for (int i = 0; i < n; ++i) {
+    cx[i] = uni(-spread, spread), cy[i] = flat ? 0.0 : uni(-spread, spread), cz[i] = uni(-spread, spread);
+    r[i] = uni(-1, 1) * spread * 0.05;
+    switch (irand(0, 60)) {
+      case 0: cx[i] = std::numeric_limits<double>::quiet_NaN(); break;
+      case 1: r[i] = std::numeric_limits<double>::infinity(); break;
+      case 2: r[i] = 0; break;
+      case 3: if (i) cx[i] = cx[i - 1], cy[i] = cy[i - 1], cz[i] = cz[i - 1]; break;
+      case 4: r[i] = spread * 3; break;  // wider than the cloud: a global sphere
+    }
+  }
+  rtk::UgridHost g;
+  if (!rtk::build_ugrid(cx.data(), cy.data(), cz.data(), r.data(), n, size_t(1) << 20, g, uni(0.3, 6))) return;
+  const size_t cells = (size_t)g.nx * g.ny * g.nz;
+  CHECK(g.nx >= 1 && g.ny >= 1 && g.nz >= 1 && g.cs > 0.0f);
+  CHECK(g.start.size() == cells + 1 && g.start[0] == 0 && (size_t)g.start[cells] == g.ids.size());
+  CHECK(g.rec.size() == 4 * cells && g.rid.size() == 4 * cells && g.q.size() >= g.ids.size());
+  for (int32_t k : g.glob) CHECK(k >= 0 && k < n);
+  for (size_t c = 0; c < cells; ++c) {
+    const int32_t b = g.start[c], e = g.start[c + 1];
+    CHECK(b <= e);
+    for (int32_t k = b; k < e; ++k) CHECK(g.ids[(size_t)k] >= 0 && g.ids[(size_t)k] < n);
+    for (int j = 0; j < 4; ++j) {
+      const rtk::UgRec &q = g.rec[4 * c + j];
+      if (q.w >= 0.0f) {
+        CHECK(g.rid[4 * c + j] == g.ids[(size_t)b + j]);
+      } else if (q.w == -2.0f) {
+        int32_t k0, k1;
+        std::memcpy(&k0, &q.x, sizeof k0);
+        std::memcpy(&k1, &q.y, sizeof k1);
+        CHECK(j == 3 && k0 == b + 3 && k1 == e);
+      } else {
+        CHECK(q.w == -1.0f && j >= e - b);  // past the last entry
+      }
+    }
+  }
+}
+
 void grid_case(int n, int nl) {
   std::vector<double> cx(n), cy(n), cz(n), r(n), lx(nl), ly(nl), lz(nl);
   for (int i = 0; i < n; ++i) {
@@ -255,6 +300,7 @@ int main(int argc, char **argv) {
   for (int i = 0; i < iters; ++i) {
     parse_and_use(random_scene_text(), tmp.c_str());
     bvh_case(irand(0, 300));
+    ugrid_case(irand(0, 400));
     grid_case(irand(0, 80), irand(0, 5));
     sched_case();
     if (i % 16 == 0) {

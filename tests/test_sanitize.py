@@ -1,5 +1,5 @@
 """Host ASan + UBSan build: the C++ host side of librt_hip.so --
-scene parser and PPM writer (rt_host.cpp), BVH builders (rt_bvh.cpp), light
+scene parser and PPM writer (rt_host.cpp), BVH and uniform-grid builders (rt_bvh.cpp), light
 direction grids (rt_lightgrid.cpp), tile scheduler (rt_sched.cpp) -- plus
 ray_hybrid's CPU tile worker (rt_cpu.cpp) and the oracle (oracle/rt_oracle.c),
 compiled with -fsanitize=address,undefined -fno-sanitize-recover=all and
