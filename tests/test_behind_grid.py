@@ -207,3 +207,44 @@ def test_default_uses_behind_grid_on_large_scenes(gpu_renderer):
     assert info.behind_grid == 1 and info.behind_grid_last == 1 and info.behind_grid_entries > 0
     want = golden_rgb("synth10k_384x216_d6")
     assert bytes(rgb) == want, diff_summary(bytes(rgb), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F", [2, 3, 7])
+@pytest.mark.parametrize("W,H", [(40, 24), (97, 61)])
+def test_xcd_frame_mapping_vs_oracle(monkeypatch, F, W, H):
+    """Multi-frame launches with every frame of a tile group on one XCD
+    (RT_HIP_XCD_FRAMES=1; the grid padded to a multiple of 8 groups): group
+    counts that are not multiples of 8, odd frame counts, distinct cameras per
+    frame -- every frame equals the oracle's render of its own camera."""
+    import orc
+    import rt_hip
+    import torch
+
+    monkeypatch.setenv("RT_HIP_XCD_FRAMES", "1")
+    text = TANGENT_SCENES["reflection_ray"]
+    sc = rt_hip.Scene.parse(text)
+    r = rt_hip.Renderer(0)
+    try:
+        r.upload(sc)
+        base = sc.camera()
+        cams = []
+        for k in range(F):
+            c = rt_hip.rt_camera.from_buffer_copy(base)
+            c.position[0] = base.position[0] + 0.05 * k
+            cams.append(c)
+        stride = H * W * 3
+        buf = torch.full((F * stride,), 77, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
+        r.render_frames_async(cams, W, H, 5, None, buf.data_ptr(), stride)
+        r.stats()
+        host = buf.cpu().numpy()
+        for k in range(F):
+            one, _ = r.render(cams[k], W, H, 5)
+            got = bytes(host[k * stride:(k + 1) * stride])
+            assert got == bytes(one), ("frame", k, diff_summary(got, bytes(one)))
+            if k == 0:
+                ref, _, _ = orc.OracleScene(text=text).render(W, H, 5, threads=4)
+                assert got == ref, diff_summary(got, ref)
+    finally:
+        r.close()
