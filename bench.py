@@ -308,13 +308,18 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
             for b, m in enumerate(rt_frames.batch_sizes(n, F)):
                 render_batch(shards[b & 1][:m])
 
-    # at least one full batch: the launch shape of the timed region has run
-    # once (scratch sized, tile order built) before the clock starts
-    frames(max(warmup, F))
-    render(shards[0][0])  # one single-frame launch (untimed): the ray counts of ONE frame of this rank's shard
+    # one single-frame launch (untimed): the ray counts of ONE frame of this rank's shard
+    render(shards[0][0])
     st = r.stats()  # syncs
-    info_warm = r.info()  # the camera grid / tile order the timed launches use (built in warmup)
-    r.kernel_times()  # drop warmup launches from the history
+    # then at least one full batch: the launch shape of the timed region has
+    # run once (scratch sized, tile order and camera grid built) before the
+    # clock starts, and the warmup launches are the last GPU work before the
+    # barrier: no host work leaves the GPU idle in between (a launch after a
+    # 0.38 ms idle gap ran 2.9 % slower than the next, profiles/r3u/trace96);
+    # the timed launches' durations are read after the timed region
+    frames(max(warmup, F))
+    info_warm = r.info()  # the camera grid / tile order the timed launches use (built in warmup), host only
+    timed_launches = len(rt_frames.batch_sizes(steps, F)) if steps > 0 else 0
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
@@ -324,7 +329,8 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ktimes = r.kernel_times(max(steps, 1))  # one entry per launch (F frames each, the last maybe fewer)
+    # one entry per timed launch (F frames each, the last maybe fewer): the most recent ones
+    ktimes = r.kernel_times(max(timed_launches, 1))
     kmean = sum(ktimes) / len(ktimes)
     kframe = sum(ktimes) / max(steps, 1)  # kernel time per frame
     my_rays = st.rays
