@@ -92,6 +92,82 @@ def dist_env():
     return world, rank, local
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_gpu_count() -> int:
+    """GPUs a child process would see, counted in a separate interpreter so
+    this (launcher) process never loads the HIP runtime; device_count() does
+    not initialise the GPU on this image."""
+    out = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                         capture_output=True, text=True, timeout=600)
+    try:
+        return int(out.stdout.strip().splitlines()[-1])
+    except (IndexError, ValueError):
+        return 0
+
+
+def launch_ranks(n: int, argv: list, child: list | None = None, gpu_count: int | None = None,
+                 out=None, poll_s: float = 0.1) -> int:
+    """`bench.py --gpus N` without an external launcher: start N rank processes
+    of this script (plain child processes -- nothing here has touched the GPU,
+    and the parent never execs), one per local GPU, with the env
+    torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT).  Rank 0's
+    stdout (the JSON line) is relayed to `out`; every other rank's stdout goes
+    to stderr.  Returns 0 only if every rank exits 0; when one fails, the rest
+    are terminated and its exit code is returned.  `child` replaces the
+    command (tests use a stub); `gpu_count` skips the device probe."""
+    import threading
+
+    out = out or sys.stdout
+    if gpu_count is None:
+        gpu_count = visible_gpu_count()
+    if gpu_count < n:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, this host has {gpu_count}", file=sys.stderr)
+        return 2
+    cmd = child or [sys.executable, os.path.abspath(__file__)] + list(argv)
+    port = str(free_port())
+    procs = []
+    for i in range(n):
+        env = dict(os.environ, RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if i == 0 else sys.stderr.fileno()))
+    lines = []
+    reader = threading.Thread(target=lambda: lines.extend(procs[0].stdout.read().decode().splitlines()),
+                              daemon=True)
+    reader.start()
+    rc = 0
+    while None in [p.poll() for p in procs]:  # poll every rank each round
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(poll_s)
+    reader.join(timeout=20)
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    for ln in lines:
+        print(ln, file=out, flush=True)
+    if rc != 0:
+        print(f"bench.py: a rank failed (exit {rc}) of {n}", file=sys.stderr)
+    return rc
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -191,7 +267,7 @@ def moving_camera(rt_hip, torch, r, cam, W, H, D, rows, shard, F, launches=2):
     return {"mrays_per_s": round(st.rays * launches / el / 1e6, 1), "frames": F * launches,
             "ms_per_frame": round(el / (F * launches) * 1e3, 4),
             "kernel_ms_per_frame": round(sum(ktimes) / (F * launches), 4),
-            "camera_grid_used": bool(r.info().cam_grid_last),
+            "camera_grid_used": bool(info.cam_grid_last) if (info := info_or_none(r)) else None,
             "what": "%d launches of %d frames, every frame's camera position distinct (moved 1e-3 per frame)"
                     % (launches, F)}
 
@@ -229,6 +305,33 @@ def end_to_end(rt_hip, scene_file, W, H, D, device, runs=3):
     res.update({"kernel_ms": round(kernel_ms, 4), "rays": rays, "p3_bytes": size, "runs": runs,
                 "mrays_per_s_end_to_end": round(rays / median(parts["total_ms"]) / 1e3, 1)})
     return res
+
+
+def golden_check(torch, workload, depth, shards, launches, image, rank):
+    """Untimed, after the timed region: the bytes the timed launches produced
+    against the reference's own image of this workload (tests/golden/
+    manifest.json `sha256_rgb`, rendered by the reference's trace_ray).  At
+    N = 1 every frame of the last timed launch (still in its shard buffer);
+    for N > 1, rank 0's last reassembled frame.  None when the workload has no
+    golden (or the depth is overridden)."""
+    if not launches or depth is not None or rank != 0:
+        return None
+    path = os.path.join(REPO, "tests", "golden", "manifest.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        want = json.load(f).get(workload, {}).get("sha256_rgb")
+    if want is None:
+        return None
+    if image is not None:
+        frames = [image.cpu().numpy().tobytes()]
+    else:
+        last = shards[(len(launches) - 1) & 1][:launches[-1]].cpu().numpy()
+        frames = [last[j].tobytes() for j in range(last.shape[0])]
+    got = [hashlib.sha256(b).hexdigest() for b in frames]
+    return {"frames_checked": len(got), "frames_equal": sum(g == want for g in got),
+            "all_equal": all(g == want for g in got), "sha256_rgb": want,
+            "what": "every frame of the last timed launch" if image is None else "rank 0's last reassembled frame"}
 
 
 def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, cull=True, batch=4, dist_on=None,
@@ -318,7 +421,7 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     # 0.38 ms idle gap ran 2.9 % slower than the next, profiles/r3u/trace96);
     # the timed launches' durations are read after the timed region
     frames(max(warmup, F))
-    info_warm = r.info()  # the camera grid / tile order the timed launches use (built in warmup), host only
+    info_warm = info_or_none(r)  # the camera grid / tile order the timed launches use (built in warmup), host only
     timed_launches = len(rt_frames.batch_sizes(steps, F)) if steps > 0 else 0
     if dist_on:
         dist.barrier()
@@ -351,6 +454,8 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
         frame_rays = my_rays
         rank_kernel_ms = [round(kframe, 5)]
         seen_world = 1
+    golden = golden_check(torch, workload, depth, shards, rt_frames.batch_sizes(steps, F), image if dist_on else None,
+                          rank)
     assembled_ok = None
     if dist_on and rank == 0 and steps > 0:
         # untimed: the last frame reassembled from the gathered shards must equal
@@ -359,24 +464,25 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
         r.render_async(cam, W, H, D, rt_hip.rt_rows(1, 0, 1, H), full.data_ptr())
         torch.cuda.synchronize()
         assembled_ok = bool(torch.equal(full, image))
-    info_timed = r.info()
-    camera_grid = {"used_by_timed_launches": bool(info_timed.cam_grid_last), "cells_per_face_edge": info_timed.cam_grid_n,
-                   "builds_in_warmup": info_warm.cam_grid_builds,
-                   "builds_in_timed_region": info_timed.cam_grid_builds - info_warm.cam_grid_builds,
-                   "build_ms_total": round(info_warm.cam_grid_build_ms, 2),
-                   "tile_order_builds_in_timed_region": info_timed.tile_order_builds - info_warm.tile_order_builds,
-                   "upload_ms": round(info_timed.upload_ms, 2)}
-    # sphere grids (reflection rays' closest hit), built by rt_upload_scene (in upload_ms)
-    sphere_grids = {"grids": getattr(info_timed, "sphere_grids", None),
-                    "cells_per_face_edge": getattr(info_timed, "sphere_grid_n", None),
-                    "entries": getattr(info_timed, "sphere_grid_entries", None),
-                    "build_ms": round(getattr(info_timed, "sphere_grid_build_ms", 0.0), 2)}
-    # behind grid (the backward half of the BVH walks' closest-hit lines), built by rt_upload_scene
-    behind_grid = {"built": bool(getattr(info_timed, "behind_grid", 0)),
-                   "used_by_timed_launches": bool(getattr(info_timed, "behind_grid_last", 0)),
-                   "cells": getattr(info_timed, "behind_grid_cells", None),
-                   "entries": getattr(info_timed, "behind_grid_entries", None),
-                   "build_ms": round(getattr(info_timed, "behind_grid_build_ms", 0.0), 2)}
+    info_timed = info_or_none(r)  # None: an RT_HIP_LIB diagnostic build without rt_get_info
+    camera_grid = sphere_grids = behind_grid = None
+    if info_timed is not None and info_warm is not None:
+        camera_grid = {"used_by_timed_launches": bool(info_timed.cam_grid_last),
+                       "cells_per_face_edge": info_timed.cam_grid_n,
+                       "builds_in_warmup": info_warm.cam_grid_builds,
+                       "builds_in_timed_region": info_timed.cam_grid_builds - info_warm.cam_grid_builds,
+                       "build_ms_total": round(info_warm.cam_grid_build_ms, 2),
+                       "tile_order_builds_in_timed_region": info_timed.tile_order_builds - info_warm.tile_order_builds,
+                       "upload_ms": round(info_timed.upload_ms, 2)}
+        # sphere grids (reflection rays' closest hit), built by rt_upload_scene (in upload_ms)
+        sphere_grids = {"grids": info_timed.sphere_grids, "cells_per_face_edge": info_timed.sphere_grid_n,
+                        "entries": info_timed.sphere_grid_entries,
+                        "build_ms": round(info_timed.sphere_grid_build_ms, 2)}
+        # uniform grid (closest hits of scenes above 1,024 spheres), built by rt_upload_scene
+        behind_grid = {"built": bool(info_timed.behind_grid),
+                       "used_by_timed_launches": bool(info_timed.behind_grid_last),
+                       "cells": info_timed.behind_grid_cells, "entries": info_timed.behind_grid_entries,
+                       "build_ms": round(info_timed.behind_grid_build_ms, 2)}
     extra = {}
     if extras and not dist_on:
         extra["single_frame"] = single_frame(rt_hip, r, cam, W, H, D, rows, shards[0][0].data_ptr())
@@ -395,7 +501,7 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
         torch.cuda.synchronize()
         gather_ms = e0.elapsed_time(e1) / 5
     r.close()
-    return {"assembled_ok": assembled_ok, "scene": scene_name, "scene_file": scene_file, "W": W, "H": H, "D": D, "spheres": scene.num_spheres,
+    return {"assembled_ok": assembled_ok, "golden": golden, "scene": scene_name, "scene_file": scene_file, "W": W, "H": H, "D": D, "spheres": scene.num_spheres,
             "lights": scene.num_lights, "frame_rays": frame_rays, "rank_rays": my_rays, "elapsed": elapsed,
             "kernel_ms_mean": kmean, "kernel_ms_per_frame": kframe, "kernel_ms_per_frame_max_rank": kmax,
             "kernel_ms_min": min(ktimes), "frames_per_launch": F,
@@ -426,17 +532,30 @@ def main():
     ap.add_argument("--brute-force", action="store_true",
                     help="disable the exact per-wave sphere culling: every ray tests every sphere")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no external launcher: start the ranks here, before anything loads torch
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local = dist_env()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree",
+              file=sys.stderr)
+        sys.exit(2)
 
     # The JSON line is the only thing on stdout: RCCL's banner and any other
     # library output written to fd 1 go to stderr instead.
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
 
-    world, rank, local = dist_env()
     import torch  # loads torch's HIP runtime first; librt_hip.so binds to it
     import torch.distributed as dist
     import rt_hip
 
+    if torch.cuda.device_count() < world:
+        print(f"bench.py: WORLD_SIZE={world} needs {world} visible GPUs, rank {rank} sees "
+              f"{torch.cuda.device_count()}", file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dist_on = world > 1 or args.force_dist
     if dist_on:
@@ -457,7 +576,7 @@ def main():
             "mrays_per_s": round(a["frame_rays"] * max(args.steps // 2, 5) / a["elapsed"] / 1e6, 2),
             "ms_per_frame": round(a["elapsed"] / max(args.steps // 2, 5) * 1e3, 4),
             "kernel_ms_per_frame": round(a["kernel_ms_per_frame"], 4), "rays_per_frame": a["frame_rays"],
-            "target_mrays_per_s": 1000}
+            "target_mrays_per_s": 1000, "frame_equals_golden": a["golden"]["all_equal"] if a["golden"] else None}
         for k in ("single_frame", "moving_camera"):
             if k in a:
                 also["complex_1920x1080_d4"][k] = a[k]
@@ -512,6 +631,9 @@ def main():
                        "depth": m["D"], "spheres": m["spheres"], "lights": m["lights"],
                        "rays_per_frame": m["frame_rays"],
                        **({"assembled_frame_equals_single_gpu_render": m["assembled_ok"]} if dist_on else {}),
+                       # untimed: the timed launches' output vs the reference's image (tests/golden)
+                       "frame_equals_golden": m["golden"]["all_equal"] if m["golden"] else None,
+                       "golden_check": m["golden"],
                        "frames_per_launch": batch,
                        # the slowest rank's kernel time per frame and, for N > 1,
                        # one batch's gather to rank 0 measured alone (overlapped with rendering

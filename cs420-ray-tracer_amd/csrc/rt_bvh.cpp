@@ -309,15 +309,18 @@ bool build_ugrid(const double *cx, const double *cy, const double *cz, const dou
   }
   E += 2.0 * mg;
   int dim[3];
-  for (int it = 0; it < 2; it++) {  // at most 512 cells per axis and 16 M cells
+  constexpr double kMaxCells = 16.0 * (1 << 20);
+  bool fits = false;
+  for (int it = 0; it < 8 && !fits; it++) {  // at most 512 cells per axis and 16 M cells
     double cells = 1.0;
     for (int k = 0; k < 3; k++) {
       dim[k] = (int)std::min(512.0, std::max(1.0, std::ceil((hi[k] - lo[k]) / cs)));
       cells *= dim[k];
     }
-    if (cells <= 16.0 * (1 << 20)) break;
-    cs *= std::cbrt(cells / (16.0 * (1 << 20))) * 1.01;
+    fits = cells <= kMaxCells;
+    if (!fits) cs *= std::cbrt(cells / kMaxCells) * 1.01;
   }
+  if (!fits) return false;  // the cap still fails: no grid (the BVH walks stay)
   for (int k = 0; k < 3; k++) cs = std::max(cs, (hi[k] - lo[k]) / dim[k] * (1.0 + 1e-6));
   if (!(cs > 0.0) || !std::isfinite(cs)) return false;
   // fp32 origin and cell size, rounded so that the fp32 grid still covers [lo, hi]

@@ -690,8 +690,8 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
   // the finished pixels (flush_tile), at an LDS offset the host placed after the walk stacks
   auto pixbuf = [&]() { return (LdsU8 *)rt_dyn_lds + kernarg_late<true, offsetof(RenderArgs, pix_off)>(a.pix_off); };
 #pragma unroll
-  for (int i = 0; i < (int)(kPixbufBytes / 256); ++i)  // padding, depth 0 and deferred pixels: 0
-    reinterpret_cast<LdsU32 *>(pixbuf())[i * 64 + lane] = 0u;
+  for (int i = 0; i < (int)((kPixbufIds + 255) / 256); ++i)  // padding, depth 0 and deferred pixels: 0
+    if ((size_t)(i * 256 + lane * 4) < kPixbufIds) reinterpret_cast<LdsU32 *>(pixbuf())[i * 64 + lane] = 0u;
   const int depth = a.depth;
   const unsigned sstride = (unsigned)ca.npx;
   int qn = 0;        // queued rays q[0 .. qn), wave-uniform, < Q between passes
@@ -1711,6 +1711,11 @@ int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
       rho[(size_t)i] = (r + kEps) * (1.0 + 1e-6) + 1e-12 * mag + 1e-9 * diam;
   }
   const int N = c->sg_n_opt ? c->sg_n_opt : (n <= kSgFineSpheres ? kSgNFine : kSgN);
+  // the device indexes grid key's starts at key * (6 N^2 + 1) in 32 bits, and
+  // every sphere has its row of starts: refuse grids that would overflow it
+  // or hold more than 1 GiB of starts
+  const size_t nstart = (size_t)n * (6 * (size_t)N * N + 1);
+  if (nstart > (size_t)INT32_MAX || nstart * sizeof(int32_t) > ((size_t)1 << 30)) return RT_OK;
   std::vector<int32_t> start, ent;
   std::vector<uint8_t> ok;
   const size_t entries = build_sphere_grids(c->h_sx.data(), c->h_sy.data(), c->h_sz.data(), c->h_sr.data(), n,

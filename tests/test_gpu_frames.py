@@ -66,6 +66,26 @@ def test_frames_equal_golden(gpu_renderer, name, F):
                                                                    F * rays["reflect"])
 
 
+def test_bench_launch_shape_equals_golden(gpu_renderer):
+    """The bench's exact timed launch shapes on the metric workload (synth200
+    1920x1080 d4, static camera: the camera grid on, frames packed with no gap
+    so every tile row is dword aligned): a 32-frame launch (warmup, scratch
+    sized), then a 20-frame one (the driver's --steps 20) and another 32-frame
+    one, each frame equal to the reference's image."""
+    name = "synth200_1920x1080_d4"
+    sc, m = _load(gpu_renderer, name)
+    W, H, D = m["width"], m["height"], m["depth"]
+    want = golden_rgb(name)
+    rays = m["rays"]
+    for F in (32, 20, 32):
+        frames, st, _ = _frames(gpu_renderer, [sc.camera()] * F, W, H, D)
+        assert gpu_renderer.info().cam_grid_last == 1, "the static-view launch did not use the camera grid"
+        for f in range(F):
+            assert frames[f].tobytes() == want, f"F={F} frame {f}: {diff_summary(frames[f].tobytes(), want)}"
+        assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (F * rays["primary"], F * rays["shadow"],
+                                                                       F * rays["reflect"])
+
+
 @pytest.mark.parametrize("name", ["complex_97x61_d4", "synth200_1920x1080_d4"])
 def test_frames_distinct_cameras(gpu_renderer, name):
     sc, m = _load(gpu_renderer, name)
