@@ -31,6 +31,65 @@ __device__ __forceinline__ unsigned long long *counter_shard(unsigned long long 
   return counters + (size_t)(wg % kShards) * kShardStride;
 }
 
+// ---------------------------------------------------------------------------
+// Bounds-checked build (-DRT_CHECK: variants/librt_hip_check.so; SURVEY 5's
+// "HIP bounds-checked debug build").  RT_CK(site, i, bound) is `i` itself in
+// every other build.  In the checked build each index the kernels take out
+// of a host-built structure -- grid CSR starts and list ids, uniform-grid
+// cells, records and overflow lists, BVH node references and leaf slots, the
+// tile order, deferred-queue and reflection-stack slots, LDS queue and
+// pixel-buffer slots -- is compared with the size of what it indexes.  A
+// violation is recorded (the first one's site, index and bound, and a count)
+// and the access goes to element 0 instead, so the launch still drains and
+// rt_render_stats returns RT_ERR_CHECK naming the site, rather than the
+// queue faulting or a pixel coming out silently wrong.
+enum CkSite {
+  kCkSphere = 1,  // a sphere index from a list, grid, leaf or hit (geometry, material)
+  kCkLgStart,     // light grid: CSR start of (light, cell)
+  kCkLgId,        // light grid: list slot
+  kCkCgStart,     // camera grid: CSR start of a cell
+  kCkCgEnt,       // camera / sphere grid: list slot
+  kCkSgStart,     // sphere grid: CSR start of (grid, cell)
+  kCkSgKey,       // sphere grid: the sphere a reflection ray leaves
+  kCkUgCell,      // uniform grid: cell record
+  kCkUgOver,      // uniform grid: overflow-list slot
+  kCkBvhNode,     // BVH node reference
+  kCkBvhLeaf,     // BVH leaf slot (prefilter record, sphere id)
+  kCkTile,        // tile order slot / tile id
+  kCkDeferQ,      // deferred-queue slot
+  kCkStack,       // reflection-stack slot
+  kCkLdsQueue,    // merge_tiles' LDS ray-queue slot
+  kCkPixbuf,      // merge_tiles' LDS finished-pixel slot
+  kCkOut,         // framebuffer byte offset of a tile row or deferred pixel
+  kCkSites
+};
+#ifdef RT_CHECK
+struct CheckRec {
+  unsigned long long count, site, idx, bound;
+};
+__device__ CheckRec g_check;
+__device__ __attribute__((noinline)) void ck_fail(int site, long long i, long long bound) {
+  if (atomicAdd(&g_check.count, 1ull) == 0ull) {  // the first violation names itself
+    g_check.site = (unsigned long long)site;
+    g_check.idx = (unsigned long long)i;
+    g_check.bound = (unsigned long long)bound;
+  }
+}
+template <class I>
+__host__ __device__ __forceinline__ I ck(int site, I i, long long bound) {
+#ifdef __HIP_DEVICE_COMPILE__
+  if (__builtin_expect(!((long long)i >= 0 && (long long)i < bound), 0)) {
+    ck_fail(site, (long long)i, bound);
+    return (I)0;
+  }
+#endif
+  return i;
+}
+#define RT_CK(site, i, bound) ::rtk::ck((site), (i), (long long)(bound))
+#else
+#define RT_CK(site, i, bound) (i)
+#endif
+
 struct __attribute__((aligned(32))) SphGeo {
   double cx, cy, cz, rr;  // rr = radius*radius, rounded once on the host as sphere.h:33 does
 };
@@ -453,6 +512,7 @@ struct UgArgs {
   int on;
   int closest;  // 1: closest hits walk the grid along the whole line (grid_closest_line) instead of the BVH
   float tol;    // 1e-4 * the grid's extent: the DDA's error bound, with room to spare
+  int nq;       // overflow-list entries (RT_CHECK bound)
 };
 struct BvhArgs {
   const BvhNode *nodes;
@@ -485,6 +545,7 @@ struct BvhArgs {
   // origin are then behind_cells' part), -inf without it
   float tf_min;
   UgArgs ug;
+  int nn2, nn4, nprims;  // two-child / 4-wide nodes and leaf slots (RT_CHECK bounds)
 };
 constexpr int kOrderedStack = 24;  // pending far children; the host requires depth <= this
 
@@ -530,17 +591,13 @@ __device__ __forceinline__ void bvh_walk(const BvhArgs &bv, D3 o, D3 d, T &&tmax
   const float m = bv.margin;
   int i = 0;
   while (i < bv.nnodes) {
-    const BvhNode nd = bv.nodes[i];
+    const BvhNode nd = bv.nodes[RT_CK(kCkBvhNode, i, bv.nnodes)];
     const float ax = (nd.lo[0] - m - ox) * ix, bx = (nd.hi[0] + m - ox) * ix;
     const float ay = (nd.lo[1] - m - oy) * iy, by = (nd.hi[1] + m - oy) * iy;
     const float az = (nd.lo[2] - m - oz) * iz, bz = (nd.hi[2] + m - oz) * iz;
     const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-#ifdef RT_EXPERIMENT_FWD  // diagnostic only (not exact): skip boxes wholly behind the origin
-    const bool in = tn <= tf && tf >= -m && !((double)tn > tmax_fn());
-#else
     const bool in = tn <= tf && !((double)tn > tmax_fn());
-#endif
     work.cull += 1;
     RT_CNT(work, st[7], 1);
 #ifdef RT_STAMPS
@@ -552,12 +609,12 @@ __device__ __forceinline__ void bvh_walk(const BvhArgs &bv, D3 o, D3 d, T &&tmax
         // fp32 prefilter: the line misses the sphere grown by pmargin (fp32
         // rounding of the distance is < 6e-7 * diameter, the fp64 test can
         // only hit within 2e-8 * diameter of the surface; NaN passes)
-        const float4 q = bv.pf[first + k];
+        const float4 q = bv.pf[RT_CK(kCkBvhLeaf, first + k, bv.nprims)];
         const float wx = q.x - ox, wy = q.y - oy, wz = q.z - oz;
         const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
         const float R = q.w + bv.pmargin;
         if (cx * cx + cy * cy + cz * cz > R * R * dd) continue;
-        if (!leaf_fn((int)bv.prims[first + k])) return;
+        if (!leaf_fn((int)bv.prims[RT_CK(kCkBvhLeaf, first + k, bv.nprims)])) return;
       }
       i = nd.skip;
     } else {
@@ -597,7 +654,7 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
   for (;;) {
     work.cull += 1;
     if (ref >= 0) {
-      const BvhNode2 nd = bv.n2[ref];
+      const BvhNode2 nd = bv.n2[RT_CK(kCkBvhNode, ref, bv.nn2)];
       float t0, t1;
       const bool h0 = slab(nd.lo0, nd.hi0, t0), h1 = slab(nd.lo1, nd.hi1, t1);
       if (h0 && h1) {
@@ -614,12 +671,12 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
     } else {
       const int leaf = -(ref + 1), first = leaf >> 4, cnt = leaf & 15;
       for (int k = 0; k < cnt; ++k) {
-        const float4 q = bv.pf[first + k];  // fp32 prefilter, as bvh_walk
+        const float4 q = bv.pf[RT_CK(kCkBvhLeaf, first + k, bv.nprims)];  // fp32 prefilter, as bvh_walk
         const float wx = q.x - ox, wy = q.y - oy, wz = q.z - oz;
         const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
         const float R = q.w + bv.pmargin;
         if (cx * cx + cy * cy + cz * cz > R * R * dd) continue;
-        if (!leaf_fn((int)bv.prims[first + k])) return;
+        if (!leaf_fn((int)bv.prims[RT_CK(kCkBvhLeaf, first + k, bv.nprims)])) return;
       }
     }
     bool more = false;
@@ -681,7 +738,7 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
   for (;;) {
     work.cull += 1;
     if (ref >= 0) {
-      const BvhNode4 *nd = bv.n4 + ref;
+      const BvhNode4 *nd = bv.n4 + RT_CK(kCkBvhNode, ref, bv.nn4);
       float t[4];
       int r[4];
       int hits = 0;
@@ -719,12 +776,12 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
     } else {
       const int leaf = -(ref + 1), first = leaf >> 4, cnt = leaf & 15;
       for (int k = 0; k < cnt; ++k) {
-        const float4 q = bv.pf[first + k];  // fp32 prefilter, as bvh_walk
+        const float4 q = bv.pf[RT_CK(kCkBvhLeaf, first + k, bv.nprims)];  // fp32 prefilter, as bvh_walk
         const float wx = q.x - ox, wy = q.y - oy, wz = q.z - oz;
         const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
         const float R = q.w + bv.pmargin;
         if (cx * cx + cy * cy + cz * cz > R * R * dd) continue;
-        if (!leaf_fn((int)bv.prims[first + k])) return;
+        if (!leaf_fn((int)bv.prims[RT_CK(kCkBvhLeaf, first + k, bv.nprims)])) return;
       }
       tmf = tmax_f();
     }
@@ -782,7 +839,7 @@ __device__ __forceinline__ bool walk4_step(const BvhArgs &bv, const Walk4Ray &r,
   LdsU64 *st = ordered_stack_lds(bv);
   work.cull += 1;
   if (ref >= 0) {
-    const BvhNode4 *nd = bv.n4 + ref;
+    const BvhNode4 *nd = bv.n4 + RT_CK(kCkBvhNode, ref, bv.nn4);
     float t[4];
     int c[4];
     int hits = 0;
@@ -819,12 +876,12 @@ __device__ __forceinline__ bool walk4_step(const BvhArgs &bv, const Walk4Ray &r,
   } else {
     const int leaf = -(ref + 1), first = leaf >> 4, cnt = leaf & 15;
     for (int k = 0; k < cnt; ++k) {
-      const float4 q = bv.pf[first + k];  // fp32 prefilter, as bvh_walk
+      const float4 q = bv.pf[RT_CK(kCkBvhLeaf, first + k, bv.nprims)];  // fp32 prefilter, as bvh_walk
       const float wx = q.x - r.ox, wy = q.y - r.oy, wz = q.z - r.oz;
       const float cx = wy * r.dz - wz * r.dy, cy = wz * r.dx - wx * r.dz, cz = wx * r.dy - wy * r.dx;
       const float R = q.w + bv.pmargin;
       if (cx * cx + cy * cy + cz * cz > R * R * r.dd) continue;
-      leaf_fn((int)bv.prims[first + k]);
+      leaf_fn((int)bv.prims[RT_CK(kCkBvhLeaf, first + k, bv.nprims)]);
     }
     tmf = tmf_fn();
   }
@@ -951,7 +1008,7 @@ __host__ __device__ __forceinline__ void grid_line(const BvhArgs &bv, D3 o, D3 d
     return (iv == __builtin_inff() || iv == -__builtin_inff()) ? __builtin_inff()
                                                               : ((float)(c + (st > 0 ? 1 : 0)) * cs - p) * iv;
   };
-  int ci = (c2 * ug.ny + c1) * ug.nx + c0;
+  int ci = RT_CK(kCkUgCell, (c2 * ug.ny + c1) * ug.nx + c0, ug.nx * ug.ny * ug.nz);
   float4 r0 = ug.rec[4 * ci], r1 = ug.rec[4 * ci + 1], r2 = ug.rec[4 * ci + 2], r3 = ug.rec[4 * ci + 3];
   int guard = ug.nx + ug.ny + ug.nz + 2;  // every step leaves the cell along one axis for good
   int last = -1;                          // the sphere tested last (spheres span neighbouring cells)
@@ -979,7 +1036,7 @@ __host__ __device__ __forceinline__ void grid_line(const BvhArgs &bv, D3 o, D3 d
     const int cur = ci;
     float4 n0 = r0, n1 = r1, n2 = r2, n3 = r3;
     if (more) {
-      ci = (c2 * ug.ny + c1) * ug.nx + c0;
+      ci = RT_CK(kCkUgCell, (c2 * ug.ny + c1) * ug.nx + c0, ug.nx * ug.ny * ug.nz);
       n0 = ug.rec[4 * ci];
       n1 = ug.rec[4 * ci + 1];
       n2 = ug.rec[4 * ci + 2];
@@ -1008,7 +1065,8 @@ __host__ __device__ __forceinline__ void grid_line(const BvhArgs &bv, D3 o, D3 d
         return true;
       }
       if (q.w == -2.0f)  // the cell continues in the overflow list
-        for (int k = __builtin_bit_cast(int, q.x), ke = __builtin_bit_cast(int, q.y); k < ke; ++k) one(ug.q[k], k, ug.ids);
+        for (int k = __builtin_bit_cast(int, q.x), ke = __builtin_bit_cast(int, q.y); k < ke; ++k)
+          one(ug.q[RT_CK(kCkUgOver, k, ug.nq)], RT_CK(kCkUgOver, k, ug.nq), ug.ids);
       return false;
     };
     if (slot(r0, 0) && slot(r1, 1) && slot(r2, 2)) slot(r3, 3);
@@ -1141,7 +1199,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
   // division.
   auto test = [&](int i) {
     double num;
-    const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+    const int r = fast ? intersect_num(g[RT_CK(kCkSphere, i, n)], o, d, a4, num) : 2;
     if (r == 1) {
       if (num < bn || i < bi) {
         const double t = num / a2;
@@ -1286,7 +1344,7 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
   bool occ = false;
   auto test = [&](int i) {
     double num;
-    const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
+    const int r = fast ? intersect_num(g[RT_CK(kCkSphere, i, n)], o, d, a4, num) : 2;
     if (r == 1) {
       if (num < qlo) occ = true;
       else if (!(num > qhi)) {
@@ -1376,6 +1434,7 @@ struct LgArgs {
   int N;
   int on;          // 0: shadow rays use sweep_shadow
   double max_off;  // largest distance of a ray's line from its light the grid margins cover
+  long long nstart, nids;  // CSR starts and list ids (RT_CHECK bounds)
 };
 
 // The cell list a shadow query of light l from point hp will test: the cell
@@ -1422,15 +1481,16 @@ __device__ __forceinline__ LgRange lg_range(const LgArgs &lg, int l, D3 hp, D3 l
       r.cb = -1;
     } else {
       const int32_t *st = lg.start + (size_t)l * (size_t)(cells + 2);
-      r.cb = st[c];
-      r.ce = st[c + 1];
+      const int cc = RT_CK(kCkLgStart, c, lg.nstart - 1 - (long long)l * (cells + 2));
+      r.cb = st[cc];
+      r.ce = st[cc + 1];
     }
   }
   return r;
 }
 
 __device__ __forceinline__ int lg_first(const LgArgs &lg, LgRange r) {
-  return (r.cb >= 0 && r.ce > r.cb) ? lg.ids[r.cb] : 0;
+  return (r.cb >= 0 && r.ce > r.cb) ? lg.ids[RT_CK(kCkLgId, r.cb, lg.nids)] : 0;
 }
 
 // `pre` >= 0: the sphere the shaded point lies on (see below).
@@ -1446,11 +1506,7 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
   bool occ = false;
   auto test = [&](int i) {
     double num;
-    #if RT_ABL == 8  // ablation (wrong images): the shadow tests read one fixed sphere (no gathers)
-    const int r = fast ? intersect_num(g[0], o, d, a4, num) : 2;
-#else
-    const int r = fast ? intersect_num(g[i], o, d, a4, num) : 2;
-#endif
+    const int r = fast ? intersect_num(g[RT_CK(kCkSphere, i, n)], o, d, a4, num) : 2;
     if (r == 1) {
       if (num < qlo) occ = true;
       else if (!(num > qhi)) {
@@ -1481,7 +1537,7 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
   //    reference keeps, sphere.h:43-47) and every other case take the test.
   bool self_miss = false;
   if (act && pre >= 0 && fast) {
-    const SphGeo s = g[pre];
+    const SphGeo s = g[RT_CK(kCkSphere, pre, n)];
     const double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
     const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.rr;
     if (c < 0.0) {
@@ -1498,30 +1554,23 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
     const int32_t *st = lg.start + (size_t)l * (size_t)(cells + 2);
     // The line o + t d passes (up to rounding) through the light; the grid's
     // margins assume it does within max_off -- checked here, per ray.
-#if RT_ABL == 5  // ablation (diagnostic builds only, not exact): no per-ray line check
-    const double off = 0.0;
-#else
     const D3 w = sub(lp, o);
     const double off = __builtin_fabs(w.y * d.z - w.z * d.y) + __builtin_fabs(w.z * d.x - w.x * d.z) +
                        __builtin_fabs(w.x * d.y - w.y * d.x);
-#endif
-#if RT_ABL == 6  // ablation (wrong images): shadow rays built and checked, lists not tested
-    if (off > 1e300) occ = true;
-    return act && occ;
-#endif
     // the cell's list (first id prefetched), then the global list; a lane
     // whose line cannot use the grid tests every sphere (ids 0 .. n-1) in the
     // same loop
     const bool all = !(off <= lg.max_off) || cell.cb < 0;
-    const int gb = st[cells], ge = st[cells + 1];
+    const int cl = RT_CK(kCkLgStart, cells, lg.nstart - 1 - (long long)l * (cells + 2));
+    const int gb = st[cl], ge = st[cl + 1];
     const int len1 = all ? n : cell.ce - cell.cb, len = all ? n : len1 + (ge - gb);
     int k = 0;
     int nxt = all ? 0 : id0;
-    if (!all && len1 == 0 && len > 0) nxt = lg.ids[gb];
+    if (!all && len1 == 0 && len > 0) nxt = lg.ids[RT_CK(kCkLgId, gb, lg.nids)];
     while (k < len && !occ) {
       const int i = nxt;
       ++k;
-      if (k < len) nxt = all ? k : lg.ids[k < len1 ? cell.cb + k : gb + (k - len1)];
+      if (k < len) nxt = all ? k : lg.ids[RT_CK(kCkLgId, k < len1 ? cell.cb + k : gb + (k - len1), lg.nids)];
       if (i != skip) {
         work.exact += 1;
         test(i);
@@ -1544,13 +1593,15 @@ struct CgArgs {
   const int2 *ent;       // (sphere, tlo bits)
   int N;
   int on;  // the launch's frames all share the grid's camera position
+  long long nent;  // list entries (RT_CHECK bound)
 };
 // The scan of one grid's cell list for the closest hit; this lane's grid
 // starts at start + sbase (camera grid: sbase = 0; sphere grids: the grid of
 // the sphere the ray leaves).
 __device__ __forceinline__ int grid_closest(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d,
                                             const int32_t *__restrict__ start, const int2 *__restrict__ ent, int N,
-                                            int sbase, double &best_t, Work &work) {
+                                            int sbase, long long nstart, long long nent, double &best_t,
+                                            Work &work) {
   const double a = dot(d, d);
   const double a4 = 4.0 * a, a2 = 2.0 * a;
   double bt = kInf, bn = __builtin_inf();
@@ -1564,26 +1615,27 @@ __device__ __forceinline__ int grid_closest(const SphGeo *__restrict__ g, int n,
       all = true;
       len = n;
     } else {
-      cb = start[sbase + c];
-      len = start[sbase + c + 1] - cb;
+      const int cc = RT_CK(kCkCgStart, c, nstart - 1 - sbase);
+      cb = start[sbase + cc];
+      len = start[sbase + cc + 1] - cb;
     }
   }
   int k = 0;
-  int2 e = (len > 0 && !all) ? ent[cb] : make_int2(0, (int)0xff800000u);  // -inf
+  int2 e = (len > 0 && !all) ? ent[RT_CK(kCkCgEnt, cb, nent)] : make_int2(0, (int)0xff800000u);  // -inf
   while (k < len) {
     const int i = all ? k : e.x;
     if ((double)__int_as_float(e.y) > bt) break;
     ++k;
-    if (k < len && !all) e = ent[cb + k];  // the next entry, loaded during this test
+    if (k < len && !all) e = ent[RT_CK(kCkCgEnt, cb + k, nent)];  // the next entry, loaded during this test
     work.exact += 1;
-    closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi);
+    closest_test(g[RT_CK(kCkSphere, i, n)], i, o, d, a4, a2, fast, bt, bn, bi);
   }
   best_t = bt;
   return bi;
 }
 __device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d,
                                            const CgArgs &cg, double &best_t, Work &work) {
-  return grid_closest(g, n, act, o, d, cg.start, cg.ent, cg.N, 0, best_t, work);
+  return grid_closest(g, n, act, o, d, cg.start, cg.ent, cg.N, 0, 6LL * cg.N * cg.N + 1, cg.nent, best_t, work);
 }
 
 // Closest hit of reflection rays through the sphere grids (rt_lightgrid.h
@@ -1598,12 +1650,15 @@ struct SgArgs {
   const double *rho2;    // [n] squared origin-ball radius, < 0: no grid
   int N;
   int on;
+  long long nstart, nent;  // CSR starts and list entries (RT_CHECK bounds)
+  int nsph;                // spheres (RT_CHECK bound of the grid key)
 };
 __device__ __forceinline__ bool sg_usable(const SphGeo *__restrict__ g, const SgArgs &sg, bool act, D3 o, int key) {
   if (!act || key < 0) return false;
-  const SphGeo s = g[key];
+  const int k = RT_CK(kCkSgKey, key, sg.nsph);
+  const SphGeo s = g[k];
   const double ox = o.x - s.cx, oy = o.y - s.cy, oz = o.z - s.cz;
-  return (ox * ox + oy * oy) + oz * oz <= sg.rho2[key];
+  return (ox * ox + oy * oy) + oz * oz <= sg.rho2[k];
 }
 
 struct Cam {

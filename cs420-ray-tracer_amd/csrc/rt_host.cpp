@@ -138,6 +138,7 @@ const char *rt_error_string(int status) {
     case RT_ERR_NO_SCENE: return "no scene uploaded";
     case RT_ERR_IO: return "I/O error";
     case RT_ERR_DEPTH: return "depth exceeds RT_MAX_DEPTH";
+    case RT_ERR_CHECK: return "device index out of range (bounds-checked build)";
     default: return "unknown status";
   }
 }

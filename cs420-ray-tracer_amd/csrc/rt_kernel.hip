@@ -27,12 +27,6 @@
 
 #pragma clang fp contract(off)
 
-// RT_ABL=k: ablation builds for cost attribution only (scripts/build_rev.sh
-// ... -DRT_ABL=k); they render WRONG images and are never the product.
-#ifndef RT_ABL
-#define RT_ABL 0
-#endif
-
 #include "rt_device.h"
 #include "rt_sched.h"
 
@@ -167,7 +161,7 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
     color = add(scale(mk(1.0, 1.0, 1.0), 1.0 - st), scale(mk(0.5, 0.7, 1.0), st));
     outcome = kEnded;
   }
-  const int hi = hit ? bi : 0;
+  const int hi = RT_CK(kCkSphere, hit ? bi : 0, n > 0 ? n : 1);
   const D3 hp = add(o, scale(d, bt));                            // main.cpp:32
   D3 col;
   {
@@ -188,11 +182,7 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
         const LgArgs &lg0 = kernarg_late<kArgMem, offsetof(RenderArgs, lg)>(lg_arg);
         if (lg0.on && nl > 0) next = lg_range(lg0, 0, hp, mk(slight[0].px, slight[0].py, slight[0].pz), hit);
       }
-#if RT_ABL == 1  // ablation (diagnostic builds only, wrong images): no lights
-      for (int l = 0; l < 0; ++l) {
-#else
       for (int l = 0; l < nl; ++l) {
-#endif
         const LgArgs &lg = kernarg_late<kArgMem, offsetof(RenderArgs, lg)>(lg_arg);
         RT_T0(t_setup);
         // this light's first list id, and the next light's cell range, are
@@ -205,32 +195,14 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
         const D3 to_light = sub(lp, hp);
         const double dist = length(to_light);
         const D3 ldir = normalized(to_light);
-#if RT_ABL == 7  // ablation (wrong images): shadow queries of camera-ray hits only
-        const bool need = hit && key < 0;
-#else
         const bool need = hit;
-#endif
         RT_ACC(work, 3, t_setup);
         RT_T0(t_sh);
         bool occ = false;
-#if RT_ABL == 2  // ablation: no shadow queries
-        if (false) {
-#else
         if (__ballot(need)) {
-#endif
-#if RT_ABL == 4  // ablation: shadow rays without the second normalisation / offset
-          const D3 so = hp, sd = ldir;
-#elif RT_ABL == 13  // ablation (not exact): shadow rays without the second normalisation
-          const D3 so = add(hp, scale(ldir, kEps)), sd = ldir;
-#else
           const D3 so = add(hp, scale(ldir, kEps)), sd = renormalized(ldir);
-#endif
           if constexpr (kFast) {
             occ = shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi);
-#if RT_ABL == 21  // ablation (diagnostic builds only): every shadow query done twice
-            const bool occ2 = shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi);
-            asm volatile("" ::"v"(occ2));
-#endif
           }
           else
             occ = lg.on ? shadow_cells(g, n, need, so, sd, lp, dist, lg, l, cell, id0, work, hi)
@@ -248,13 +220,8 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
           // pow(+0, y > 0) is +0 exactly (C99 F.10.4.4), so most lanes skip ocml's pow.
           double spec = 0.0;
           int ipow = 0;
-#if RT_ABL == 3  // ablation: no pow
-          spec = rdv;
-          (void)ipow;
-#else
           if (!(rdv == 0.0 && m.shin > 0.0))
             spec = int_pow_ok(rdv, m.shin, ipow) ? int_pow(rdv, ipow) : pow_call(rdv, m.shin);
-#endif
           const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
           col = add(add(specular, diffuse), col);                  // scene.h:117
         }
@@ -301,13 +268,6 @@ __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const d
   if constexpr (kFast && kArgMem) {
     if (cam_pass) {
       bi = cam_closest(g, n, alive, o, d, kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{}), bt, work);
-#if RT_ABL == 23  // ablation (diagnostic builds only): the camera rays' closest hit done twice
-      {
-        double bt2 = kInf;
-        const int bi2 = cam_closest(g, n, alive, o, d, kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{}), bt2, work);
-        asm volatile("" ::"v"(bi2), "v"(bt2));
-      }
-#endif
       swept = true;
     } else if (kernarg_late<true, offsetof(RenderArgs, sg)>(SgArgs{}).on) {
       // reflection rays through the sphere grid of the sphere they leave; the
@@ -319,14 +279,8 @@ __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const d
       }
       if (__ballot(grid)) {
         const SgArgs &sg = kernarg_late<true, offsetof(RenderArgs, sg)>(SgArgs{});
-        bi = grid_closest(g, n, grid, o, d, sg.start, sg.ent, sg.N, grid ? key * (6 * sg.N * sg.N + 1) : 0, bt,
-                          work);
-#if RT_ABL == 20
-        double bt2 = kInf;
-        const int bi2 = grid_closest(g, n, grid, o, d, sg.start, sg.ent, sg.N, grid ? key * (6 * sg.N * sg.N + 1) : 0,
-                                     bt2, work);
-        asm volatile("" ::"v"(bi2), "v"(bt2));
-#endif
+        bi = grid_closest(g, n, grid, o, d, sg.start, sg.ent, sg.N, grid ? key * (6 * sg.N * sg.N + 1) : 0, sg.nstart,
+                          sg.nent, bt, work);
       }
       const bool rest = alive && !grid;
       if (__ballot(rest)) {
@@ -344,14 +298,6 @@ __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const d
   if (!swept)
     bi = sweep_closest<kCull, kFast>(g, rad, n, alive, o, d, key, kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv),
                                      bt, work);
-#if RT_ABL == 20  // ablation (diagnostic builds only): the reflection rays' closest-hit search done twice
-  if (!swept) {
-    double bt2 = kInf;
-    const int bi2 = sweep_closest<kCull, kFast>(g, rad, n, alive, o, d, key,
-                                                kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt2, work);
-    asm volatile("" ::"v"(bi2), "v"(bt2));
-  }
-#endif
   RT_ACC(work, 8, t_cl);
   bt_out = bt;
   return bi;
@@ -398,7 +344,8 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
                            color, refl, no, nd, nkey);
     if (alive) {
       if (outcome == kSpawned) {
-        sbase[sidx + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
+        sbase[RT_CK(kCkStack, sidx + (unsigned)lev * sstride, (long long)(depth - 1) * sstride)] =
+            StackEnt{color.x, color.y, color.z, refl};
         ++lev;
         o = no;
         d = nd;
@@ -415,7 +362,7 @@ __device__ __forceinline__ D3 trace_wave(const SphGeo *__restrict__ g, const dou
   if (kPark && traced) res = park[threadIdx.x & 63];
   while (lev > 0) {  // unwind: shade*(1-refl) + reflected*refl, innermost first
     --lev;
-    const StackEnt e = sbase[sidx + (unsigned)lev * sstride];
+    const StackEnt e = sbase[RT_CK(kCkStack, sidx + (unsigned)lev * sstride, (long long)(depth - 1) * sstride)];
     res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
   }
   return res;
@@ -592,9 +539,6 @@ __device__ __forceinline__ unsigned pack_px(D3 c, unsigned &c_neg) {
 // neighbours in those dwords may be other deferred pixels being OR-ed at the
 // same time: a dword atomic OR per covered dword, no byte stores.
 __device__ __forceinline__ void or_px(uint8_t *out, unsigned pix, unsigned v) {
-#if RT_ABL == 11  // ablation (wrong images): no pixel stores
-  if (v != 0x5a5a5a5au) return;
-#endif
   const uintptr_t a = reinterpret_cast<uintptr_t>(out) + (uintptr_t)pix * 3;
   unsigned *d = reinterpret_cast<unsigned *>(a & ~(uintptr_t)3);
   const unsigned sh = (unsigned)(a & 3) * 8;
@@ -652,9 +596,6 @@ __device__ __forceinline__ void flush_tile(const RenderArgs &a, int tile, int fr
   if (rows_dword && x0 + 8 <= W && ty * 8 + 8 <= rows.count) {  // wave-uniform: the usual case
     if (lane < 48) {  // lane: row lane / 6, dword lane % 6 = LDS dword lane
       const unsigned v = reinterpret_cast<const LdsU32 *>(pb)[lane];
-#if RT_ABL == 11  // ablation (wrong images): no pixel stores
-      if (v == 0x5a5a5a5au)
-#endif
       *reinterpret_cast<unsigned *>(row_at(0) + (unsigned)(lane / 6) * (unsigned)W * 3u +
                                     4u * (unsigned)(lane - 6 * (lane / 6))) = v;
     }
@@ -707,7 +648,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     const int take = (64 - __popcll(busy)) < qn ? (64 - __popcll(busy)) : qn;
     const int r = (int)__popcll(~busy & lt);
     if (!act && r < take) {
-      const QRay &e = q[qn - 1 - r];
+      const QRay &e = q[RT_CK(kCkLdsQueue, qn - 1 - r, Q)];
       o = mk(e.ox, e.oy, e.oz);
       d = mk(e.dx, e.dy, e.dz);
       key = e.key;
@@ -732,7 +673,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
       if (next < nt) {  // camera rays of the next tile: camera.h:17-25, main.cpp:151-154 (as trace_tile)
         const int *perm = kernarg_late<true, offsetof(RenderArgs, perm)>(a.perm);
         const int slot = base + next;
-        const int tile = perm ? perm[slot] : slot;
+        const int tile = RT_CK(kCkTile, perm ? perm[RT_CK(kCkTile, slot, ntiles)] : slot, ntiles);
         const int ntx = kernarg_late<true, offsetof(RenderArgs, ntx)>(a.ntx);
         const int tx = tile % ntx, ty = tile / ntx;
         const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
@@ -751,11 +692,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         const double su = ((u - 0.5) * cam.scale) * 1.0, sv = (v - 0.5) * cam.scale;
         const D3 dir = add(add(mk(cam.fx, cam.fy, cam.fz), scale(mk(cam.rx, cam.ry, cam.rz), su)),
                            scale(mk(cam.ux, cam.uy, cam.uz), sv));
-#if RT_ABL == 13
-        d = normalized(dir);
-#else
         d = renormalized(normalized(dir));
-#endif
         o = mk(cam.px, cam.py, cam.pz);
         pix = (unsigned)(k * W + x);
         lidx = next * 64 + lane;
@@ -798,11 +735,8 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     bool defer = false;
     if (act) {
       if (outcome == kSpawned) {
-#if RT_ABL == 10  // ablation (wrong images): no reflection stack traffic
-        if (color.x > 1e300) ca.gstack[sidx] = StackEnt{color.x, color.y, color.z, refl};
-#else
-        ca.gstack[sidx + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
-#endif
+        ca.gstack[RT_CK(kCkStack, sidx + (unsigned)lev * sstride, (long long)(depth - 1) * sstride)] =
+            StackEnt{color.x, color.y, color.z, refl};
         ++lev;
         o = no;
         d = nd;
@@ -812,17 +746,14 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         defer = lev >= kernarg_late<true, offsetof(RenderArgs, defer_level)>(a.defer_level);
       } else {  // the chain ends: unwind its pixel's stack and store it
         D3 res = color;
-#if RT_ABL == 10
-        lev = 0;
-#endif
         while (lev > 0) {
           --lev;
-          const StackEnt e = ca.gstack[sidx + (unsigned)lev * sstride];
+          const StackEnt e = ca.gstack[RT_CK(kCkStack, sidx + (unsigned)lev * sstride, (long long)(depth - 1) * sstride)];
           res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
         }
         {
           const unsigned v = pack_px(res, c_neg);
-          LdsU8 *p = pixbuf() + 3 * lidx;
+          LdsU8 *p = pixbuf() + 3 * RT_CK(kCkPixbuf, lidx, kMergeTiles * 64);
           p[0] = (unsigned char)v;
           p[1] = (unsigned char)(v >> 8);
           p[2] = (unsigned char)(v >> 16);
@@ -845,7 +776,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         if (defer && slot < (unsigned long long)cap) {
           QRay *dq = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq);
           const unsigned wg = blockIdx.x;
-          dq[(size_t)(wg % kShards) * (size_t)cap + slot] =
+          dq[RT_CK(kCkDeferQ, (size_t)(wg % kShards) * (size_t)cap + slot, (long long)kShards * cap)] =
               QRay{o.x, o.y, o.z, d.x, d.y, d.z, lev, dleft, key, (int)sidx};
           act = false;
         }
@@ -855,7 +786,8 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     if (tile_pass && next < nt && __popcll(busy) + qn < Q) {
       // this tile's reflection rays wait for the next tiles' (queue < Q entries)
       if (act)
-        q[qn + (int)__popcll(busy & lt)] = QRay{o.x, o.y, o.z, d.x, d.y, d.z, lidx, dleft, key, (int)pix};
+        q[RT_CK(kCkLdsQueue, qn + (int)__popcll(busy & lt), Q)] =
+            QRay{o.x, o.y, o.z, d.x, d.y, d.z, lidx, dleft, key, (int)pix};
       qn += __popcll(busy);
       act = false;
     } else if (qn > 0 && busy != ~0ull) {
@@ -877,10 +809,9 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
       if (off != 0xFFFFFFFFu) {
         if (lane < 48) {
           const unsigned v = reinterpret_cast<const LdsU32 *>(pixbuf() + 192 * t)[lane];
-#if RT_ABL == 11  // ablation (wrong images): no pixel stores
-          if (v == 0x5a5a5a5au)
-#endif
-          *reinterpret_cast<unsigned *>(out + off + roff) = v;
+          *reinterpret_cast<unsigned *>(
+              out + RT_CK(kCkOut, (size_t)off + roff,
+                          (long long)(kernarg_late<true, offsetof(RenderArgs, rows)>(a.rows).count) * W * 3 - 3)) = v;
         }
       } else {
         flush_tile(a, (int)__builtin_amdgcn_readfirstlane(ids[2 * t]), frame, pixbuf() + 192 * t);
@@ -993,7 +924,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
   } else {
     if (a.perm) {
       if (slot >= a.nslots) return;
-      tile = a.perm[slot];  // heaviest predicted tiles first, or a batch's listed blocks
+      tile = a.perm[RT_CK(kCkTile, slot, a.nslots)];  // heaviest predicted tiles first, or a batch's listed blocks
     }
     if (tile >= a.ntiles) return;  // workgroup-uniform, before any barrier
   }
@@ -1091,7 +1022,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
       const unsigned long long i = base + (unsigned long long)__popcll(idle & lt);
       more = base + (unsigned long long)__popcll(idle) < n_dq;
       if (!act && i < n_dq) {
-        const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[(size_t)shard * (size_t)cap + i];
+        const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[RT_CK(kCkDeferQ, (size_t)shard * (size_t)cap + i, (long long)kShards * cap)];
         o = mk(e.ox, e.oy, e.oz);
         d = mk(e.dx, e.dy, e.dz);
         lev = e.orig;
@@ -1106,26 +1037,13 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
       int outcome = 0, nkey = 0;
       D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
       double refl = 0.0;
-#if RT_ABL == 12  // ablation (wrong images): deferred rays find their closest hit and end (no shading)
-      {
-        double bt = 0.0;
-        const int bi = sweep_closest<kCull, kFast>(a.geo, a.radius, a.n, act,  o, d, key,
-                                                   kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv), bt, work);
-        outcome = kEnded;
-        color = mk(bt, (double)bi, 0.0);
-      }
-#else
       bounce<kCull, true, kFast>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft,
                           work, c_shadow, outcome, color, refl, no, nd, nkey);
-#endif
       if (act) {
         StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, gstack)>(a.gstack);
         if (outcome == kSpawned) {
-#if RT_ABL == 10
-          if (color.x > 1e300) gs[pixg] = StackEnt{color.x, color.y, color.z, refl};
-#else
-          gs[pixg + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
-#endif
+          gs[RT_CK(kCkStack, pixg + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)] =
+              StackEnt{color.x, color.y, color.z, refl};
           ++lev;
           o = no;
           d = nd;
@@ -1134,17 +1052,14 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
           ++c_reflect;
         } else {
           D3 res = color;
-#if RT_ABL == 10
-          lev = 0;
-#endif
           while (lev > 0) {  // main.cpp:54, innermost first
             --lev;
-            const StackEnt e = gs[pixg + (unsigned)lev * sstride];
+            const StackEnt e = gs[RT_CK(kCkStack, pixg + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)];
             res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
           }
           const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
           const unsigned f = pixg / npx_frame;
-          or_px(static_cast<uint8_t *>(od.ptr) + (size_t)f * (size_t)od.fstride, pixg - f * npx_frame,
+          or_px(static_cast<uint8_t *>(od.ptr) + (size_t)RT_CK(kCkOut, f, a.frames) * (size_t)od.fstride, pixg - f * npx_frame,
                 pack_px(res, c_neg));
           act = false;
         }
@@ -1213,7 +1128,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
         const unsigned long long i = base + (unsigned long long)__popcll(idle & lt);
         more = base + (unsigned long long)__popcll(idle) < n_dq;
         if (!act && i < n_dq) {
-          const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[(size_t)shard * (size_t)cap + i];
+          const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[RT_CK(kCkDeferQ, (size_t)shard * (size_t)cap + i, (long long)kShards * cap)];
           o = mk(e.ox, e.oy, e.oz);
           d = mk(e.dx, e.dy, e.dz);
           lev = e.orig;
@@ -1239,7 +1154,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
         if (walking) {
           auto leaf = [&](int i) {
             work.exact += 1;
-            closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi);
+            closest_test(g[RT_CK(kCkSphere, i, a.n)], i, o, d, a4, a2, fast, bt, bn, bi);
           };
           walking = walk4_step(bv, r, [&] { return prune(bv); }, work, leaf, ref, sp, tmf);
         }
@@ -1254,7 +1169,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
           const double a4 = 4.0 * dot(d, d), a2 = 0.5 * a4;
           const bool fast = a2_ok(a2);
           const SphGeo *__restrict__ g = a.geo;
-          behind_cells(bv, o, d, work, [&](int i) { closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi); });
+          behind_cells(bv, o, d, work, [&](int i) { closest_test(g[RT_CK(kCkSphere, i, a.n)], i, o, d, a4, a2, fast, bt, bn, bi); });
         }
       }
       int outcome = 0, nkey = 0;
@@ -1266,7 +1181,8 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
       if (ready) {
         StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, gstack)>(a.gstack);
         if (outcome == kSpawned) {
-          gs[pixg + (unsigned)lev * sstride] = StackEnt{color.x, color.y, color.z, refl};
+          gs[RT_CK(kCkStack, pixg + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)] =
+              StackEnt{color.x, color.y, color.z, refl};
           ++lev;
           o = no;
           d = nd;
@@ -1278,12 +1194,12 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
           D3 res = color;
           while (lev > 0) {  // main.cpp:54, innermost first
             --lev;
-            const StackEnt e = gs[pixg + (unsigned)lev * sstride];
+            const StackEnt e = gs[RT_CK(kCkStack, pixg + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)];
             res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
           }
           const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
           const unsigned f = pixg / npx_frame;
-          or_px(static_cast<uint8_t *>(od.ptr) + (size_t)f * (size_t)od.fstride, pixg - f * npx_frame,
+          or_px(static_cast<uint8_t *>(od.ptr) + (size_t)RT_CK(kCkOut, f, a.frames) * (size_t)od.fstride, pixg - f * npx_frame,
                 pack_px(res, c_neg));
           act = false;
         }
@@ -1346,9 +1262,11 @@ struct rt_ctx {
   BvhNode4 *d_bvh4 = nullptr;  // 4-wide nodes for the ordered walk (RT_HIP_BVH4=0: two-child walk)
   int bvh4_root = -1, bvh4_stack = 0, bvh_wide = 1;
   int bvh_nodes = 0;
+  int bvh2_nodes = 0, bvh4_nodes = 0, bvh_prims = 0;  // sizes the RT_CHECK build checks node / leaf indices against
   // per-light direction grids for shadow rays (rt_lightgrid.h), built at upload
   int32_t *d_lg_start = nullptr, *d_lg_ids = nullptr;
   int lg_n = 128, lg_on = 1;  // lg_n: the grid of the uploaded scene
+  long long lg_nstart = 0, lg_nids = 0;
   int lg_n_opt = 0;            // RT_HIP_SHADOW_GRID_N; 0 = 128, or 768 above kBvhAlwaysAbove spheres
   double lg_max_off = 0.0;
   // camera grid (rt_lightgrid.h build_point_grid): the closest hit of camera
@@ -1359,6 +1277,7 @@ struct rt_ctx {
   int2 *d_cg_ent = nullptr;
   size_t cg_start_cap = 0, cg_ent_cap = 0;
   int cg_n = 0;
+  long long cg_nent = 0;
   bool cg_ok = false;                  // the grid for (cg_pos, cg_gen) exists
   double cg_pos[3] = {0, 0, 0};
   unsigned long long cg_gen = ~0ull;   // scene_gen it was built (or refused) for
@@ -1374,6 +1293,7 @@ struct rt_ctx {
   int2 *d_sg_ent = nullptr;
   double *d_sg_rho2 = nullptr;
   int sg_n = 0, sg_grids = 0;
+  long long sg_nstart = 0, sg_nent = 0;
   bool sg_ok = false;
   size_t sg_entries = 0;
   double sg_build_ms = 0.0;
@@ -1564,6 +1484,9 @@ BvhArgs bvh_args(const rt_ctx *c, const Cam &cam) {
   b.n2 = c->d_bvh2;
   b.root_ref = c->bvh2_root;
   b.nnodes = (c->bvh_on && c->cull) ? c->bvh_nodes : 0;
+  b.nn2 = c->bvh2_nodes;
+  b.nn4 = c->bvh4_nodes;
+  b.nprims = c->bvh_prims;
   b.n4 = c->d_bvh4;
   b.root4 = c->bvh4_root;
   b.wide = (c->bvh_wide && c->d_bvh4 && c->bvh4_stack <= kOrderedStack) ? 1 : 0;
@@ -1615,6 +1538,8 @@ LgArgs lg_args(const rt_ctx *c) {
   g.N = c->lg_n;
   g.on = (c->lg_on && c->cull && c->d_lg_start) ? 1 : 0;
   g.max_off = c->lg_max_off;
+  g.nstart = c->lg_nstart;
+  g.nids = c->lg_nids;
   return g;
 }
 
@@ -1676,12 +1601,13 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
       RT_TRY(c, hipMemcpy(c->d_cg_start, start.data(), sb, hipMemcpyHostToDevice));
       if (!ent.empty()) RT_TRY(c, hipMemcpy(c->d_cg_ent, ent.data(), ent.size() * sizeof(int32_t), hipMemcpyHostToDevice));
       c->cg_n = N;
+      c->cg_nent = (long long)ent.size() / 2;
       c->cg_ok = true;
     }
     c->cg_builds++;
     c->cg_build_ms += ms_since(t0);
   }
-  if (c->cg_ok) out = CgArgs{c->d_cg_start, c->d_cg_ent, c->cg_n, 1};
+  if (c->cg_ok) out = CgArgs{c->d_cg_start, c->d_cg_ent, c->cg_n, 1, c->cg_nent};
   return RT_OK;
 }
 
@@ -1735,6 +1661,8 @@ int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
       RT_TRY(c, hipMemcpy(c->d_sg_ent, ent.data(), sizeof(int32_t) * ent.size(), hipMemcpyHostToDevice));
     RT_TRY(c, hipMemcpy(c->d_sg_rho2, rho2.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
     c->sg_n = N;
+    c->sg_nstart = (long long)start.size();
+    c->sg_nent = (long long)ent.size() / 2;
     c->sg_ok = true;
   }
   c->sg_grids = grids;
@@ -1965,7 +1893,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       const int rc = cam_grid(c, cam, nf, ra.cg);
       if (rc != RT_OK) return rc;
     }
-    if (fast && kCull && c->sg_ok) ra.sg = SgArgs{c->d_sg_start, c->d_sg_ent, c->d_sg_rho2, c->sg_n, 1};
+    if (fast && kCull && c->sg_ok)
+      ra.sg = SgArgs{c->d_sg_start, c->d_sg_ent, c->d_sg_rho2, c->sg_n, 1, c->sg_nstart, c->sg_nent, c->nsph};
     c->cg_last = ra.cg.on != 0;
     c->cg_last_n = ra.cg.on ? ra.cg.N : 0;
     RT_TRY(c, mark_start(c));  // the launch's timing starts after the host-side builds
@@ -2097,12 +2026,20 @@ int rt_create(int device, rt_ctx **out) {
   if (device < 0 || device >= n) return RT_ERR_INVALID_ARG;
   rt_ctx *c = new rt_ctx();
   c->device = device;
+  // Environment knobs.  The product build reads two: RT_HIP_LDS_SCENE (the
+  // north star's sphere array and light list staged in LDS per workgroup) and
+  // RT_HIP_CAM_GRID (when the camera grid is built: 0 never, 1 auto, 2 for
+  // every launch).  The tuning build (-DRT_TUNING: variants/librt_hip_tuning.so)
+  // also reads the layout and grid knobs that the parity tests sweep and the
+  // A/B scripts measured; every default below is the measured optimum.
+  if (const char *e = std::getenv("RT_HIP_LDS_SCENE")) c->lds_scene = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_CAM_GRID")) c->cg_mode = std::max(0, std::min(2, std::atoi(e)));
+#ifdef RT_TUNING
   if (const char *e = std::getenv("RT_HIP_BVH")) c->bvh_on = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_MIN")) c->bvh_min = std::atoi(e);
   if (const char *e = std::getenv("RT_HIP_BVH_ALWAYS")) c->bvh_always = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_GROUPS")) c->bvh_groups = std::max(1, std::atoi(e));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID")) c->lg_on = std::atoi(e) != 0;
-  if (const char *e = std::getenv("RT_HIP_LDS_SCENE")) c->lds_scene = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_SCHED")) c->sched = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_STACK")) c->stack_mode = std::atoi(e) == kStackGlobal ? kStackGlobal : kStackMerge;
   if (const char *e = std::getenv("RT_HIP_BVH_ORDERED")) c->bvh_ordered = std::atoi(e) != 0;
@@ -2113,7 +2050,6 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_DEFER_LEVEL")) c->defer_level = std::max(1, std::min(RT_MAX_DEPTH, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(8, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
-  if (const char *e = std::getenv("RT_HIP_CAM_GRID")) c->cg_mode = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_CAM_GRID_N")) c->cg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID")) c->sg_mode = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID_N")) c->sg_n_opt = std::max(1, std::min(256, std::atoi(e)));
@@ -2123,6 +2059,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_GRID_CELLS")) c->ug_cells = std::max(0.05, std::min(64.0, std::atof(e)));
   if (const char *e = std::getenv("RT_HIP_SINGLE_CLASS"))
     c->single_class = std::max(0, std::min(kSchedClasses, std::atoi(e)));
+#endif
   auto bail = [&](int rc) {
     rt_destroy(c);
     return rc;
@@ -2324,7 +2261,8 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
       }
       c->ug = UgArgs{reinterpret_cast<const float4 *>(c->d_ug_rec), c->d_ug_rid,
                      reinterpret_cast<const float4 *>(c->d_ug_q), c->d_ug_ids, c->d_ug_glob, (int)ug.glob.size(),
-                     ug.nx, ug.ny, ug.nz, ug.gx, ug.gy, ug.gz, ug.cs, 0, 0, (float)(1e-4 * (double)ug.extent)};
+                     ug.nx, ug.ny, ug.nz, ug.gx, ug.gy, ug.gz, ug.cs, 0, 0, (float)(1e-4 * (double)ug.extent),
+                     (int)ug.q.size()};
       c->ug_reg_margin = ug.reg_margin;
       c->ug_extent = ug.extent;
       c->ug_entries = ug.ids.size();
@@ -2333,6 +2271,9 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     c->ug_build_ms = ms_since(t_ug);
   }
   c->bvh_nodes = (int)nodes.size();
+  c->bvh2_nodes = (int)nodes2.size();
+  c->bvh4_nodes = (int)nodes4.size();
+  c->bvh_prims = (int)prims.size();
   c->bvh2_root = root2;
   c->bvh_depth = depth2;
   c->bvh4_root = root4;
@@ -2356,6 +2297,8 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     build_light_grid(sx.data(), sy.data(), sz.data(), br.data(), n, lx.data(), ly.data(), lz.data(), nl, diam,
                      c->lg_n, lg_start, lg_ids);
     c->lg_max_off = std::isfinite(diam) ? 1e-7 * diam : 0.0;
+    c->lg_nstart = (long long)lg_start.size();
+    c->lg_nids = (long long)lg_ids.size();
     c->h_sx = sx;
     c->h_sy = sy;
     c->h_sz = sz;
@@ -2462,6 +2405,28 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
   st->negative_clamped = sum[3];
   st->tests_exact = sum[4];
   st->tests_cull = sum[5];
+#ifdef RT_CHECK
+  {
+    // the first out-of-range device index of the launches since the last
+    // read (rt_device.h RT_CK), then cleared for the next ones
+    static const char *const kSiteNames[kCkSites] = {
+        "?", "sphere index", "light-grid start", "light-grid list slot", "camera-grid start",
+        "camera/sphere-grid list slot", "sphere-grid start", "sphere-grid key", "uniform-grid cell",
+        "uniform-grid overflow slot", "BVH node reference", "BVH leaf slot", "tile order slot / tile id",
+        "deferred-queue slot", "reflection-stack slot", "LDS ray-queue slot", "LDS pixel slot",
+        "framebuffer offset"};
+    CheckRec rec{};
+    RT_TRY(c, hipMemcpyFromSymbol(&rec, HIP_SYMBOL(g_check), sizeof rec));
+    if (rec.count) {
+      const CheckRec zero{};
+      RT_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_check), &zero, sizeof zero));
+      c->err = std::string("RT_CHECK: ") + (rec.site < (unsigned long long)kCkSites ? kSiteNames[rec.site] : "?") +
+               " index " + std::to_string((long long)rec.idx) + " outside [0, " + std::to_string(rec.bound) +
+               ") (" + std::to_string(rec.count) + " violations)";
+      return RT_ERR_CHECK;
+    }
+  }
+#endif
 #ifdef RT_STAMPS
   if (const char *tf = std::getenv("RT_HIP_STAMPS_FILE")) {
     static unsigned long long host_tl[kTimelineWaves * kTl];
@@ -2473,6 +2438,7 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
     }
   }
 #endif
+#ifdef RT_STAMPS
   if (std::getenv("RT_HIP_STAMPS")) {  // diagnostic builds (-DRT_STAMPS) fill slots 8..14
     unsigned long long d[12] = {};
     for (int sh = 0; sh < kShards; sh++)
@@ -2489,6 +2455,7 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
                  (double)d[2] / (d[6] ? d[6] : 1), (double)d[3] / (d[6] ? d[6] : 1),
                  (double)d[4] / (d[6] ? d[6] : 1), (double)d[5] / (d[6] ? d[6] : 1));
   }
+#endif
   st->kernel_ms = ms;
   return RT_OK;
 }

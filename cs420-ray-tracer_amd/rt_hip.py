@@ -20,9 +20,15 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # RT_HIP_LIB selects an alternative build of the same ABI (tuning experiments).
 LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(HERE, "librt_hip.so")
+# Test builds of the same sources (csrc/Makefile), selected per context with
+# Renderer(variant=...): "tuning" reads every layout / grid knob (RT_TUNING),
+# "check" range-checks every indirect device index (RT_CHECK).  The product
+# build reads only RT_HIP_LDS_SCENE and RT_HIP_CAM_GRID.
+VARIANTS = {"tuning": os.path.join(HERE, "variants", "librt_hip_tuning.so"),
+            "check": os.path.join(HERE, "variants", "librt_hip_check.so")}
 
 RT_MAX_DEPTH = 64
-ABI_VERSION = 9  # RT_HIP_ABI_VERSION in include/rt_hip.h
+ABI_VERSION = 10  # RT_HIP_ABI_VERSION in include/rt_hip.h
 MAX_FRAMES = 32  # RT_MAX_FRAMES
 
 
@@ -159,12 +165,12 @@ COMPAT_SIGNATURES = {
 # framebuffer formats of rt_render_tile (rt_hip.h)
 RT_FB_RGB8, RT_FB_F32X3, RT_FB_F64X3 = 0, 1, 2
 
-_lib = None
+_libs = {}
 
 
 def lib(path: str = LIB_PATH):
-    """Load librt_hip.so (raises if it has not been built)."""
-    global _lib
+    """Load librt_hip.so (or a test variant of it; raises if it has not been built)."""
+    _lib = _libs.get(path)
     if _lib is None:
         # torch bundles its own libamdhip64.so (SONAME libamdhip64.so.7).  If it
         # is importable, load it first so the dynamic linker binds librt_hip.so
@@ -183,8 +189,17 @@ def lib(path: str = LIB_PATH):
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        _lib = L
+        _libs[path] = _lib = L
     return _lib
+
+
+def variant_lib(variant: str | None):
+    """The library of a test variant ("tuning", "check") or the product's (None)."""
+    if variant is None:
+        return lib()
+    if variant not in VARIANTS:
+        raise ValueError(f"unknown librt_hip variant {variant!r} (one of {sorted(VARIANTS)})")
+    return lib(VARIANTS[variant])
 
 
 def status_string(status: int) -> str:
@@ -194,9 +209,9 @@ def status_string(status: int) -> str:
         return f"status {status}"
 
 
-def _check(rc: int, what: str, ctx=None):
+def _check(rc: int, what: str, ctx=None, L=None):
     if rc != 0:
-        detail = lib().rt_last_error(ctx).decode() if ctx else ""
+        detail = (L or lib()).rt_last_error(ctx).decode() if ctx else ""
         raise RtError(rc, what, detail)
 
 
@@ -275,9 +290,12 @@ def rows_for_shard(height: int, band: int, rank: int, world: int) -> rt_rows:
 class Renderer:
     """One device context (rt_ctx).  Mirrors GPUResources + launch_gpu_kernel."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, variant: str | None = None):
+        """variant: None = the product library; "tuning" / "check" = a test build (VARIANTS)."""
+        self._L = variant_lib(variant)
+        self.variant = variant
         self._ctx = C.c_void_p()
-        _check(lib().rt_create(device, C.byref(self._ctx)), f"rt_create({device})")
+        _check(self._L.rt_create(device, C.byref(self._ctx)), f"rt_create({device})", L=self._L)
         self.device = device
 
     @property
@@ -285,13 +303,13 @@ class Renderer:
         return self._ctx
 
     def set_stream(self, stream_ptr: int | None):
-        _check(lib().rt_set_stream(self._ctx, C.c_void_p(stream_ptr or 0)), "rt_set_stream", self._ctx)
+        _check(self._L.rt_set_stream(self._ctx, C.c_void_p(stream_ptr or 0)), "rt_set_stream", self._ctx, L=self._L)
 
     def set_culling(self, enable: bool):
-        _check(lib().rt_set_culling(self._ctx, int(enable)), "rt_set_culling", self._ctx)
+        _check(self._L.rt_set_culling(self._ctx, int(enable)), "rt_set_culling", self._ctx, L=self._L)
 
     def upload(self, scene: Scene):
-        _check(lib().rt_upload_scene(self._ctx, C.byref(scene.raw)), "rt_upload_scene", self._ctx)
+        _check(self._L.rt_upload_scene(self._ctx, C.byref(scene.raw)), "rt_upload_scene", self._ctx, L=self._L)
 
     def render(self, cam: rt_camera, width: int, height: int, depth: int, rows: rt_rows | None = None,
                out=None, out_on_device: bool = False) -> tuple[object, rt_stats]:
@@ -301,70 +319,70 @@ class Renderer:
             out = bytearray(count * width * 3)
         ptr = _addr(out)
         st = rt_stats()
-        _check(lib().rt_render(self._ctx, C.byref(cam), width, height, depth,
+        _check(self._L.rt_render(self._ctx, C.byref(cam), width, height, depth,
                                C.byref(rows) if rows is not None else None, C.c_void_p(ptr), int(out_on_device),
-                               C.byref(st)), "rt_render", self._ctx)
+                               C.byref(st)), "rt_render", self._ctx, L=self._L)
         return out, st
 
     def render_async(self, cam: rt_camera, width: int, height: int, depth: int, rows: rt_rows | None,
                      out_device_ptr: int):
-        _check(lib().rt_render_async(self._ctx, C.byref(cam), width, height, depth,
+        _check(self._L.rt_render_async(self._ctx, C.byref(cam), width, height, depth,
                                      C.byref(rows) if rows is not None else None, C.c_void_p(out_device_ptr)),
-               "rt_render_async", self._ctx)
+               "rt_render_async", self._ctx, L=self._L)
 
     def render_frames_async(self, cams, width: int, height: int, depth: int, rows: rt_rows | None,
                             out_device_ptr: int, frame_stride: int):
         """rt_render_frames_async: len(cams) frames (<= MAX_FRAMES) in one launch, frame f
         (seen through cams[f]) at out_device_ptr + f * frame_stride."""
         arr = (rt_camera * len(cams))(*cams)
-        _check(lib().rt_render_frames_async(self._ctx, arr, len(cams), width, height, depth,
+        _check(self._L.rt_render_frames_async(self._ctx, arr, len(cams), width, height, depth,
                                             C.byref(rows) if rows is not None else None,
                                             C.c_void_p(out_device_ptr), frame_stride),
-               "rt_render_frames_async", self._ctx)
+               "rt_render_frames_async", self._ctx, L=self._L)
 
     def set_antialias(self, samples: int):
         """1 = the serial path, 4 = the reference GPU's `-a` mode (main_gpu.cu:249-333)."""
-        _check(lib().rt_set_antialias(self._ctx, samples), "rt_set_antialias", self._ctx)
+        _check(self._L.rt_set_antialias(self._ctx, samples), "rt_set_antialias", self._ctx, L=self._L)
 
     def render_tile(self, cam: rt_camera, width: int, height: int, depth: int, tile_x: int, tile_y: int,
                     tile_w: int, tile_h: int, fb_format: int, fb_device_ptr: int):
         """launch_gpu_kernel tile semantics (kernel.cu:185-200) into a full-image device framebuffer."""
-        _check(lib().rt_render_tile(self._ctx, C.byref(cam), width, height, depth, tile_x, tile_y, tile_w, tile_h,
-                                    fb_format, C.c_void_p(fb_device_ptr)), "rt_render_tile", self._ctx)
+        _check(self._L.rt_render_tile(self._ctx, C.byref(cam), width, height, depth, tile_x, tile_y, tile_w, tile_h,
+                                    fb_format, C.c_void_p(fb_device_ptr)), "rt_render_tile", self._ctx, L=self._L)
 
     def render_tiles(self, cam: rt_camera, width: int, height: int, depth: int, tiles, fb_format: int,
                      fb_device_ptr: int):
         """rt_render_tiles: every (x, y, w, h) tile of `tiles` in ONE launch (the 8x8 blocks covering them)."""
         arr = (rt_tile * max(1, len(tiles)))(*[rt_tile(*t) for t in tiles])
-        _check(lib().rt_render_tiles(self._ctx, C.byref(cam), width, height, depth, arr, len(tiles), fb_format,
-                                     C.c_void_p(fb_device_ptr)), "rt_render_tiles", self._ctx)
+        _check(self._L.rt_render_tiles(self._ctx, C.byref(cam), width, height, depth, arr, len(tiles), fb_format,
+                                     C.c_void_p(fb_device_ptr)), "rt_render_tiles", self._ctx, L=self._L)
 
     def stats(self) -> rt_stats:
         st = rt_stats()
-        _check(lib().rt_render_stats(self._ctx, C.byref(st)), "rt_render_stats", self._ctx)
+        _check(self._L.rt_render_stats(self._ctx, C.byref(st)), "rt_render_stats", self._ctx, L=self._L)
         return st
 
     def info(self) -> rt_info:
         """rt_get_info: the host-side builds the render calls made (camera grid, tile order)."""
         inf = rt_info()
-        _check(lib().rt_get_info(self._ctx, C.byref(inf)), "rt_get_info", self._ctx)
+        _check(self._L.rt_get_info(self._ctx, C.byref(inf)), "rt_get_info", self._ctx, L=self._L)
         return inf
 
     def kernel_times(self, max_n: int = 256) -> list[float]:
         """Per-launch kernel durations (ms) since the previous call (syncs the stream)."""
         buf = (C.c_double * max_n)()
         n = C.c_int(0)
-        _check(lib().rt_kernel_times(self._ctx, buf, max_n, C.byref(n)), "rt_kernel_times", self._ctx)
+        _check(self._L.rt_kernel_times(self._ctx, buf, max_n, C.byref(n)), "rt_kernel_times", self._ctx, L=self._L)
         return list(buf[: n.value])
 
     def unpermute(self, gathered_ptr: int, image_ptr: int, width: int, height: int, band: int, shards: int,
                   rows_per_shard: int):
-        _check(lib().rt_unpermute_rows(self._ctx, C.c_void_p(gathered_ptr), C.c_void_p(image_ptr), width, height,
-                                       band, shards, rows_per_shard), "rt_unpermute_rows", self._ctx)
+        _check(self._L.rt_unpermute_rows(self._ctx, C.c_void_p(gathered_ptr), C.c_void_p(image_ptr), width, height,
+                                       band, shards, rows_per_shard), "rt_unpermute_rows", self._ctx, L=self._L)
 
     def close(self):
         if self._ctx:
-            lib().rt_destroy(self._ctx)
+            self._L.rt_destroy(self._ctx)
             self._ctx = C.c_void_p()
 
     def __del__(self):

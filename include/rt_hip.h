@@ -52,9 +52,9 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 9  /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
+#define RT_HIP_ABI_VERSION 10 /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
                                    6: rt_render_tiles; 7: rt_get_info; 8: rt_info sphere-grid fields;
-                                   9: rt_info behind-grid fields */
+                                   9: rt_info behind-grid fields; 10: RT_ERR_CHECK */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -67,6 +67,8 @@ typedef enum rt_status {
     RT_ERR_NO_SCENE = 5,     /* rt_render before rt_upload_scene */
     RT_ERR_IO = 6,           /* scene file could not be opened / image not written */
     RT_ERR_DEPTH = 7,        /* depth > RT_MAX_DEPTH */
+    RT_ERR_CHECK = 8,        /* bounds-checked build (-DRT_CHECK) only: a device index into a host-built
+                                structure was out of range; rt_last_error() names the site (rt_render_stats) */
 } rt_status;
 
 /* Sphere + Material, include/sphere.h:8-21.  reflectivity = the file's

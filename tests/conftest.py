@@ -49,6 +49,18 @@ def diff_summary(a: bytes, b: bytes) -> str:
     return f"{int((d > 0).sum())} channels differ, {int((d > 1).sum())} by >1, max {int(d.max()) if d.size else 0}"
 
 
+# RT_HIP_* knobs the product library reads itself (rt_create); every other
+# layout / grid knob is read only by the tuning build (variants/librt_hip_tuning.so)
+PRODUCT_KNOBS = {"RT_HIP_LDS_SCENE", "RT_HIP_CAM_GRID", "RT_HIP_LIB"}
+
+
+def knob_variant():
+    """The library a test context must use for the RT_HIP_* knobs now set: the
+    product's when only its own knobs are set, else the tuning build."""
+    tuning = [k for k in os.environ if k.startswith("RT_HIP_") and k not in PRODUCT_KNOBS]
+    return "tuning" if tuning else None
+
+
 @pytest.fixture(scope="session")
 def gpu_renderer():
     import rt_hip

@@ -4,7 +4,7 @@ its own camera, and the launch's ray counts are the sums over its frames."""
 import numpy as np
 import pytest
 
-from conftest import diff_summary, golden_rgb, manifest, scene_path
+from conftest import diff_summary, golden_rgb, manifest, scene_path, knob_variant
 
 pytestmark = pytest.mark.gpu
 
@@ -149,7 +149,7 @@ def test_frames_knobs(monkeypatch, env):
 
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    r = rt_hip.Renderer(0)
+    r = rt_hip.Renderer(0, variant=knob_variant())
     try:
         sc, m = _load(r, "synth200_1920x1080_d4")
         frames, _, _ = _frames(r, [sc.camera()] * 3, m["width"], m["height"], m["depth"])

@@ -6,7 +6,7 @@ failure report shows both)."""
 import numpy as np
 import pytest
 
-from conftest import diff_summary, golden_rgb, manifest, scene_path
+from conftest import diff_summary, golden_rgb, manifest, scene_path, knob_variant
 
 pytestmark = pytest.mark.gpu
 
@@ -332,7 +332,7 @@ def test_fractional_shininess_mirror_cloud_vs_oracle(monkeypatch, n):
     text = _mirror_cloud(11, n, frac=True)
     sc = rt_hip.Scene.parse(text)
     monkeypatch.setenv("RT_HIP_DEFER", "1")
-    r = rt_hip.Renderer(0)
+    r = rt_hip.Renderer(0, variant=knob_variant())
     r.upload(sc)
     ref, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=8)
     try:
@@ -360,16 +360,15 @@ def test_cull_equals_bruteforce_at_4k(gpu_renderer):
     assert sa.rays == sb.rays
 
 
-@pytest.fixture(params=[{"RT_HIP_BVH_ALWAYS": "1"}, {"RT_HIP_BVH_MIN": "0"}, {"RT_HIP_BVH": "0"},
-                        {"RT_HIP_BVH_ALWAYS": "1", "RT_HIP_BVH4": "0"}, {"RT_HIP_BVH_LEAF": "4"}],
-                ids=["bvh-always", "bvh-min0", "bvh-off", "bvh-always-two-child", "leaf-4"])
+@pytest.fixture(params=[{"RT_HIP_BVH_ALWAYS": "1"}, {"RT_HIP_BVH_ALWAYS": "1", "RT_HIP_BVH4": "0"}],
+                ids=["bvh-always", "bvh-always-two-child"])
 def bvh_renderer(request, monkeypatch):
     """A fresh context per BVH policy (the knobs are read at rt_create)."""
     import rt_hip
 
     for k, v in request.param.items():
         monkeypatch.setenv(k, v)
-    r = rt_hip.Renderer(0)
+    r = rt_hip.Renderer(0, variant=knob_variant())
     yield r
     r.close()
 
@@ -415,32 +414,28 @@ def test_bvh_far_from_origin(bvh_renderer):
     assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
 
 
+# the layouts the product reaches without a knob (the global stack: tiles,
+# antialias; scanline order: launches under 1,024 tiles; an 8-entry merge
+# queue: scenes whose walk stacks fill the LDS; deferral on / off: multi- /
+# one-frame launches) plus the north star's LDS-staged scene
 @pytest.fixture(params=[{"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_SCHED": "0"}, {"RT_HIP_STACK": "1"},
-                        {"RT_HIP_STACK": "1", "RT_HIP_SCHED": "0"}, {"RT_HIP_STACK": "4", "RT_HIP_LDS_SCENE": "1"},
-                        {"RT_HIP_MERGE_Q": "16"}, {"RT_HIP_DEFER": "0"}, {"RT_HIP_DEFER": "1"},
-                        {"RT_HIP_DEFER": "1", "RT_HIP_DEFER_LEVEL": "1"},
-                        {"RT_HIP_DEFER": "1", "RT_HIP_DEFER_LEVEL": "3"},
-                        {"RT_HIP_DEFER": "1", "RT_HIP_DEFER_WALK": "0"}, {"RT_HIP_MERGE_Q": "8"},
-                        {"RT_HIP_SINGLE_CLASS": "0"}, {"RT_HIP_SINGLE_CLASS": "4"}],
-                ids=["lds-scene", "scanline-order", "global-stack", "global-stack-scanline", "merge-lds-scene",
-                     "merge-queue-16", "no-defer", "defer-one-frame", "defer-level-1", "defer-level-3",
-                     "defer-walk-off", "merge-queue-8", "one-tile-waves-all", "one-tile-waves-none"])
+                        {"RT_HIP_DEFER": "0"}, {"RT_HIP_DEFER": "1"}, {"RT_HIP_MERGE_Q": "8"}],
+                ids=["lds-scene", "scanline-order", "global-stack", "no-defer", "defer-one-frame",
+                     "merge-queue-8"])
 def stack_renderer(request, monkeypatch):
     """Non-default kernel layouts (RT_HIP_STACK=1: one tile per wave with the
     per-pixel global stack instead of merged levels; RT_HIP_LDS_SCENE=1:
     scenes that fit staged in LDS with 4-wave workgroups; RT_HIP_SCHED=0: tiles
     launched in scanline order instead of heaviest-predicted first;
-    RT_HIP_MERGE_Q / RT_HIP_DEFER / RT_HIP_DEFER_LEVEL: merge-queue size and
-    the deferred-ray kernel (these single-frame renders defer only with
-    RT_HIP_DEFER=1: by default one-frame launches keep every level in the
-    megakernel); RT_HIP_SINGLE_CLASS: which tiles get a wave each in one-frame
-    launches; RT_HIP_DEFER_WALK=0: large scenes' deferred rays
-    through render_deferred instead of render_deferred_walk)."""
+    RT_HIP_MERGE_Q / RT_HIP_DEFER: merge-queue size and the deferred-ray kernel
+    (these single-frame renders defer only with RT_HIP_DEFER=1: by default
+    one-frame launches keep every level in the megakernel)).  Knobs other
+    than RT_HIP_LDS_SCENE are read by the tuning build only."""
     import rt_hip
 
     for k, v in request.param.items():
         monkeypatch.setenv(k, v)
-    r = rt_hip.Renderer(0)
+    r = rt_hip.Renderer(0, variant=knob_variant())
     yield r
     r.close()
 
@@ -476,25 +471,21 @@ def test_stack_modes_depth_edges(stack_renderer, depth):
             assert np.array_equal(got[k], want[y])
 
 
-@pytest.mark.parametrize("walk", [{}, {"RT_HIP_DEFER": "1"}, {"RT_HIP_BVH4": "0"}, {"RT_HIP_BVH_ORDERED": "0"},
-                                  {"RT_HIP_DEFER_WALK": "0", "RT_HIP_DEFER": "1"},
-                                  {"RT_HIP_DEFER_LEVEL": "1", "RT_HIP_DEFER": "1"}],
-                         ids=["ordered4", "ordered4-defer", "ordered2", "stackless", "defer-walk-off",
-                              "defer-walk-level-1"])
+@pytest.mark.parametrize("walk", [{}, {"RT_HIP_DEFER": "1"}, {"RT_HIP_BVH4": "0"}, {"RT_HIP_BVH_ORDERED": "0"}],
+                         ids=["ordered4", "ordered4-defer", "ordered2", "stackless"])
 @pytest.mark.parametrize("seed,count", [(101, 700), (102, 1100), (103, 1600)])
 def test_large_scenes_global_memory_paths(monkeypatch, walk, seed, count):
     """Scenes read through L2 with the BVH fallback: the ordered 4-wide walk
     (default), the ordered two-child walk (RT_HIP_BVH4=0) and the stackless
     preorder walk (RT_HIP_BVH_ORDERED=0) against the oracle; above 1024 spheres
     every group walks the tree (384-cell shadow grids, 1-sphere leaves) and the
-    deferred rays go through render_deferred_walk (RT_HIP_DEFER_WALK=0: through
-    render_deferred; RT_HIP_DEFER_LEVEL=1: every reflection ray through it)."""
+    deferred rays go through render_deferred (the uniform grid's closest hits)."""
     import orc
     import rt_hip
 
     for k, v in walk.items():
         monkeypatch.setenv(k, v)
-    r = rt_hip.Renderer(0)
+    r = rt_hip.Renderer(0, variant=knob_variant())
     try:
         text = _random_scene(seed, count)
         W, H, D = 96, 64, 5
@@ -548,7 +539,7 @@ def test_deferred_queue_overflow_vs_oracle(n):
     old1 = os.environ.get("RT_HIP_DEFER")
     os.environ["RT_HIP_DEFER"] = "1"
     try:
-        r = rt_hip.Renderer(0)
+        r = rt_hip.Renderer(0, variant=knob_variant())
     finally:
         if old1 is None:
             del os.environ["RT_HIP_DEFER"]
@@ -565,7 +556,7 @@ def test_deferred_queue_overflow_vs_oracle(n):
     old = os.environ.get("RT_HIP_DEFER")
     os.environ["RT_HIP_DEFER"] = "0"
     try:
-        r0 = rt_hip.Renderer(0)
+        r0 = rt_hip.Renderer(0, variant=knob_variant())
     finally:
         if old is None:
             del os.environ["RT_HIP_DEFER"]

@@ -15,7 +15,7 @@ import subprocess
 
 import pytest
 
-from conftest import diff_summary
+from conftest import diff_summary, knob_variant
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "cs420-ray-tracer_amd", "csrc")
@@ -71,7 +71,7 @@ def grid_renderer(request, monkeypatch):
     on, n = request.param
     monkeypatch.setenv("RT_HIP_SHADOW_GRID", on)
     monkeypatch.setenv("RT_HIP_SHADOW_GRID_N", n)
-    r = rt_hip.Renderer(0)
+    r = rt_hip.Renderer(0, variant=knob_variant())
     yield r
     r.close()
 
@@ -101,7 +101,7 @@ def test_grid_in_other_layouts(monkeypatch, env):
 
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    r = rt_hip.Renderer(0)
+    r = rt_hip.Renderer(0, variant=knob_variant())
     try:
         for name in ("lights_in_cluster", "axis_tangent"):
             text = GRID_SCENES[name]
@@ -169,7 +169,7 @@ def camgrid_renderer(request, monkeypatch):
 
     monkeypatch.setenv("RT_HIP_CAM_GRID", "2")
     monkeypatch.setenv("RT_HIP_CAM_GRID_N", request.param)
-    r = rt_hip.Renderer(0)
+    r = rt_hip.Renderer(0, variant=knob_variant())
     yield r
     r.close()
 
@@ -198,7 +198,7 @@ def test_camera_grid_goldens(monkeypatch):
     from conftest import golden_rgb, manifest, scene_path
 
     monkeypatch.setenv("RT_HIP_CAM_GRID", "2")
-    r = rt_hip.Renderer(0)
+    r = rt_hip.Renderer(0, variant=knob_variant())
     try:
         for name, m in sorted(manifest().items()):
             sc = rt_hip.Scene.load(scene_path(m["scene"]))
@@ -242,7 +242,7 @@ def spheregrid_renderer(request, monkeypatch):
     else:
         monkeypatch.setenv("RT_HIP_SPHERE_GRID", "1")
         monkeypatch.setenv("RT_HIP_SPHERE_GRID_N", request.param)
-    r = rt_hip.Renderer(0)
+    r = rt_hip.Renderer(0, variant=knob_variant())
     yield r, request.param
     r.close()
 
@@ -288,7 +288,7 @@ def test_sphere_grid_goldens(monkeypatch):
     for n in ("16", "3"):
         monkeypatch.setenv("RT_HIP_SPHERE_GRID", "1")
         monkeypatch.setenv("RT_HIP_SPHERE_GRID_N", n)
-        r = rt_hip.Renderer(0)
+        r = rt_hip.Renderer(0, variant=knob_variant())
         try:
             for name, m in sorted(manifest().items()):
                 sc = rt_hip.Scene.load(scene_path(m["scene"]))
