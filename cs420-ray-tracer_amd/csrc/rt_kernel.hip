@@ -835,6 +835,8 @@ __device__ __forceinline__ void flush_counts(unsigned long long *counters, const
 #ifdef RT_STAMPS
     for (int q = 0; q < 6; q++) atomicAdd(&sc[8 + q], work.st[q]);
     atomicAdd(&sc[20], work.st[6]);
+    atomicAdd(&sc[21], work.st[8]);  // closest hits
+    atomicAdd(&sc[22], work.st[9]);  // shadow queries
     atomicAdd(&sc[14], 1ull);
     atomicAdd(&sc[15], work.iters);
     atomicAdd(&sc[16], work.sweeps);
@@ -2450,6 +2452,12 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
                  "RT_STAMPS per wave: candidate iterations %.1f (closest %.1f, of which primary %.1f), sweeps %.2f "
                  "(closest %.2f), bvh cycles %.0f\n",
                  d[7] / nw, d[9] / nw, d[11] / nw, d[8] / nw, d[10] / nw, bvh / nw);
+    unsigned long long cl = 0, sh = 0;
+    for (int s2 = 0; s2 < kShards; s2++) {
+      cl += c->h_counters[s2 * kShardStride + 21];
+      sh += c->h_counters[s2 * kShardStride + 22];
+    }
+    std::fprintf(stderr, "RT_STAMPS cycles/wave: closest hits %.0f, shadow queries %.0f\n", cl / nw, sh / nw);
     std::fprintf(stderr, "RT_STAMPS waves=%llu cycles/wave: bound %.0f cull %.0f cand %.0f setup %.0f shade %.0f total %.0f\n",
                  d[6], (double)d[0] / (d[6] ? d[6] : 1), (double)d[1] / (d[6] ? d[6] : 1),
                  (double)d[2] / (d[6] ? d[6] : 1), (double)d[3] / (d[6] ? d[6] : 1),
