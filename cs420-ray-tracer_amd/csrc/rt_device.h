@@ -113,7 +113,33 @@ __device__ __forceinline__ D3 sub(D3 a, D3 b) { return mk(a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ D3 mul(D3 a, D3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ D3 scale(D3 a, double t) { return mk(a.x * t, a.y * t, a.z * t); }
 __device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ double length(D3 a) { return __builtin_sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+// sqrt(x) for x in [2^-767, DBL_MAX]: the compiler's correctly rounded fp64
+// sqrt expansion (v_rsq_f64, g = x y, h = y / 2, r = 1/2 - h g, g += g r,
+// h += h r, then two residual corrections g += (x - g^2) h) without its range
+// handling -- the scaling of x below 2^-767 by 2^256 (and of the result by
+// 2^-128) and the pass-through of zeros and infinities -- which operands in
+// that range never take: the same operations in the same order, so the same
+// bits as __builtin_sqrt there (tests/native/renorm_gpu_check.hip checks it
+// on the device).  5 fewer VALU instructions and 2 fewer wait states per root.
+constexpr double kSqrtCoreLo = 0x1p-767;
+__device__ __forceinline__ double sqrt_core(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  const double d0 = __builtin_fma(-g, g, x);
+  h = __builtin_fma(h, r, h);
+  g = __builtin_fma(d0, h, g);
+  const double d1 = __builtin_fma(-g, g, x);
+  return __builtin_fma(d1, h, g);
+}
+__device__ __forceinline__ bool sqrt_core_ok(double x) { return x >= kSqrtCoreLo && x <= 0x1.fffffffffffffp+1023; }
+// IEEE sqrt: the core on its range, the compiler's full expansion elsewhere
+__device__ __forceinline__ double sqrt_rn(double x) {
+  if (__builtin_expect(sqrt_core_ok(x), 1)) return sqrt_core(x);
+  return __builtin_sqrt(x);
+}
+__device__ __forceinline__ double length(D3 a) { return sqrt_rn(a.x * a.x + a.y * a.y + a.z * a.z); }
 
 // (a.x / b, a.y / b, a.z / b), bit-identical to three IEEE divisions.  The
 // compiler lowers one fp64 division to v_div_scale (x2), v_rcp_f64, two
@@ -288,7 +314,8 @@ __device__ __forceinline__ int intersect_num(const SphGeo &s, D3 o, D3 d, double
     num = -b;  // t = -b / a2, negative roots included (sphere.h:43-47)
     return 1;
   }
-  double sq = __builtin_sqrt(disc);
+  if (!sqrt_core_ok(disc)) return 2;  // a disc below 2^-767 (or infinite): the exact intersect()
+  double sq = sqrt_core(disc);
   double n1 = -b - sq, n2 = -b + sq;
   if (__builtin_fabs(n1) < kTinyNum || __builtin_fabs(n2) < kTinyNum) return 2;
   if (n2 < 0.0) return 0;

@@ -3,7 +3,10 @@ setting (RT_HIP_* environment read at rt_create), per workload:
   single-frame launches from fresh camera positions (kernel ms, median),
   the batched rate (launches of F frames, kernel ms per frame),
 and a byte check that every setting renders the same image.
-  python scripts/ab_launch.py VAR=v1,v2,... [workload ...]"""
+  python scripts/ab_launch.py VAR=v1,v2,... [workload ...]
+  python scripts/ab_launch.py "A=1+B=0;A=2;default" [workload ...]   (settings of several knobs)
+Every setting runs on the tuning build (variants/librt_hip_tuning.so), the
+default one included, so the A/B compares one library."""
 import os
 import sys
 
@@ -24,7 +27,7 @@ def run(workload, env, reps=3):
     try:
         sc = rt_hip.Scene.load(os.path.join(bench.PKG, "scenes", name + ".txt"))
         cam = sc.camera()
-        r = rt_hip.Renderer(0)
+        r = rt_hip.Renderer(0, variant="tuning")
         r.upload(sc)
         rows = rt_hip.rt_rows(1, 0, 1, H)
         F = 32
@@ -50,17 +53,25 @@ def run(workload, env, reps=3):
             del os.environ[k]
 
 
+def settings(arg):
+    if ";" in arg or "+" in arg:  # "A=1+B=0;A=2;default"
+        out = []
+        for setting in arg.split(";"):
+            out.append({} if setting == "default" else dict(kv.split("=", 1) for kv in setting.split("+")))
+        return out
+    var, vals = arg.split("=")
+    return [{} if v == "default" else {var: v} for v in vals.split(",")]
+
+
 def main():
-    var, vals = sys.argv[1].split("=")
     loads = sys.argv[2:] or ["synth200_1920x1080_d4", "complex_1920x1080_d4"]
     for wl in loads:
         ref = None
-        for v in vals.split(","):
-            env = {} if v == "default" else {var: v}
+        for env in settings(sys.argv[1]):
             res, img = run(wl, env)
             same = ref is None or img == ref
             ref = ref or img
-            print(f"{wl} {var}={v}: {res} same_image={same}", flush=True)
+            print(f"{wl} {env or 'default'}: {res} same_image={same}", flush=True)
             assert same
 
 
