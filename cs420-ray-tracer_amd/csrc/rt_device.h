@@ -113,33 +113,7 @@ __device__ __forceinline__ D3 sub(D3 a, D3 b) { return mk(a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ D3 mul(D3 a, D3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ D3 scale(D3 a, double t) { return mk(a.x * t, a.y * t, a.z * t); }
 __device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-// sqrt(x) for x in [2^-767, DBL_MAX]: the compiler's correctly rounded fp64
-// sqrt expansion (v_rsq_f64, g = x y, h = y / 2, r = 1/2 - h g, g += g r,
-// h += h r, then two residual corrections g += (x - g^2) h) without its range
-// handling -- the scaling of x below 2^-767 by 2^256 (and of the result by
-// 2^-128) and the pass-through of zeros and infinities -- which operands in
-// that range never take: the same operations in the same order, so the same
-// bits as __builtin_sqrt there (tests/native/renorm_gpu_check.hip checks it
-// on the device).  5 fewer VALU instructions and 2 fewer wait states per root.
-constexpr double kSqrtCoreLo = 0x1p-767;
-__device__ __forceinline__ double sqrt_core(double x) {
-  const double y = __builtin_amdgcn_rsq(x);
-  double g = x * y, h = y * 0.5;
-  const double r = __builtin_fma(-h, g, 0.5);
-  g = __builtin_fma(g, r, g);
-  const double d0 = __builtin_fma(-g, g, x);
-  h = __builtin_fma(h, r, h);
-  g = __builtin_fma(d0, h, g);
-  const double d1 = __builtin_fma(-g, g, x);
-  return __builtin_fma(d1, h, g);
-}
-__device__ __forceinline__ bool sqrt_core_ok(double x) { return x >= kSqrtCoreLo && x <= 0x1.fffffffffffffp+1023; }
-// IEEE sqrt: the core on its range, the compiler's full expansion elsewhere
-__device__ __forceinline__ double sqrt_rn(double x) {
-  if (__builtin_expect(sqrt_core_ok(x), 1)) return sqrt_core(x);
-  return __builtin_sqrt(x);
-}
-__device__ __forceinline__ double length(D3 a) { return sqrt_rn(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ double length(D3 a) { return __builtin_sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
 
 // (a.x / b, a.y / b, a.z / b), bit-identical to three IEEE divisions.  The
 // compiler lowers one fp64 division to v_div_scale (x2), v_rcp_f64, two
@@ -314,8 +288,7 @@ __device__ __forceinline__ int intersect_num(const SphGeo &s, D3 o, D3 d, double
     num = -b;  // t = -b / a2, negative roots included (sphere.h:43-47)
     return 1;
   }
-  if (!sqrt_core_ok(disc)) return 2;  // a disc below 2^-767 (or infinite): the exact intersect()
-  double sq = sqrt_core(disc);
+  double sq = __builtin_sqrt(disc);
   double n1 = -b - sq, n2 = -b + sq;
   if (__builtin_fabs(n1) < kTinyNum || __builtin_fabs(n2) < kTinyNum) return 2;
   if (n2 < 0.0) return 0;
@@ -1205,6 +1178,64 @@ __device__ __forceinline__ unsigned long long next_group(unsigned long long todo
   return __ballot(key == kf) & todo;
 }
 
+// The nearest-first scan of sweep_closest's camera-ray candidates.  Lane j <
+// seen holds candidate j (cand[j]) and tl, a lower bound of every t the
+// reference's test (sphere.h:26-59) can return for that sphere on a ray from
+// P (the camera position, every lane's origin): with D = |C - P| and the
+// camera grid's grown radius R = |r|(1 + 1e-6) + 1e-6 (D + diameter)
+// (rt_lightgrid.h: covers |d| != 1 and the rounding of the computed root),
+// every root is >= (D - R)(1 - 1e-9) when the sphere lies wholly ahead of P
+// for every lane's direction -- its angular radius asin(R / D) plus the
+// bound's widest angle theta plus its angle from the axis under pi/2, every
+// lane's d within theta of the axis and on its side (checked) -- and the only
+// other root it can give, the tangent one kept at disc == 0 (sphere.h:43-47),
+// is >= -(D + R)(1 + 1e-9); a sphere containing P (D <= R), or NaN data,
+// gets -inf.  Candidates are visited by ascending (tl, index); a lane stops
+// at the first whose tl exceeds its best t: every later candidate can only
+// give a t > best, so neither a smaller t nor a tie -- the lexicographic
+// (t, index) minimum is unchanged (the camera grid's argument, with the
+// wave's candidate set as the cell).
+template <typename T>
+__device__ __forceinline__ void sorted_scan(const SphGeo *__restrict__ g, const double *__restrict__ rad,
+                                            const BvhArgs &bv, const Bound &B, bool gact, D3 d, int seen,
+                                            const __attribute__((address_space(3))) int *cand, const double &bt,
+                                            Work &work, T &&test) {
+  const int lane = (int)(threadIdx.x & 63);
+  const bool fwd = B.cull && __ballot(gact && !(d.x * B.ax + d.y * B.ay + d.z * B.az > 0.0)) == 0;
+  const double ct = __builtin_sqrt(B.cos2);
+  int ci = 0;
+  double tl = -__builtin_inf();
+  if (lane < seen) {
+    ci = cand[lane];
+    const SphGeo s = g[RT_CK(kCkSphere, ci, 1LL << 30)];
+    const double vx = s.cx - B.px, vy = s.cy - B.py, vz = s.cz - B.pz;
+    const double D = __builtin_sqrt((vx * vx + vy * vy) + vz * vz);
+    const double R = rad[ci] * (1.0 + 1e-6) + 1e-6 * (D + bv.diam);
+    if (D > R) {
+      const double sb = R / D, cb = __builtin_sqrt(1.0 - sb * sb);
+      const bool ahead = fwd && (vx * B.ax + vy * B.ay + vz * B.az) / D > B.sin_t * cb + ct * sb + 1e-9;
+      tl = ahead ? (D - R) * (1.0 - 1e-9) : -(D + R) * (1.0 + 1e-9);
+    }
+  }
+  int rank = 0;  // position by ascending (tl, index); the ids are distinct
+  for (int k = 0; k < seen; ++k) {
+    const double tk = lane_bcast(tl, k);
+    const int ik = __builtin_amdgcn_readlane(ci, k);
+    rank += (tk < tl || (tk == tl && ik < ci)) ? 1 : 0;
+  }
+  for (int r = 0; r < seen; ++r) {
+    const int k = __builtin_ctzll(__ballot(lane < seen && rank == r));
+    const int i = __builtin_amdgcn_readlane(ci, k);
+    const double tk = lane_bcast(tl, k);
+    const bool want = gact && !(bt < tk);
+    if (__ballot(want) == 0) break;
+    if (want) {
+      work.exact += 1;
+      test(i);
+    }
+  }
+}
+
 // Scene::find_intersection (scene.h:41-61): all candidate spheres in file
 // order, strict '<' (so ties keep the lowest index), t starts at 1e20.
 // kFast: the default configuration only (ordered 4-wide BVH walk); the other
@@ -1270,6 +1301,19 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       RT_ACC(work, 0, tb);
       RT_CNT(work, sweeps, 1);
       int seen = 0;
+      // Camera rays (key -1, every lane leaving P itself): the candidates are
+      // collected first (their ids in the wave's walk-stack LDS, unused until a
+      // walk) and tested nearest first, each lane stopping at the first whose
+      // least possible t exceeds its best (sorted_scan, below).  Other groups
+      // test the candidates of each 64-sphere step in file order.
+      bool sorted = false;
+      if constexpr (kFast) {
+        sorted = bv.ostk_off >= 0 && bv.odepth >= 1 && __builtin_amdgcn_readlane(key, fl) < 0 &&
+                 __ballot(gact && !(o.x == B.px && o.y == B.py && o.z == B.pz)) == 0;
+      }
+      typedef __attribute__((address_space(3))) int LdsI32;
+      LdsI32 *cand = reinterpret_cast<LdsI32 *>(ordered_stack_lds(bv) - lane);
+      bool loose = false;
       for (int base = 0; base < n; base += 64) {
         RT_T0(tc);
         unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
@@ -1278,7 +1322,16 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
         seen += __popcll(mask);
         if (have_bvh && seen > bv.min_cands) {  // loose bound: this group walks the BVH
           need = need || gact;
+          loose = true;
           break;
+        }
+        if (sorted) {
+          if (seen > 64) {  // more candidates than lanes: file order from here on
+            sorted = false;
+          } else {
+            if ((mask >> lane) & 1ull) cand[seen - __popcll(mask) + __popcll(mask & ((1ull << lane) - 1ull))] = base + lane;
+            continue;
+          }
         }
         RT_T0(tt);
         if (gact) {
@@ -1293,6 +1346,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
         }
         RT_ACC(work, 2, tt);
       }
+      if (sorted && !loose && seen > 0) sorted_scan(g, rad, bv, B, gact, d, seen, cand, bt, work, test);
     } else {
       for (int base = 0; base < n; base += 64) {
         unsigned long long mask = candidates<false>(g, rad, n, base, Bound{});

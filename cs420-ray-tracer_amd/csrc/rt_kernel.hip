@@ -98,7 +98,6 @@ struct RenderArgs {
   int rows_dword;                 // kStackMerge: every 8-pixel tile row starts dword aligned (flush_tile)
   int defer_level;                // kStackMerge: rays of this reflection level and deeper are deferred
   int xcd_frames;                 // multi-frame launches: every frame of a tile group on one XCD (render_kernel)
-  int prio_end[3];                // kStackMerge: tile slots [0, prio_end[k]) are of class >= 3 - k (rt_sched); -1: off
 };
 // the whole struct is the kernel's argument block (kernarg segment, at most 4 KiB)
 static_assert(sizeof(RenderArgs) <= 4096, "RenderArgs exceeds the kernel-argument segment");
@@ -661,19 +660,6 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     }
     qn -= take;
   };
-  {
-    // issue priority by the group's predicted cost (its first tile's class,
-    // rt_sched.h): the heaviest chains -- a one-frame launch's critical path --
-    // issue first on their SIMD when waves of lighter tiles share it
-    const int *pe = kernarg_late<true, offsetof(RenderArgs, prio_end)>(a.prio_end);
-    if (pe[0] >= 0) {
-      const int ns = kernarg_late<true, offsetof(RenderArgs, nsingle)>(a.nsingle);
-      const int b0 = group < ns ? group : ns + (group - ns) * kMergeTiles;
-      if (b0 < pe[0]) __builtin_amdgcn_s_setprio(3);
-      else if (b0 < pe[1]) __builtin_amdgcn_s_setprio(2);
-      else if (b0 < pe[2]) __builtin_amdgcn_s_setprio(1);
-    }
-  }
   while (true) {
     // the group's tile slots: [base, base + nt) -- one slot for the first nsingle
     // groups (the heaviest tiles: their own reflection rays fill the wave, and
@@ -1416,9 +1402,6 @@ struct rt_ctx {
   // 2.49 ms per frame); synth200 keeps the adjacent order (0.1943 vs 0.1958
   // ms per frame at 32 frames, equal at 20; profiles/r3u/ab_xcd_frames.log)
   int xcd_frames = -1;
-  // RT_HIP_PRIO: merge_tiles sets each wave's issue priority from its tile
-  // group's class (0 off, 1 in one-frame launches, 2 in every launch)
-  int prio = 0;
   // rt_get_info: host-side builds made by the render calls
   bool cg_last = false;
   int cg_last_n = 0;
@@ -1884,11 +1867,6 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   // row k of frame f starts at ptr + f fstride + 3 (k W + x): dword aligned for every k, f and x = 8i
   ra.rows_dword = ((reinterpret_cast<uintptr_t>(od.ptr) | (uintptr_t)(3 * (size_t)W) | (uintptr_t)od.fstride) & 3) == 0;
   ra.defer_level = c->defer_level;
-  ra.prio_end[0] = ra.prio_end[1] = ra.prio_end[2] = -1;
-  if (kStack == kStackMerge && perm && !batch_perm && (c->prio == 2 || (c->prio == 1 && nf == 1))) {
-    long long e = 0;
-    for (int k = 0; k < 3; k++) ra.prio_end[k] = (int)(e += c->perm_cls[kSchedClasses - 1 - k]);
-  }
   ra.xcd_frames = xcd_frames ? 1 : 0;
   if (kStack == kStackMerge && (c->defer > 0 || (c->defer < 0 && nf > 1)) && depth > c->defer_level) {
     // room for 1/8 of the launch's pixels (deferred rays are ~2 % on synth200); a ray
@@ -2080,7 +2058,6 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BEHIND_GRID")) c->ug_mode = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_GRID_CLOSEST")) c->ug_closest = std::atoi(e) != 0 ? 1 : 0;  // (see ug_closest)
   if (const char *e = std::getenv("RT_HIP_XCD_FRAMES")) c->xcd_frames = std::max(-1, std::min(1, std::atoi(e)));
-  if (const char *e = std::getenv("RT_HIP_PRIO")) c->prio = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_GRID_CELLS")) c->ug_cells = std::max(0.05, std::min(64.0, std::atof(e)));
   if (const char *e = std::getenv("RT_HIP_SINGLE_CLASS"))
     c->single_class = std::max(0, std::min(kSchedClasses, std::atoi(e)));

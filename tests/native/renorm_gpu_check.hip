@@ -78,65 +78,7 @@ __global__ void check(uint64_t seed, uint64_t n, unsigned long long *out) {
   }
 }
 
-// rtk::sqrt_core (rt_device.h: the compiler's fp64 sqrt expansion without its
-// range handling) against __builtin_sqrt on its range [2^-767, DBL_MAX]:
-// random significands over every exponent of the range (kind 0), operands
-// next to squares of random doubles and to the ends of the range (kind 1),
-// and the renderer's own radicands -- the discriminants and squared lengths
-// of random unit-scale rays and spheres (kind 2).  out[kind] counts tested
-// values, out[3 + kind] mismatches; out[6] the last mismatching operand.
-__global__ void sqrt_check(uint64_t seed, uint64_t n, unsigned long long *out) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  for (int kind = 0; kind < 3; ++kind) {
-    const uint64_t z0 = mix(seed ^ (i * 3 + kind) ^ 0x5157ull), z1 = mix(z0), z2 = mix(z1);
-    double x;
-    if (kind == 0) {
-      const int ex = -767 + (int)(z1 % (1023 + 767 + 1));
-      x = __builtin_ldexp(1.0 + unit(z0), ex);
-    } else if (kind == 1) {
-      const double edges[] = {0x1p-767, 0x1.0000000000001p-767, 0x1.fffffffffffffp+1023, 1.0, 0x1.fffffffffffffp-1,
-                              0x1.0000000000001p+0, 4.0, 2.0};
-      const double q = __builtin_ldexp(1.0 + unit(z0), (int)(z1 % 1000) - 383);
-      x = (z2 % 4 == 0) ? edges[(z2 >> 8) % 8] : __double_as_longlong(q * q) + (int64_t)((z2 >> 16) % 5) - 2 > 0
-                                                    ? __longlong_as_double(__double_as_longlong(q * q) +
-                                                                           (int64_t)((z2 >> 16) % 5) - 2)
-                                                    : q * q;
-    } else {
-      const rtk::D3 d = rtk::normalized(rtk::mk(unit(z0) - 0.5, unit(z1) - 0.5, unit(z2) - 0.5));
-      const rtk::D3 o = rtk::mk(unit(mix(z2)) * 8 - 4, unit(mix(z0)) * 8 - 4, unit(mix(z1)) * 8 - 4);
-      const double r = 0.1 + unit(mix(mix(z2))) * 3.0;
-      const double b = 2.0 * ((o.x * d.x + o.y * d.y) + o.z * d.z);
-      const double c = ((o.x * o.x + o.y * o.y) + o.z * o.z) - r * r;
-      const double disc = b * b - 4.0 * rtk::dot(d, d) * c;
-      x = (z2 & 1) ? disc : (o.x * o.x + o.y * o.y) + o.z * o.z;
-    }
-    if (!rtk::sqrt_core_ok(x)) continue;
-    volatile double vx = x;  // the reference computed apart
-    const double want = __builtin_sqrt(vx), got = rtk::sqrt_core(x);
-    atomicAdd(&out[kind], 1ull);
-    if (!same(want, got)) {
-      atomicAdd(&out[3 + kind], 1ull);
-      out[6] = __double_as_longlong(x);
-    }
-  }
-}
-
 }  // namespace
-
-extern "C" int sqrtcheck_run(unsigned long long seed, unsigned long long n, unsigned long long *counts) {
-  unsigned long long *d = nullptr;
-  hipError_t e = hipMalloc(&d, 7 * sizeof(unsigned long long));
-  if (e != hipSuccess) return (int)e;
-  e = hipMemset(d, 0, 7 * sizeof(unsigned long long));
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(sqrt_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, (uint64_t)seed, (uint64_t)n, d);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) e = hipMemcpy(counts, d, 7 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-  (void)hipFree(d);
-  return (int)e;
-}
 
 // counts[14]: per kind {tested, length class in the fast range, mismatches},
 // then the last mismatching (a.x, a.y) bit patterns.  Returns 0 on success,

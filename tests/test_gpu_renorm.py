@@ -30,23 +30,3 @@ def test_renormalized_bit_identical_on_device(seed):
         assert bad == 0, f"kind {kind}: {bad} mismatches, last a.x={c[12]:#x} a.y={c[13]:#x}"
     # the renormalised directions nearly always take the fast path
     assert c[1] > 0.99 * n and 0 < c[7] < n
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("seed", [5, 20261017])
-def test_sqrt_core_bit_identical_on_device(seed):
-    """rtk::sqrt_core (the compiler's fp64 sqrt expansion without its range
-    handling, used by length() and the exact tests' discriminants) equals
-    __builtin_sqrt bit for bit on [2^-767, DBL_MAX]: 3 x 4M operands over every
-    exponent, next to perfect squares and the range ends, and ray-sphere
-    discriminants / squared lengths."""
-    import torch  # noqa: F401
-
-    lib = C.CDLL(LIB)
-    lib.sqrtcheck_run.argtypes = [C.c_ulonglong, C.c_ulonglong, C.POINTER(C.c_ulonglong)]
-    counts = (C.c_ulonglong * 7)()
-    n = 1 << 22
-    assert lib.sqrtcheck_run(seed, n, counts) == 0
-    c = list(counts)
-    assert c[0] == n and c[1] > 0.9 * n and c[2] > 0.5 * n, c
-    assert c[3] == c[4] == c[5] == 0, f"mismatches {c[3:6]}, last operand bits {c[6]:#x}"
