@@ -1178,64 +1178,6 @@ __device__ __forceinline__ unsigned long long next_group(unsigned long long todo
   return __ballot(key == kf) & todo;
 }
 
-// The nearest-first scan of sweep_closest's camera-ray candidates.  Lane j <
-// seen holds candidate j (cand[j]) and tl, a lower bound of every t the
-// reference's test (sphere.h:26-59) can return for that sphere on a ray from
-// P (the camera position, every lane's origin): with D = |C - P| and the
-// camera grid's grown radius R = |r|(1 + 1e-6) + 1e-6 (D + diameter)
-// (rt_lightgrid.h: covers |d| != 1 and the rounding of the computed root),
-// every root is >= (D - R)(1 - 1e-9) when the sphere lies wholly ahead of P
-// for every lane's direction -- its angular radius asin(R / D) plus the
-// bound's widest angle theta plus its angle from the axis under pi/2, every
-// lane's d within theta of the axis and on its side (checked) -- and the only
-// other root it can give, the tangent one kept at disc == 0 (sphere.h:43-47),
-// is >= -(D + R)(1 + 1e-9); a sphere containing P (D <= R), or NaN data,
-// gets -inf.  Candidates are visited by ascending (tl, index); a lane stops
-// at the first whose tl exceeds its best t: every later candidate can only
-// give a t > best, so neither a smaller t nor a tie -- the lexicographic
-// (t, index) minimum is unchanged (the camera grid's argument, with the
-// wave's candidate set as the cell).
-template <typename T>
-__device__ __forceinline__ void sorted_scan(const SphGeo *__restrict__ g, const double *__restrict__ rad,
-                                            const BvhArgs &bv, const Bound &B, bool gact, D3 d, int seen,
-                                            const __attribute__((address_space(3))) int *cand, const double &bt,
-                                            Work &work, T &&test) {
-  const int lane = (int)(threadIdx.x & 63);
-  const bool fwd = B.cull && __ballot(gact && !(d.x * B.ax + d.y * B.ay + d.z * B.az > 0.0)) == 0;
-  const double ct = __builtin_sqrt(B.cos2);
-  int ci = 0;
-  double tl = -__builtin_inf();
-  if (lane < seen) {
-    ci = cand[lane];
-    const SphGeo s = g[RT_CK(kCkSphere, ci, 1LL << 30)];
-    const double vx = s.cx - B.px, vy = s.cy - B.py, vz = s.cz - B.pz;
-    const double D = __builtin_sqrt((vx * vx + vy * vy) + vz * vz);
-    const double R = rad[ci] * (1.0 + 1e-6) + 1e-6 * (D + bv.diam);
-    if (D > R) {
-      const double sb = R / D, cb = __builtin_sqrt(1.0 - sb * sb);
-      const bool ahead = fwd && (vx * B.ax + vy * B.ay + vz * B.az) / D > B.sin_t * cb + ct * sb + 1e-9;
-      tl = ahead ? (D - R) * (1.0 - 1e-9) : -(D + R) * (1.0 + 1e-9);
-    }
-  }
-  int rank = 0;  // position by ascending (tl, index); the ids are distinct
-  for (int k = 0; k < seen; ++k) {
-    const double tk = lane_bcast(tl, k);
-    const int ik = __builtin_amdgcn_readlane(ci, k);
-    rank += (tk < tl || (tk == tl && ik < ci)) ? 1 : 0;
-  }
-  for (int r = 0; r < seen; ++r) {
-    const int k = __builtin_ctzll(__ballot(lane < seen && rank == r));
-    const int i = __builtin_amdgcn_readlane(ci, k);
-    const double tk = lane_bcast(tl, k);
-    const bool want = gact && !(bt < tk);
-    if (__ballot(want) == 0) break;
-    if (want) {
-      work.exact += 1;
-      test(i);
-    }
-  }
-}
-
 // Scene::find_intersection (scene.h:41-61): all candidate spheres in file
 // order, strict '<' (so ties keep the lowest index), t starts at 1e20.
 // kFast: the default configuration only (ordered 4-wide BVH walk); the other
@@ -1301,19 +1243,6 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       RT_ACC(work, 0, tb);
       RT_CNT(work, sweeps, 1);
       int seen = 0;
-      // Camera rays (key -1, every lane leaving P itself): the candidates are
-      // collected first (their ids in the wave's walk-stack LDS, unused until a
-      // walk) and tested nearest first, each lane stopping at the first whose
-      // least possible t exceeds its best (sorted_scan, below).  Other groups
-      // test the candidates of each 64-sphere step in file order.
-      bool sorted = false;
-      if constexpr (kFast) {
-        sorted = bv.ostk_off >= 0 && bv.odepth >= 1 && __builtin_amdgcn_readlane(key, fl) < 0 &&
-                 __ballot(gact && !(o.x == B.px && o.y == B.py && o.z == B.pz)) == 0;
-      }
-      typedef __attribute__((address_space(3))) int LdsI32;
-      LdsI32 *cand = reinterpret_cast<LdsI32 *>(ordered_stack_lds(bv) - lane);
-      bool loose = false;
       for (int base = 0; base < n; base += 64) {
         RT_T0(tc);
         unsigned long long mask = candidates<kCull>(g, rad, n, base, B);
@@ -1322,16 +1251,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
         seen += __popcll(mask);
         if (have_bvh && seen > bv.min_cands) {  // loose bound: this group walks the BVH
           need = need || gact;
-          loose = true;
           break;
-        }
-        if (sorted) {
-          if (seen > 64) {  // more candidates than lanes: file order from here on
-            sorted = false;
-          } else {
-            if ((mask >> lane) & 1ull) cand[seen - __popcll(mask) + __popcll(mask & ((1ull << lane) - 1ull))] = base + lane;
-            continue;
-          }
         }
         RT_T0(tt);
         if (gact) {
@@ -1346,7 +1266,6 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
         }
         RT_ACC(work, 2, tt);
       }
-      if (sorted && !loose && seen > 0) sorted_scan(g, rad, bv, B, gact, d, seen, cand, bt, work, test);
     } else {
       for (int base = 0; base < n; base += 64) {
         unsigned long long mask = candidates<false>(g, rad, n, base, Bound{});

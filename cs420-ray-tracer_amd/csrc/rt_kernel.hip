@@ -94,6 +94,8 @@ struct RenderArgs {
   int dq_cap;                     // entries per shard segment; 0 = no deferral
   int merge_q;                    // kStackMerge: LDS ray-queue entries per wave (16..64)
   int nsingle;                    // kStackMerge: the first nsingle tile slots (heaviest class) get a wave each
+  int merge_end;                  // kStackMerge: slots [nsingle, merge_end) go kMergeTiles per wave, the rest
+                                  // (the launch's tail: its lightest tiles) one per wave again
   int pix_off;                    // kStackMerge: LDS offset of the wave's finished pixels (flush_tile)
   int rows_dword;                 // kStackMerge: every 8-pixel tile row starts dword aligned (flush_tile)
   int defer_level;                // kStackMerge: rays of this reflection level and deeper are deferred
@@ -663,17 +665,21 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
   while (true) {
     // the group's tile slots: [base, base + nt) -- one slot for the first nsingle
     // groups (the heaviest tiles: their own reflection rays fill the wave, and
-    // a frame's critical path is its slowest wave), kMergeTiles after them
-    const int ntiles = kernarg_late<true, offsetof(RenderArgs, ntiles)>(a.ntiles);
+    // a frame's critical path is its slowest wave), kMergeTiles up to
+    // merge_end, then one slot per group again (the launch's last, lightest
+    // tiles: the waves that end a launch are short, so fewer slots idle while
+    // the last ones finish)
     const int ns = kernarg_late<true, offsetof(RenderArgs, nsingle)>(a.nsingle);
-    const int base = group < ns ? group : ns + (group - ns) * kMergeTiles;
-    const int nt = group < ns ? 1 : (ntiles - base < kMergeTiles ? ntiles - base : kMergeTiles);
+    const int me = kernarg_late<true, offsetof(RenderArgs, merge_end)>(a.merge_end);
+    const int nm = (me - ns + kMergeTiles - 1) / kMergeTiles;
+    const int base = group < ns ? group : (group < ns + nm ? ns + (group - ns) * kMergeTiles : me + (group - ns - nm));
+    const int nt = group < ns || group >= ns + nm ? 1 : (me - base < kMergeTiles ? me - base : kMergeTiles);
     bool tile_pass = false;
     if (__ballot(act) == 0) {
       if (next < nt) {  // camera rays of the next tile: camera.h:17-25, main.cpp:151-154 (as trace_tile)
         const int *perm = kernarg_late<true, offsetof(RenderArgs, perm)>(a.perm);
         const int slot = base + next;
-        const int tile = RT_CK(kCkTile, perm ? perm[RT_CK(kCkTile, slot, ntiles)] : slot, ntiles);
+        const int tile = RT_CK(kCkTile, perm ? perm[RT_CK(kCkTile, slot, a.ntiles)] : slot, a.ntiles);
         const int ntx = kernarg_late<true, offsetof(RenderArgs, ntx)>(a.ntx);
         const int tx = tile % ntx, ty = tile / ntx;
         const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
@@ -1396,6 +1402,9 @@ struct rt_ctx {
   // share their reflection rays' passes (class >= 1 there: 0.2285 -> 0.2364 ms
   // per frame, profiles/r3c/ab_single.log)
   int single_class = -1;
+  // RT_HIP_TAIL: multi-frame launches give their last tiles (the lightest, about
+  // one per wave slot of the chip) a wave each (merge_end); 0: four per wave to the end
+  int tail = 1;
   // RT_HIP_XCD_FRAMES: multi-frame launches put every frame of a tile group on
   // one XCD (render_kernel).  -1 (default): for scenes with the uniform grid
   // (large scenes, whose lists and nodes outgrow an XCD's L2: synth10k 2.58 ->
@@ -1809,6 +1818,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   }
   const int *perm = nullptr;
   int nsingle = 0;
+  long long tail = 0;
   // The heavy-first order pays off when a launch has many more tiles than the
   // chip has wave slots; a small launch (a hybrid driver's 64x64 tile) keeps
   // scanline order and skips building and uploading one (which waits for the
@@ -1823,7 +1833,11 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       long long heavy = 0;
       for (int k = sc; k < kSchedClasses; k++) heavy += c->perm_cls[k];
       nsingle = (int)std::min<long long>(heavy, ntiles);
-      nslots = nsingle + (ntiles - nsingle + kMergeTiles - 1) / kMergeTiles;
+      // multi-frame launches end on their lightest tiles one per wave: about
+      // as many as the chip holds waves (12 per CU), over the launch's frames
+      if (c->tail && nf > 1)
+        tail = std::min<long long>(ntiles - nsingle, ((long long)c->n_cu * 12 + nf - 1) / nf);
+      nslots = nsingle + (ntiles - nsingle - tail + kMergeTiles - 1) / kMergeTiles + tail;
     }
   }
   const bool xcd_frames = nf > 1 && (c->xcd_frames > 0 || (c->xcd_frames < 0 && bv.ug.on));
@@ -1861,6 +1875,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.dq_cap = 0;
   ra.merge_q = c->merge_q;
   ra.nsingle = nsingle;
+  ra.merge_end = (int)(ntiles - tail);
   // merge_tiles' pixel bytes: after the scene and the walk stacks, where render_kernel's park/queue region starts
   ra.pix_off = (int)(((lds_layout(kLds, c->nsph, c->nlight, bv.nnodes).end + 31) & ~(size_t)31) +
                      (bv.ordered ? (size_t)kWg * bv.odepth * 64 * sizeof(int2) : 0));
@@ -2058,6 +2073,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BEHIND_GRID")) c->ug_mode = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_GRID_CLOSEST")) c->ug_closest = std::atoi(e) != 0 ? 1 : 0;  // (see ug_closest)
   if (const char *e = std::getenv("RT_HIP_XCD_FRAMES")) c->xcd_frames = std::max(-1, std::min(1, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_TAIL")) c->tail = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_GRID_CELLS")) c->ug_cells = std::max(0.05, std::min(64.0, std::atof(e)));
   if (const char *e = std::getenv("RT_HIP_SINGLE_CLASS"))
     c->single_class = std::max(0, std::min(kSchedClasses, std::atoi(e)));
