@@ -7,7 +7,7 @@
 ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
 TAG="${TAG:-r2}"
 OUT="$ROOT/gpurun_out/prof_$TAG"
-WORKLOADS="${WORKLOADS:-synth200_1920x1080_d4 complex_1920x1080_d4 synth10k_3840x2160_d6}"
+WORKLOADS="${WORKLOADS:-synth200_1920x1080_d4 complex_1920x1080_d4 complex_3840x2160_d4 synth10k_3840x2160_d6}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
@@ -16,14 +16,8 @@ echo "bench: $(head -c 300 "$OUT/bench.json")"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
   python3 "$ROOT/bench.py" --no-cpu-baseline --no-also --no-extras > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err" || { echo "trace failed"; tail -5 "$OUT/trace_bench.err"; exit 1; }
 echo "trace ok"
-# PMC passes: one-wave heavy tiles off (RT_HIP_SINGLE_CLASS=4), so the
-# bench's one-frame stats launch has the per-frame grid of its multi-frame
-# launches (make_pmc_json.py counts frames by grid size); it changes nothing
-# in multi-frame launches
-export RT_HIP_SINGLE_CLASS=4
-# and the deferred kernel in every launch (one-frame launches skip it by
-# default), so that stats launch also has the multi-frame launches' kernel split
-export RT_HIP_DEFER=1
+# PMC passes: make_pmc_json.py folds the multi-frame launches only (32
+# frames each at --steps 32 --warmup 16), so the product library runs as is
 for w in $WORKLOADS; do
   i=0; mkdir -p "$OUT/pmc_$w"
   while IFS= read -r counters; do

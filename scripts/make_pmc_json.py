@@ -3,12 +3,11 @@
 
   python scripts/make_pmc_json.py WORKLOAD PMC_DIR [KERNEL_SUBSTR]
 
-Per FRAME: a render dispatch of g threads renders g / g_min frames (g_min =
-the smallest render dispatch of the run, bench.py's single-frame stats launch;
-multi-frame launches are rt_render_frames_async), and every counter is summed
-over the render dispatches -- each with the render_deferred dispatch that
-follows it (the launch's deep reflection rays) -- and divided by the frames
-they rendered:
+Per FRAME: every counter is summed over the multi-frame render dispatches
+(the largest render grid of the run; FRAMES frames each, bench.py's
+--frames-per-launch, default 32) -- each with the render_deferred dispatch
+that follows it (the launch's deep reflection rays) -- and divided by the
+frames they rendered:
   hbm_bytes_per_frame = (2 * FETCH_SIZE + WRITE_SIZE) * 1024  (rocprofv3 reports
       KiB; FETCH_SIZE doubled: MI355X_MICROARCH.md's gfx950 correction -- it
       reports half the bytes of 128-B requests; fetch_bytes / write_bytes are
@@ -30,6 +29,7 @@ import os
 import sys
 
 SIMDS, XCDS = 1024, 8
+FRAMES = int(os.environ.get("FRAMES", "32"))  # frames per multi-frame launch of the PMC runs (bench.py's default)
 
 
 def main():
@@ -42,15 +42,25 @@ def main():
         main = [r for r in rows if "render_deferred" not in r["Kernel_Name"]]
         if not main:
             continue
-        gmin = min(int(r["Grid_Size"]) for r in main)
+        # the multi-frame launches only (the largest render grid; bench.py's
+        # one-frame ray-count launch has the one-frame kernel split), each with
+        # the render_deferred dispatch that follows it (its deep reflection rays)
+        gmax = max(int(r["Grid_Size"]) for r in main)
+        last_main_grid, keep = None, set()
+        for r in sorted({(int(r["Dispatch_Id"]), r["Kernel_Name"], int(r["Grid_Size"])) for r in rows}):
+            did, name, grid = r
+            if "render_deferred" not in name:
+                last_main_grid = grid
+            if last_main_grid == gmax:
+                keep.add(did)
         agg = collections.defaultdict(float)
         frames = collections.defaultdict(float)
         for r in rows:
-            # render_deferred (the deep rays of the render launch just before it) adds its
-            # counters to that launch; frames are counted on the render launches only
+            if int(r["Dispatch_Id"]) not in keep:
+                continue
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
             if "render_deferred" not in r["Kernel_Name"]:
-                frames[r["Counter_Name"]] += int(r["Grid_Size"]) / gmin
+                frames[r["Counter_Name"]] += FRAMES
         for k, v in agg.items():
             vals[k] = v / frames[k]
     out = {}
