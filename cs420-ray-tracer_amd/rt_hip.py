@@ -278,6 +278,12 @@ class Scene:
             pass
 
 
+def camera_array(cams) -> C.Array:
+    """The rt_camera array rt_render_frames_async takes, built once (a caller
+    that launches the same frames repeatedly keeps it off its launch path)."""
+    return (rt_camera * len(cams))(*cams)
+
+
 def rows_for_shard(height: int, band: int, rank: int, world: int) -> rt_rows:
     """Cyclic bands of `band` rows: rank r renders bands r, r+G, r+2G, ...
     (rt_rows_for_shard: the one layout ray_hip --gpus and bench.py share)."""
@@ -333,8 +339,9 @@ class Renderer:
     def render_frames_async(self, cams, width: int, height: int, depth: int, rows: rt_rows | None,
                             out_device_ptr: int, frame_stride: int):
         """rt_render_frames_async: len(cams) frames (<= MAX_FRAMES) in one launch, frame f
-        (seen through cams[f]) at out_device_ptr + f * frame_stride."""
-        arr = (rt_camera * len(cams))(*cams)
+        (seen through cams[f]) at out_device_ptr + f * frame_stride.  `cams` may
+        be a ctypes array of rt_camera built beforehand (camera_array)."""
+        arr = cams if isinstance(cams, C.Array) else (rt_camera * len(cams))(*cams)
         _check(self._L.rt_render_frames_async(self._ctx, arr, len(cams), width, height, depth,
                                             C.byref(rows) if rows is not None else None,
                                             C.c_void_p(out_device_ptr), frame_stride),

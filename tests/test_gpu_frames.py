@@ -142,8 +142,8 @@ def test_frames_antialias(gpu_renderer):
 
 
 @pytest.mark.parametrize("env", [{"RT_HIP_LDS_SCENE": "1"}, {"RT_HIP_SCHED": "0"}, {"RT_HIP_STACK": "1"},
-                                 {"RT_HIP_STACK": "4"}],
-                         ids=["lds-scene", "scanline", "global-stack", "merge"])
+                                 {"RT_HIP_STACK": "4"}, {"RT_HIP_TAIL": "0"}],
+                         ids=["lds-scene", "scanline", "global-stack", "merge", "no-single-tail"])
 def test_frames_knobs(monkeypatch, env):
     import rt_hip
 
