@@ -72,6 +72,9 @@ FLOP_PER_CULL = 34          # rtk::keep(): 3 sub, |v.a| 5, v x a 9, |v x a|^2 5,
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X vector FP64 (spec; 256 CU x 2.4 GHz x 128 FLOP/clk)
 HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 BAND = 8
+# back-to-back warmup launches after the host-side builds (clocks settle; measure());
+# BENCH_WARM_BUSY_S overrides it for the A/B that measured it
+WARM_BUSY_S = float(os.environ.get("BENCH_WARM_BUSY_S", "0.05"))
 # the sources the PMC record in profiles/pmc_traffic.json must have been measured with
 KERNEL_SOURCES = ("rt_kernel.hip", "rt_device.h", "rt_bvh.cpp", "rt_bvh.h", "rt_lightgrid.cpp", "rt_lightgrid.h",
                   "rt_sched.cpp", "rt_sched.h")
@@ -425,6 +428,25 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     # 0.38 ms idle gap ran 2.9 % slower than the next, profiles/r3u/trace96);
     # the timed launches' durations are read after the timed region
     frames(max(warmup, F))
+    # ... and then back-to-back launches for at least WARM_BUSY_S of GPU time:
+    # the first warmup launch waits for the host-side builds (camera grid, tile
+    # order: 30-100 ms with the GPU idle), and after an idle gap that long the
+    # GPU's clocks need more than one launch to come back -- a 20-frame launch
+    # after 20 ms idle runs 8 % slower, after 1 ms or less it does not
+    # (profiles/r4e/idle_gap.log) -- so the timed launches would otherwise pay
+    # for the build.  Every rank runs the same number of batches (collectives).
+    torch.cuda.synchronize()
+    t_w = time.perf_counter()
+    frames(F)
+    torch.cuda.synchronize()
+    per_batch = time.perf_counter() - t_w
+    extra = max(0, -(-WARM_BUSY_S // max(per_batch, 1e-6)) - 1)
+    if dist_on:
+        n_t = torch.tensor([extra], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(n_t, op=dist.ReduceOp.MAX)
+        extra = n_t.item()
+    for _ in range(int(min(extra, 1000))):
+        frames(F)
     info_warm = info_or_none(r)  # the camera grid / tile order the timed launches use (built in warmup), host only
     timed_launches = len(rt_frames.batch_sizes(steps, F)) if steps > 0 else 0
     if dist_on:
@@ -512,7 +534,8 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
             "launches_timed": len(ktimes), "rows_per_rank": R, "tests_exact": tests_exact,
             "tests_cull": tests_cull, "cull": cull, "gather_ms_per_batch": gather_ms,
             "rank_kernel_ms_per_frame": rank_kernel_ms, "world_size_seen": seen_world,
-            "warmup_frames_rendered": max(warmup, F), "launch_frames": rt_frames.batch_sizes(steps, F),
+            "warmup_frames_rendered": max(warmup, F) + (1 + int(min(extra, 1000))) * F,
+            "launch_frames": rt_frames.batch_sizes(steps, F),
             "camera_grid": camera_grid, "sphere_grids": sphere_grids, "behind_grid": behind_grid, **extra}
 
 
