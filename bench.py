@@ -440,12 +440,12 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
     frames(F)
     torch.cuda.synchronize()
     per_batch = time.perf_counter() - t_w
-    extra = max(0, -(-WARM_BUSY_S // max(per_batch, 1e-6)) - 1)
+    warm_extra = int(min(1000, max(0, -(-WARM_BUSY_S // max(per_batch, 1e-6)) - 1)))
     if dist_on:
-        n_t = torch.tensor([extra], dtype=torch.float64, device=f"cuda:{device}")
+        n_t = torch.tensor([warm_extra], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(n_t, op=dist.ReduceOp.MAX)
-        extra = n_t.item()
-    for _ in range(int(min(extra, 1000))):
+        warm_extra = int(n_t.item())
+    for _ in range(warm_extra):
         frames(F)
     info_warm = info_or_none(r)  # the camera grid / tile order the timed launches use (built in warmup), host only
     timed_launches = len(rt_frames.batch_sizes(steps, F)) if steps > 0 else 0
@@ -534,7 +534,7 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
             "launches_timed": len(ktimes), "rows_per_rank": R, "tests_exact": tests_exact,
             "tests_cull": tests_cull, "cull": cull, "gather_ms_per_batch": gather_ms,
             "rank_kernel_ms_per_frame": rank_kernel_ms, "world_size_seen": seen_world,
-            "warmup_frames_rendered": max(warmup, F) + (1 + int(min(extra, 1000))) * F,
+            "warmup_frames_rendered": max(warmup, F) + (1 + warm_extra) * F,
             "launch_frames": rt_frames.batch_sizes(steps, F),
             "camera_grid": camera_grid, "sphere_grids": sphere_grids, "behind_grid": behind_grid, **extra}
 
