@@ -1581,19 +1581,26 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
 }
 
 // Closest hit of camera rays through the camera grid (rt_lightgrid.h
-// build_point_grid): the rays leave the grid's point P exactly, so every
-// sphere the reference's test can report lies on the list of the cell of d;
-// the list ascends by a lower bound of the sphere's t, so the scan stops at
-// the first entry whose bound exceeds the best t found so far (every later
-// entry can only give a larger t: no strict-< win, no tie).  The result is
-// the lexicographic (t, index) minimum over all spheres, as sweep_closest's.
-// A lane whose direction cannot be binned tests every sphere.
+// build_point_grid's cube map and lists, built on the device by
+// rt_kernel.hip's cg_bin_kernel / cg_sort_kernel): the rays leave the grid's
+// point P exactly, so every sphere the reference's test can report lies on
+// the list of the cell of d or on the grid's global list (spheres containing
+// or nearly containing P, tlo = -inf); a cell's list ascends by a lower bound
+// tlo of the sphere's t, so the scan stops at the first entry whose bound
+// exceeds the best t found so far (every later entry can only give a larger t:
+// no strict-< win, no tie).  The result is the lexicographic (t, index)
+// minimum over all spheres, as sweep_closest's.  A lane whose direction cannot
+// be binned tests every sphere; a lane whose cell overflowed its K slots (or a
+// frame whose grid was refused: too many global spheres) is told to sweep.
+constexpr int kCgMaxGlobal = 32;  // spheres containing the camera (on every list); more: no grid
 struct CgArgs {
-  const int32_t *start;  // [6N^2 + 1]
-  const int2 *ent;       // (sphere, tlo bits)
-  int N;
-  int on;  // the launch's frames all share the grid's camera position
-  long long nent;  // list entries (RT_CHECK bound)
+  const int32_t *count;   // [grid][6N^2] entries of each cell (> K: overflowed, its rays sweep)
+  const int2 *ent;        // [grid][6N^2][K] (sphere, tlo bits), ascending by (tlo, index)
+  const int32_t *glist;   // [grid][kCgMaxGlobal] the global spheres, file order
+  const int32_t *gcount;  // [grid] how many (> kCgMaxGlobal: no grid for that frame)
+  int N, K;
+  int on;         // the launch's frames have grids
+  int per_frame;  // 1: frame f scans grid f; 0: every frame grid 0 (one camera position)
 };
 // The scan of one grid's cell list for the closest hit; this lane's grid
 // starts at start + sbase (camera grid: sbase = 0; sphere grids: the grid of
@@ -1634,8 +1641,57 @@ __device__ __forceinline__ int grid_closest(const SphGeo *__restrict__ g, int n,
   return bi;
 }
 __device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, bool act, D3 o, D3 d,
-                                           const CgArgs &cg, double &best_t, Work &work) {
-  return grid_closest(g, n, act, o, d, cg.start, cg.ent, cg.N, 0, 6LL * cg.N * cg.N + 1, cg.nent, best_t, work);
+                                           const CgArgs &cg, int grid, bool &sweep, double &best_t, Work &work) {
+  const double a = dot(d, d);
+  const double a4 = 4.0 * a, a2 = 2.0 * a;
+  double bt = kInf, bn = __builtin_inf();
+  int bi = -1;
+  sweep = false;
+  const int ng = __builtin_amdgcn_readfirstlane(cg.gcount[grid]);
+  if (ng > kCgMaxGlobal) {  // this frame has no grid
+    sweep = act;
+    best_t = bt;
+    return bi;
+  }
+  const bool fast = a2_ok(a2);
+  const long long cells = 6LL * cg.N * cg.N;
+  for (int k = 0; k < ng; ++k) {  // the global list: every lane, tlo = -inf
+    const int i = RT_CK(kCkSphere, cg.glist[(size_t)grid * kCgMaxGlobal + k], n);
+    if (act) {
+      work.exact += 1;
+      closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi);
+    }
+  }
+  long long cb = 0;
+  int len = 0;
+  bool all = false;
+  if (act) {
+    const int c = lg_cell_rcp((float)d.x, (float)d.y, (float)d.z, cg.N);
+    if (c < 0) {
+      all = true;
+      len = n;
+    } else {
+      const long long gc = (long long)grid * cells + RT_CK(kCkCgStart, c, cells);
+      len = cg.count[gc];
+      if (len > cg.K) {  // overflowed: this lane sweeps
+        sweep = true;
+        len = 0;
+      }
+      cb = gc * cg.K;
+    }
+  }
+  int k = 0;
+  int2 e = (len > 0 && !all) ? cg.ent[cb] : make_int2(0, (int)0xff800000u);  // -inf
+  while (k < len) {
+    const int i = all ? k : RT_CK(kCkSphere, e.x, n);
+    if ((double)__int_as_float(e.y) > bt) break;
+    ++k;
+    if (k < len && !all) e = cg.ent[cb + k];  // the next entry, loaded during this test
+    work.exact += 1;
+    closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi);
+  }
+  best_t = bt;
+  return bi;
 }
 
 // Closest hit of reflection rays through the sphere grids (rt_lightgrid.h

@@ -260,7 +260,7 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
 template <bool kCull, bool kArgMem = false, bool kFast = false>
 __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
                                            const BvhArgs &bv, bool alive, D3 o, D3 d, int key, Work &work,
-                                           double &bt_out, bool cam_pass = false) {
+                                           double &bt_out, bool cam_pass = false, int frame = 0) {
   double bt = kInf;
   RT_T0(t_cl);
   int bi = -1;
@@ -269,7 +269,20 @@ __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const d
   bool swept = false;
   if constexpr (kFast && kArgMem) {
     if (cam_pass) {
-      bi = cam_closest(g, n, alive, o, d, kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{}), bt, work);
+      bool rest;
+      {
+        const CgArgs &cg = kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{});
+        bi = cam_closest(g, n, alive, o, d, cg, cg.per_frame ? frame : 0, rest, bt, work);
+      }
+      if (__ballot(rest)) {  // lanes of an overflowed cell, or a frame without a grid, sweep
+        double bt2 = kInf;
+        const int bi2 = sweep_closest<kCull, kFast>(g, rad, n, rest, o, d, key,
+                                                    kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt2, work);
+        if (rest) {
+          bi = bi2;
+          bt = bt2;
+        }
+      }
       swept = true;
     } else if (kernarg_late<true, offsetof(RenderArgs, sg)>(SgArgs{}).on) {
       // reflection rays through the sphere grid of the sphere they leave; the
@@ -734,7 +747,8 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     double refl = 0.0;
     double bt;
     const int bi = closest_hit<kCull, true, kFast>(g, rad, a.n, a.bv, act, o, d, key, work, bt,
-                                             kFast && tile_pass && kernarg_late<true, offsetof(RenderArgs, cg)>(a.cg).on);
+                                             kFast && tile_pass && kernarg_late<true, offsetof(RenderArgs, cg)>(a.cg).on,
+                                             frame);
     shade_hit<kCull, true, kFast>(g, rad, mat, slight, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft, bi, bt,
                                   work, c_shadow, outcome, color, refl, no, nd, nkey);
     const unsigned sidx = pix + ca.fpx;
@@ -1245,6 +1259,142 @@ __global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// The camera grid, built on the device for each camera position of a launch:
+// build_point_grid (rt_lightgrid.cpp) on the GPU.  cg_bin_kernel (one wave per
+// grid and sphere) lists the sphere's two disks seen from the grid's point P
+// -- along +u with tlo = (D - R)(1 - 1e-9), along -u (the negative tangent
+// root, sphere.h:43-47) with -(D + R)(1 + 1e-9), R the light grids' grown
+// radius, each disk's angular radius asin(R / D) + kLgSlack -- in every cell
+// they meet, by the host builder's patch hierarchy and tests (faces, blocks of
+// 8 x 8 tiles, tiles of 8 x 8 cells -- a tile well inside a disk takes all its
+// cells untested -- cells against the per-(i, j) table), the same patches and
+// margins; a sphere that contains (or nearly contains) P, or has non-finite
+// data, goes to the grid's global list.  A cell keeps K entries; one that
+// overflows is marked by its count, and its rays sweep.  cg_sort_kernel (one
+// thread per cell) orders each list by (tlo, index).
+struct CgBuild {
+  const SphGeo *geo;
+  const double *rad;
+  const CubePatch *faces, *blocks, *tiles;
+  const double *cell_cbsb;
+  int32_t *count, *glist, *gcount;
+  int2 *ent;
+  int n, N, NT, NB, K, ngrid;
+  double px[RT_MAX_FRAMES], py[RT_MAX_FRAMES], pz[RT_MAX_FRAMES], diam[RT_MAX_FRAMES];
+};
+static_assert(sizeof(CgBuild) <= 4096, "CgBuild exceeds the kernel-argument segment");
+
+__device__ __forceinline__ float float_down(double x) {  // x rounded down to fp32
+  float f = (float)x;
+  if ((double)f > x) {
+    const int b = __float_as_int(f);
+    f = f == 0.0f ? -0x1p-149f : __int_as_float(f > 0.0f ? b - 1 : b + 1);
+  }
+  return f;
+}
+
+__global__ __launch_bounds__(64) void cg_bin_kernel(const CgBuild a) {
+  const int s = (int)blockIdx.x, grid = (int)blockIdx.y;
+  if (s >= a.n || grid >= a.ngrid) return;
+  const int lane = (int)(threadIdx.x & 63);
+  const long long cells = 6LL * a.N * a.N;
+  const SphGeo sp = a.geo[s];
+  const double vx = sp.cx - a.px[grid], vy = sp.cy - a.py[grid], vz = sp.cz - a.pz[grid];
+  const double D = __builtin_sqrt(vx * vx + vy * vy + vz * vz);
+  const double R = a.rad[s] * (1.0 + 1e-6) + 1e-6 * (D + a.diam[grid]);
+  if (!__builtin_isfinite(D) || !__builtin_isfinite(R) || !(D > R)) {
+    if (lane == 0) {  // contains (or nearly) P, or non-finite: every direction, tlo = -inf
+      const int k = atomicAdd(&a.gcount[grid], 1);
+      if (k < kCgMaxGlobal) a.glist[(size_t)grid * kCgMaxGlobal + k] = s;
+    }
+    return;
+  }
+  const double alpha = asin(R / D) + kLgSlack, ca = cos(alpha), sa = sin(alpha);
+  const bool wide = alpha + kLgSlack >= 3.0;
+  const int nb = 6 * a.NB * a.NB;
+  for (int side = 0; side < 2; ++side) {
+    const double sg = side ? -1.0 : 1.0;
+    const double ux = sg * (vx / D), uy = sg * (vy / D), uz = sg * (vz / D);
+    const float tlo = side ? float_down(-(D + R) * (1.0 + 1e-9)) : float_down((D - R) * (1.0 - 1e-9));
+    auto meets = [&](double cx, double cy, double cz, double rad, double cb, double sb) {
+      if (alpha + rad + kLgSlack >= 3.14159) return true;
+      return ux * cx + uy * cy + uz * cz >= ca * cb - sa * sb - 1e-12;
+    };
+    auto meets_p = [&](const CubePatch &p) { return meets(p.cx, p.cy, p.cz, p.rad, p.cb, p.sb); };
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+      const int b = b0 + lane;
+      bool m = false;
+      if (b < nb) m = meets_p(a.faces[b / (a.NB * a.NB)]) && meets_p(a.blocks[b]);
+      unsigned long long bm = __ballot(m);
+      while (bm) {
+        const int bb = __builtin_ctzll(bm);
+        bm &= bm - 1;
+        const int f = bb / (a.NB * a.NB), bj = (bb / a.NB) % a.NB, bi = bb % a.NB;
+        const int ti = bi * kCubeB + (lane & 7), tj = bj * kCubeB + (lane >> 3);
+        bool tm = false, inside = false;
+        if (ti < a.NT && tj < a.NT) {
+          const CubePatch tp = a.tiles[((size_t)f * a.NT + tj) * a.NT + ti];
+          tm = meets_p(tp);
+          inside = tm && alpha < 3.0 && alpha > tp.rad + 1e-3 &&
+                   ux * tp.cx + uy * tp.cy + uz * tp.cz >= cos(alpha - tp.rad - 1e-3);
+        }
+        unsigned long long tmask = __ballot(tm);
+        const unsigned long long imask = __ballot(inside);
+        while (tmask) {
+          const int tl = __builtin_ctzll(tmask);
+          tmask &= tmask - 1;
+          const bool tin = (imask >> tl) & 1ull;
+          const int i = (bi * kCubeB + (tl & 7)) * kCubeT + (lane & 7), j = (bj * kCubeB + (tl >> 3)) * kCubeT + (lane >> 3);
+          bool cm = false;
+          if (i < a.N && j < a.N) {
+            if (tin) {
+              cm = true;
+            } else {  // the cell's patch: centre formed as face_dir does, cos / sin of rad + slack from the table
+              const double fa = -1.0 + (2.0 * i + 1.0) / a.N, fb = -1.0 + (2.0 * j + 1.0) / a.N;
+              double dx, dy, dz;
+              switch (f) {
+                case 0: dx = 1.0, dy = fa, dz = fb; break;
+                case 1: dx = -1.0, dy = fa, dz = fb; break;
+                case 2: dx = fa, dy = 1.0, dz = fb; break;
+                case 3: dx = fa, dy = -1.0, dz = fb; break;
+                case 4: dx = fa, dy = fb, dz = 1.0; break;
+                default: dx = fa, dy = fb, dz = -1.0; break;
+              }
+              const double l = __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+              const size_t ij = (size_t)j * a.N + i;
+              cm = meets(dx / l, dy / l, dz / l, wide ? 3.2 : 0.0, a.cell_cbsb[2 * ij], a.cell_cbsb[2 * ij + 1]);
+            }
+          }
+          if (cm) {
+            const long long gc = (long long)grid * cells + ((long long)f * a.N + j) * a.N + i;
+            const int slot = atomicAdd(&a.count[gc], 1);
+            if (slot < a.K) a.ent[gc * a.K + slot] = make_int2(s, __float_as_int(tlo));
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void cg_sort_kernel(const CgBuild a) {
+  const long long cells = 6LL * a.N * a.N;
+  const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gc >= cells * a.ngrid) return;
+  const int cnt = a.count[gc] < a.K ? a.count[gc] : a.K;
+  int2 *e = a.ent + gc * a.K;
+  for (int k = 1; k < cnt; ++k) {  // insertion sort by (tlo, index); lists are short
+    const int2 x = e[k];
+    const float tx = __int_as_float(x.y);
+    int m = k - 1;
+    while (m >= 0 && (__int_as_float(e[m].y) > tx || (__int_as_float(e[m].y) == tx && e[m].x > x.x))) {
+      e[m + 1] = e[m];
+      --m;
+    }
+    e[m + 1] = x;
+  }
+}
+
 }  // namespace rtk
 
 using namespace rtk;
@@ -1277,20 +1427,24 @@ struct rt_ctx {
   long long lg_nstart = 0, lg_nids = 0;
   int lg_n_opt = 0;            // RT_HIP_SHADOW_GRID_N; 0 = 128, or 768 above kBvhAlwaysAbove spheres
   double lg_max_off = 0.0;
-  // camera grid (rt_lightgrid.h build_point_grid): the closest hit of camera
-  // rays in the merged kFast kernels, built per camera position and cached
-  int cg_mode = 1;    // RT_HIP_CAM_GRID: 0 off, 1 launches of >= kCgMinFrames frames or a repeated position, 2 always
-  int cg_n_opt = 0;   // RT_HIP_CAM_GRID_N; 0 = kCgN
-  int32_t *d_cg_start = nullptr;
+  // camera grids (rt_device.h CgArgs), built on the device per camera
+  // position of a launch (cg_bin_kernel / cg_sort_kernel) and kept while the
+  // positions and the scene stay the same
+  int cg_mode = 1;    // RT_HIP_CAM_GRID: 0 off, 1 (= 2) every launch of the kFast kernels
+  int cg_n_opt = 0;   // RT_HIP_CAM_GRID_N (tuning build); 0 = kCgNStatic / kCgNMoving
+  int32_t *d_cg_count = nullptr, *d_cg_glist = nullptr, *d_cg_gcount = nullptr;
   int2 *d_cg_ent = nullptr;
-  size_t cg_start_cap = 0, cg_ent_cap = 0;
-  int cg_n = 0;
-  long long cg_nent = 0;
-  bool cg_ok = false;                  // the grid for (cg_pos, cg_gen) exists
-  double cg_pos[3] = {0, 0, 0};
-  unsigned long long cg_gen = ~0ull;   // scene_gen it was built (or refused) for
-  double last_pos[3] = {0, 0, 0};      // the previous launch's camera position
-  bool have_last = false;
+  size_t cg_count_cap = 0, cg_ent_cap = 0, cg_glist_cap = 0;  // bytes
+  int cg_n = 0, cg_ngrid = 0;
+  std::vector<double> cg_pos;          // the grids' points (3 per grid)
+  unsigned long long cg_gen = ~0ull;   // scene_gen they were built for
+  struct CgTables {                    // the cube map's patch tables of one N on the device
+    int N = 0, NT = 0, NB = 0;
+    CubePatch *faces = nullptr, *blocks = nullptr, *tiles = nullptr;
+    double *cell = nullptr;
+  };
+  CgTables cg_tab[2];
+  int cg_tab_next = 0;
   std::vector<double> h_sx, h_sy, h_sz, h_sr;  // sphere centres and radii (grid builds)
   // sphere grids (rt_lightgrid.h build_sphere_grids): the closest hit of
   // reflection rays in the kFast kernels, built at upload for the reflective
@@ -1454,7 +1608,6 @@ void free_scene(rt_ctx *c) {
   if (c->d_lg_start) (void)hipFree(c->d_lg_start);
   if (c->d_lg_ids) (void)hipFree(c->d_lg_ids);
   c->d_lg_start = c->d_lg_ids = nullptr;
-  c->cg_ok = false;
   c->cg_gen = ~0ull;
   if (c->d_sg_start) (void)hipFree(c->d_sg_start);
   if (c->d_sg_ent) (void)hipFree(c->d_sg_ent);
@@ -1554,71 +1707,126 @@ LgArgs lg_args(const rt_ctx *c) {
   return g;
 }
 
-constexpr int kCgN = 512;          // camera grid cells per face edge
-constexpr int kCgMinFrames = 8;    // RT_HIP_CAM_GRID=1: launches this long build a grid at once
-constexpr int kCgMaxGlobal = 32;   // spheres containing the camera (on every list)
-constexpr size_t kCgMaxEntries = size_t(64) << 20;
+// camera grid cells per cube-map face edge (profiles/r4e/ab_camgrid_n.log,
+// per frame of 32-frame launches at one position, synth200 / complex: 512
+// 0.1914 / 0.1761 ms, 256 0.1914 / 0.1766, 128 0.1925 / 0.1770, 64 0.1950 /
+// 0.1791, no grid 0.2177 / 0.1980): 256 for a launch at one position, 128 for
+// a grid per frame (a quarter of the cells to build)
+constexpr int kCgNStatic = 256, kCgNMoving = 128;
+constexpr int kCgSlots = 48;  // entries per cell; a cell with more has its rays sweep
 
-// The camera grid for this launch (cg.on = 0: the launch sweeps as before).
-// Used when every frame of the launch has the same camera position; built
-// (host, rt_lightgrid.cpp) when that position or the scene changed, for
-// launches of kCgMinFrames frames or more or a position repeated from the
-// previous launch (a single still frame does not pay for a build).
+// The device patch tables of the cube map with N cells per face edge (two
+// kept; replacing one waits for the launches in flight).
+int cg_tables(rt_ctx *c, int N, const rt_ctx::CgTables *&out) {
+  for (const auto &t : c->cg_tab)
+    if (t.N == N) {
+      out = &t;
+      return RT_OK;
+    }
+  rt_ctx::CgTables &t = c->cg_tab[c->cg_tab_next];
+  c->cg_tab_next ^= 1;
+  RT_TRY(c, hipStreamSynchronize(c->stream));
+  for (void *p : {(void *)t.faces, (void *)t.blocks, (void *)t.tiles, (void *)t.cell})
+    if (p) (void)hipFree(p);
+  t = rt_ctx::CgTables{};
+  std::vector<CubePatch> faces, blocks, tiles;
+  std::vector<double> cell;
+  int NT = 0, NB = 0;
+  cube_tables(N, faces, blocks, tiles, cell, NT, NB);
+  RT_TRY(c, hipMalloc(&t.faces, faces.size() * sizeof(CubePatch)));
+  RT_TRY(c, hipMalloc(&t.blocks, blocks.size() * sizeof(CubePatch)));
+  RT_TRY(c, hipMalloc(&t.tiles, tiles.size() * sizeof(CubePatch)));
+  RT_TRY(c, hipMalloc(&t.cell, cell.size() * sizeof(double)));
+  RT_TRY(c, hipMemcpy(t.faces, faces.data(), faces.size() * sizeof(CubePatch), hipMemcpyHostToDevice));
+  RT_TRY(c, hipMemcpy(t.blocks, blocks.data(), blocks.size() * sizeof(CubePatch), hipMemcpyHostToDevice));
+  RT_TRY(c, hipMemcpy(t.tiles, tiles.data(), tiles.size() * sizeof(CubePatch), hipMemcpyHostToDevice));
+  RT_TRY(c, hipMemcpy(t.cell, cell.data(), cell.size() * sizeof(double), hipMemcpyHostToDevice));
+  t.N = N;
+  t.NT = NT;
+  t.NB = NB;
+  out = &t;
+  return RT_OK;
+}
+
+// grow-only device buffer
+template <class T>
+int grow(rt_ctx *c, T *&p, size_t &cap, size_t bytes) {
+  if (cap >= bytes) return RT_OK;
+  RT_TRY(c, hipStreamSynchronize(c->stream));  // launches in flight may read the old one
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  RT_TRY(c, hipMalloc(&p, bytes));
+  cap = bytes;
+  return RT_OK;
+}
+
+// The camera grids of this launch (cg.on = 0: the launch sweeps as before):
+// one grid when every frame shares the camera position, else one per frame,
+// enqueued on the context's stream ahead of the render kernel; kept while
+// the positions and the scene stay the same.
 int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
   out = CgArgs{};
   if (c->cg_mode == 0 || !c->cull || c->nsph == 0) return RT_OK;
-  const double pos[3] = {cam.px, cam.py, cam.pz};
-  for (int f = 1; f < nf; f++) {
-    const rt_camera &cm = c->fcams[f];
-    if (std::memcmp(cm.position, pos, sizeof pos) != 0) return RT_OK;
-  }
-  const bool repeat = c->have_last && std::memcmp(c->last_pos, pos, sizeof pos) == 0;
-  std::memcpy(c->last_pos, pos, sizeof pos);
-  c->have_last = true;
-  const bool cached = c->cg_gen == c->scene_gen && std::memcmp(c->cg_pos, pos, sizeof pos) == 0;
+  std::vector<double> pos{cam.px, cam.py, cam.pz};
+  bool same = true;
+  for (int f = 1; f < nf; f++) same = same && std::memcmp(c->fcams[f].position, pos.data(), 3 * sizeof(double)) == 0;
+  const int ngrid = same ? 1 : nf;
+  for (int f = 1; f < ngrid; f++) pos.insert(pos.end(), c->fcams[f].position, c->fcams[f].position + 3);
+  const int N = c->cg_n_opt ? c->cg_n_opt : (same ? kCgNStatic : kCgNMoving);
+  const size_t cells = 6 * (size_t)N * N;
+  const bool cached = c->cg_gen == c->scene_gen && c->cg_n == N && c->cg_ngrid == ngrid && c->cg_pos == pos;
   if (!cached) {
-    if (!(c->cg_mode == 2 || nf >= kCgMinFrames || repeat)) return RT_OK;
     const auto t0 = std::chrono::steady_clock::now();
-    const int N = c->cg_n_opt ? c->cg_n_opt : kCgN;
-    double d2 = 0.0;
-    for (int k = 0; k < 3; k++) {
-      const double l = std::min(c->lo[k], pos[k]), h = std::max(c->hi[k], pos[k]);
-      d2 += (h - l) * (h - l);
+    const rt_ctx::CgTables *tab = nullptr;
+    int rc = cg_tables(c, N, tab);
+    if (rc != RT_OK) return rc;
+    if ((rc = grow(c, c->d_cg_count, c->cg_count_cap, ngrid * cells * sizeof(int32_t))) != RT_OK ||
+        (rc = grow(c, c->d_cg_ent, c->cg_ent_cap, ngrid * cells * kCgSlots * sizeof(int2))) != RT_OK ||
+        (rc = grow(c, c->d_cg_glist, c->cg_glist_cap, (size_t)ngrid * (kCgMaxGlobal + 1) * sizeof(int32_t))) != RT_OK)
+      return rc;
+    c->d_cg_gcount = c->d_cg_glist + (size_t)ngrid * kCgMaxGlobal;
+    CgBuild b{};
+    b.geo = c->d_geo;
+    b.rad = c->d_rad;
+    b.faces = tab->faces;
+    b.blocks = tab->blocks;
+    b.tiles = tab->tiles;
+    b.cell_cbsb = tab->cell;
+    b.count = c->d_cg_count;
+    b.glist = c->d_cg_glist;
+    b.gcount = c->d_cg_gcount;
+    b.ent = c->d_cg_ent;
+    b.n = c->nsph;
+    b.N = N;
+    b.NT = tab->NT;
+    b.NB = tab->NB;
+    b.K = kCgSlots;
+    b.ngrid = ngrid;
+    for (int g = 0; g < ngrid; g++) {
+      b.px[g] = pos[3 * g];
+      b.py[g] = pos[3 * g + 1];
+      b.pz[g] = pos[3 * g + 2];
+      double d2 = 0.0;  // the scene's extent with the point (the grown radius' margin)
+      for (int k = 0; k < 3; k++) {
+        const double l = std::min(c->lo[k], pos[3 * g + k]), h = std::max(c->hi[k], pos[3 * g + k]);
+        d2 += (h - l) * (h - l);
+      }
+      b.diam[g] = std::sqrt(d2);
     }
-    std::vector<int32_t> start, ent;
-    const bool ok = build_point_grid(c->h_sx.data(), c->h_sy.data(), c->h_sz.data(), c->h_sr.data(), c->nsph,
-                                     pos[0], pos[1], pos[2], std::sqrt(d2), N, kCgMaxGlobal, kCgMaxEntries, start,
-                                     ent);
-    c->cg_ok = false;
+    RT_TRY(c, hipMemsetAsync(c->d_cg_count, 0, ngrid * cells * sizeof(int32_t), c->stream));
+    RT_TRY(c, hipMemsetAsync(c->d_cg_gcount, 0, ngrid * sizeof(int32_t), c->stream));
+    hipLaunchKernelGGL(cg_bin_kernel, dim3((unsigned)c->nsph, (unsigned)ngrid), dim3(64), 0, c->stream, b);
+    hipLaunchKernelGGL(cg_sort_kernel, dim3((unsigned)((ngrid * cells + 255) / 256)), dim3(256), 0, c->stream, b);
+    RT_TRY(c, hipGetLastError());
     c->cg_gen = c->scene_gen;
-    std::memcpy(c->cg_pos, pos, sizeof pos);
-    if (ok) {
-      RT_TRY(c, hipStreamSynchronize(c->stream));  // launches in flight read the previous grid
-      const size_t sb = start.size() * sizeof(int32_t), eb = ent.size() * sizeof(int32_t) + sizeof(int2);
-      if (c->cg_start_cap < sb) {
-        if (c->d_cg_start) (void)hipFree(c->d_cg_start);
-        c->d_cg_start = nullptr;
-        c->cg_start_cap = 0;
-        RT_TRY(c, hipMalloc(&c->d_cg_start, sb));
-        c->cg_start_cap = sb;
-      }
-      if (c->cg_ent_cap < eb) {
-        if (c->d_cg_ent) (void)hipFree(c->d_cg_ent);
-        c->d_cg_ent = nullptr;
-        c->cg_ent_cap = 0;
-        RT_TRY(c, hipMalloc(&c->d_cg_ent, eb));
-        c->cg_ent_cap = eb;
-      }
-      RT_TRY(c, hipMemcpy(c->d_cg_start, start.data(), sb, hipMemcpyHostToDevice));
-      if (!ent.empty()) RT_TRY(c, hipMemcpy(c->d_cg_ent, ent.data(), ent.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-      c->cg_n = N;
-      c->cg_nent = (long long)ent.size() / 2;
-      c->cg_ok = true;
-    }
+    c->cg_n = N;
+    c->cg_ngrid = ngrid;
+    c->cg_pos = pos;
     c->cg_builds++;
     c->cg_build_ms += ms_since(t0);
   }
-  if (c->cg_ok) out = CgArgs{c->d_cg_start, c->d_cg_ent, c->cg_n, 1, c->cg_nent};
+  out = CgArgs{c->d_cg_count, c->d_cg_ent, c->d_cg_glist, c->d_cg_gcount, N, kCgSlots, 1, ngrid > 1 ? 1 : 0};
   return RT_OK;
 }
 
@@ -1906,6 +2114,9 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     // the default configuration (ordered 4-wide BVH walk, light grids) has kernels
     // compiled with only those paths (kFast): no registers held for the others
     const bool fast = bv.ordered && bv.wide && lg.on;
+    // the launch's timing starts here: the camera grids are built on the
+    // device ahead of the render kernel, part of the launch
+    RT_TRY(c, mark_start(c));
     if (fast && kCull) {
       const int rc = cam_grid(c, cam, nf, ra.cg);
       if (rc != RT_OK) return rc;
@@ -1914,7 +2125,6 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       ra.sg = SgArgs{c->d_sg_start, c->d_sg_ent, c->d_sg_rho2, c->sg_n, 1, c->sg_nstart, c->sg_nent, c->nsph};
     c->cg_last = ra.cg.on != 0;
     c->cg_last_n = ra.cg.on ? ra.cg.N : 0;
-    RT_TRY(c, mark_start(c));  // the launch's timing starts after the host-side builds
     if (fast)
       hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, true>), grid, dim3(64 * kWg), lds, c->stream, ra);
     else
@@ -2124,8 +2334,16 @@ void rt_destroy(rt_ctx *c) {
   if (c->h_perm) (void)hipHostFree(c->h_perm);
   if (c->d_bperm) (void)hipFree(c->d_bperm);
   if (c->h_bperm) (void)hipHostFree(c->h_bperm);
-  if (c->d_cg_start) (void)hipFree(c->d_cg_start);
+  if (c->d_cg_count) (void)hipFree(c->d_cg_count);
   if (c->d_cg_ent) (void)hipFree(c->d_cg_ent);
+  if (c->d_cg_glist) (void)hipFree(c->d_cg_glist);
+  if (c->d_cg_gcount) (void)hipFree(c->d_cg_gcount);
+  for (auto &t : c->cg_tab) {
+    if (t.faces) (void)hipFree(t.faces);
+    if (t.blocks) (void)hipFree(t.blocks);
+    if (t.tiles) (void)hipFree(t.tiles);
+    if (t.cell) (void)hipFree(t.cell);
+  }
   for (int i = 0; i < rt_ctx::kRing; i++) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);

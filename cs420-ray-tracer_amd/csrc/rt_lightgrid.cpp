@@ -345,6 +345,26 @@ bool point_grid(const CubeGrid &G, const double *cx, const double *cy, const dou
 
 }  // namespace
 
+void cube_tables(int N, std::vector<CubePatch> &faces, std::vector<CubePatch> &blocks, std::vector<CubePatch> &tiles,
+                 std::vector<double> &cell_cbsb, int &NT, int &NB) {
+  static_assert(CubeGrid::kT == kCubeT && CubeGrid::kB == kCubeB, "one patch hierarchy");
+  const CubeGrid G(N);
+  auto put = [](const Patch &p) { return CubePatch{p.c.x, p.c.y, p.c.z, p.rad, p.cb, p.sb}; };
+  NT = G.NT;
+  NB = G.NB;
+  faces.clear();
+  for (int f = 0; f < 6; f++) faces.push_back(put(G.facep[f]));
+  blocks.clear();
+  for (const Patch &p : G.blockp) blocks.push_back(put(p));
+  tiles.clear();
+  for (const Patch &p : G.tilep) tiles.push_back(put(p));
+  cell_cbsb.resize(2 * (size_t)N * N);
+  for (size_t ij = 0; ij < (size_t)N * N; ij++) {
+    cell_cbsb[2 * ij] = G.ct->cb[ij];
+    cell_cbsb[2 * ij + 1] = G.ct->sb[ij];
+  }
+}
+
 bool build_point_grid(const double *cx, const double *cy, const double *cz, const double *r, int n, double px,
                       double py, double pz, double diam, int N, int max_global, size_t max_entries,
                       std::vector<int32_t> &start, std::vector<int32_t> &ent) {

@@ -99,4 +99,17 @@ size_t build_sphere_grids(const double *cx, const double *cy, const double *cz, 
                           const double *rho, double diam, int N, int max_global, size_t max_entries,
                           std::vector<int32_t> &start, std::vector<int32_t> &ent, std::vector<uint8_t> &ok);
 
+// The cube map's patch hierarchy for the device-side camera-grid builder
+// (rt_kernel.hip cg_bin_kernel): faces, blocks of kCubeB x kCubeB tiles, tiles of
+// kCubeT x kCubeT cells, each with its centre direction c and rad = the largest
+// angle from c to the patch, cb / sb = cos / sin(rad + kLgSlack) (the host
+// builder's Patch); cells from a per-(i, j) table (cb, sb) shared by the six
+// faces, their centres formed on the fly.  Same values as build_point_grid's.
+constexpr int kCubeT = 8, kCubeB = 8;
+struct CubePatch {
+  double cx, cy, cz, rad, cb, sb;
+};
+void cube_tables(int N, std::vector<CubePatch> &faces, std::vector<CubePatch> &blocks, std::vector<CubePatch> &tiles,
+                 std::vector<double> &cell_cbsb, int &NT, int &NB);
+
 }  // namespace rtk
