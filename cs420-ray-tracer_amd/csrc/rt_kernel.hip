@@ -1328,7 +1328,7 @@ __global__ __launch_bounds__(64) void cg_bin_kernel(const CgBuild a) {
       if (b < nb) m = meets_p(a.faces[b / (a.NB * a.NB)]) && meets_p(a.blocks[b]);
       unsigned long long bm = __ballot(m);
       while (bm) {
-        const int bb = __builtin_ctzll(bm);
+        const int bb = b0 + __builtin_ctzll(bm);
         bm &= bm - 1;
         const int f = bb / (a.NB * a.NB), bj = (bb / a.NB) % a.NB, bi = bb % a.NB;
         const int ti = bi * kCubeB + (lane & 7), tj = bj * kCubeB + (lane >> 3);
