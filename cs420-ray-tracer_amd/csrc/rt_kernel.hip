@@ -2336,8 +2336,7 @@ void rt_destroy(rt_ctx *c) {
   if (c->h_bperm) (void)hipHostFree(c->h_bperm);
   if (c->d_cg_count) (void)hipFree(c->d_cg_count);
   if (c->d_cg_ent) (void)hipFree(c->d_cg_ent);
-  if (c->d_cg_glist) (void)hipFree(c->d_cg_glist);
-  if (c->d_cg_gcount) (void)hipFree(c->d_cg_gcount);
+  if (c->d_cg_glist) (void)hipFree(c->d_cg_glist);  // d_cg_gcount lies inside it
   for (auto &t : c->cg_tab) {
     if (t.faces) (void)hipFree(t.faces);
     if (t.blocks) (void)hipFree(t.blocks);
