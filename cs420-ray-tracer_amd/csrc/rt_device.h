@@ -1582,7 +1582,7 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
 
 // Closest hit of camera rays through the camera grid (rt_lightgrid.h
 // build_point_grid's cube map and lists, built on the device by
-// rt_kernel.hip's cg_bin_kernel / cg_sort_kernel): the rays leave the grid's
+// rt_kernel.hip's cg_*_kernel passes): the rays leave the grid's
 // point P exactly, so every sphere the reference's test can report lies on
 // the list of the cell of d or on the grid's global list (spheres containing
 // or nearly containing P, tlo = -inf); a cell's list ascends by a lower bound
@@ -1590,7 +1590,8 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
 // exceeds the best t found so far (every later entry can only give a larger t:
 // no strict-< win, no tie).  The result is the lexicographic (t, index)
 // minimum over all spheres, as sweep_closest's.  A lane whose direction cannot
-// be binned tests every sphere; a lane whose cell overflowed its K slots (or a
+// be binned tests every sphere; a lane whose cell overflowed the builder's K
+// slots (or a
 // frame whose grid was refused: too many global spheres) is told to sweep.
 constexpr int kCgMaxGlobal = 32;  // spheres containing the camera (on every list); more: no grid
 struct CgArgs {
@@ -1601,6 +1602,7 @@ struct CgArgs {
   int N, K;
   int on;         // the launch's frames have grids
   int per_frame;  // 1: frame f scans grid f; 0: every frame grid 0 (one camera position)
+  int ngrid;      // (RT_CHECK bound)
 };
 // The scan of one grid's cell list for the closest hit; this lane's grid
 // starts at start + sbase (camera grid: sbase = 0; sphere grids: the grid of
@@ -1647,7 +1649,11 @@ __device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, 
   double bt = kInf, bn = __builtin_inf();
   int bi = -1;
   sweep = false;
+#ifdef RT_EXP_NOGLOB
+  const int ng = 0;
+#else
   const int ng = __builtin_amdgcn_readfirstlane(cg.gcount[grid]);
+#endif
   if (ng > kCgMaxGlobal) {  // this frame has no grid
     sweep = act;
     best_t = bt;
@@ -1671,7 +1677,7 @@ __device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, 
       all = true;
       len = n;
     } else {
-      const long long gc = (long long)grid * cells + RT_CK(kCkCgStart, c, cells);
+      const long long gc = (long long)RT_CK(kCkCgStart, grid, cg.ngrid) * cells + RT_CK(kCkCgStart, c, cells);
       len = cg.count[gc];
       if (len > cg.K) {  // overflowed: this lane sweeps
         sweep = true;

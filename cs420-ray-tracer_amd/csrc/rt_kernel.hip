@@ -265,25 +265,16 @@ __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const d
   RT_T0(t_cl);
   int bi = -1;
   // cam_pass (kFast merged kernels, wave-uniform): every alive lane holds a
-  // camera ray of a frame whose position is the camera grid's point
-  bool swept = false;
+  // camera ray of a frame whose position is the camera grid's point.  The
+  // lanes a grid cannot serve (`rest`) take the one sweep below.
+  bool rest = alive;
   if constexpr (kFast && kArgMem) {
     if (cam_pass) {
-      bool rest;
-      {
-        const CgArgs &cg = kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{});
-        bi = cam_closest(g, n, alive, o, d, cg, cg.per_frame ? frame : 0, rest, bt, work);
-      }
-      if (__ballot(rest)) {  // lanes of an overflowed cell, or a frame without a grid, sweep
-        double bt2 = kInf;
-        const int bi2 = sweep_closest<kCull, kFast>(g, rad, n, rest, o, d, key,
-                                                    kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt2, work);
-        if (rest) {
-          bi = bi2;
-          bt = bt2;
-        }
-      }
-      swept = true;
+      const CgArgs &cg = kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{});
+      bi = cam_closest(g, n, alive, o, d, cg, cg.per_frame ? frame : 0, rest, bt, work);
+#ifdef RT_EXP_NOREST
+      rest = false;
+#endif
     } else if (kernarg_late<true, offsetof(RenderArgs, sg)>(SgArgs{}).on) {
       // reflection rays through the sphere grid of the sphere they leave; the
       // lanes whose origin fails the grid's check sweep as before
@@ -297,22 +288,18 @@ __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const d
         bi = grid_closest(g, n, grid, o, d, sg.start, sg.ent, sg.N, grid ? key * (6 * sg.N * sg.N + 1) : 0, sg.nstart,
                           sg.nent, bt, work);
       }
-      const bool rest = alive && !grid;
-      if (__ballot(rest)) {
-        double bt2 = kInf;
-        const int bi2 = sweep_closest<kCull, kFast>(g, rad, n, rest, o, d, key,
-                                                    kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt2, work);
-        if (rest) {
-          bi = bi2;
-          bt = bt2;
-        }
-      }
-      swept = true;
+      rest = alive && !grid;
     }
   }
-  if (!swept)
-    bi = sweep_closest<kCull, kFast>(g, rad, n, alive, o, d, key, kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv),
-                                     bt, work);
+  if (__ballot(rest)) {
+    double bt2 = kInf;
+    const int bi2 = sweep_closest<kCull, kFast>(g, rad, n, rest, o, d, key,
+                                                kernarg_late<kArgMem, offsetof(RenderArgs, bv)>(bv), bt2, work);
+    if (rest) {
+      bi = bi2;
+      bt = bt2;
+    }
+  }
   RT_ACC(work, 8, t_cl);
   bt_out = bt;
   return bi;
@@ -1273,14 +1260,22 @@ __global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__rest
 // data, goes to the grid's global list.  A cell keeps K entries; one that
 // overflows is marked by its count, and its rays sweep.  cg_sort_kernel (one
 // thread per cell) orders each list by (tlo, index).
+struct CgDisk {  // one side of a sphere seen from a grid's point
+  double ux, uy, uz, alpha, ca, sa;
+  float tlo;
+  int s;
+};
 struct CgBuild {
   const SphGeo *geo;
   const double *rad;
   const CubePatch *faces, *blocks, *tiles;
   const double *cell_cbsb;
   int32_t *count, *glist, *gcount;
-  int2 *ent;
-  int n, N, NT, NB, K, ngrid;
+  int2 *ent;            // [grid][cell][K] the lists (count: their lengths)
+  CgDisk *disks;        // [grid][sphere][side]
+  int2 *pairs;          // [grid][maxp] (disk, block) pairs whose block the disk meets
+  unsigned *npairs;     // [grid * kCgCntStride] their counts (a 256-byte line per grid's counter)
+  int n, N, NT, NB, K, ngrid, maxp;
   double px[RT_MAX_FRAMES], py[RT_MAX_FRAMES], pz[RT_MAX_FRAMES], diam[RT_MAX_FRAMES];
 };
 static_assert(sizeof(CgBuild) <= 4096, "CgBuild exceeds the kernel-argument segment");
@@ -1293,97 +1288,145 @@ __device__ __forceinline__ float float_down(double x) {  // x rounded down to fp
   }
   return f;
 }
+// angle(u, patch centre) <= alpha + rad + slack (the host builder's meets())
+__device__ __forceinline__ bool cg_meets(const CgDisk &k, double cx, double cy, double cz, double rad, double cb,
+                                         double sb) {
+  if (k.alpha + rad + kLgSlack >= 3.14159) return true;
+  return k.ux * cx + k.uy * cy + k.uz * cz >= k.ca * cb - k.sa * sb - 1e-12;
+}
+__device__ __forceinline__ bool cg_meets(const CgDisk &k, const CubePatch &p) {
+  return cg_meets(k, p.cx, p.cy, p.cz, p.rad, p.cb, p.sb);
+}
 
-__global__ __launch_bounds__(64) void cg_bin_kernel(const CgBuild a) {
-  const int s = (int)blockIdx.x, grid = (int)blockIdx.y;
-  if (s >= a.n || grid >= a.ngrid) return;
-  const int lane = (int)(threadIdx.x & 63);
-  const long long cells = 6LL * a.N * a.N;
+constexpr int kCgCntStride = 64;
+// Pass 1, a wave per (grid, sphere): its two disks (or the global list), and
+// every (disk, block) pair whose face and block patches the disk meets (a
+// lane per block, one atomic on the grid's pair count per wave and side).
+__global__ __launch_bounds__(256) void cg_disk_kernel(const CgBuild a) {
+  const int t = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6), lane = (int)(threadIdx.x & 63);
+  if (t >= a.n * a.ngrid) return;
+  const int grid = t / a.n, s = t - grid * a.n;
   const SphGeo sp = a.geo[s];
   const double vx = sp.cx - a.px[grid], vy = sp.cy - a.py[grid], vz = sp.cz - a.pz[grid];
   const double D = __builtin_sqrt(vx * vx + vy * vy + vz * vz);
   const double R = a.rad[s] * (1.0 + 1e-6) + 1e-6 * (D + a.diam[grid]);
   if (!__builtin_isfinite(D) || !__builtin_isfinite(R) || !(D > R)) {
-    if (lane == 0) {  // contains (or nearly) P, or non-finite: every direction, tlo = -inf
+    if (lane == 0) {  // contains (or nearly contains) P, or non-finite: every direction, tlo = -inf
       const int k = atomicAdd(&a.gcount[grid], 1);
       if (k < kCgMaxGlobal) a.glist[(size_t)grid * kCgMaxGlobal + k] = s;
     }
     return;
   }
   const double alpha = asin(R / D) + kLgSlack, ca = cos(alpha), sa = sin(alpha);
-  const bool wide = alpha + kLgSlack >= 3.0;
   const int nb = 6 * a.NB * a.NB;
   for (int side = 0; side < 2; ++side) {
     const double sg = side ? -1.0 : 1.0;
-    const double ux = sg * (vx / D), uy = sg * (vy / D), uz = sg * (vz / D);
-    const float tlo = side ? float_down(-(D + R) * (1.0 + 1e-9)) : float_down((D - R) * (1.0 - 1e-9));
-    auto meets = [&](double cx, double cy, double cz, double rad, double cb, double sb) {
-      if (alpha + rad + kLgSlack >= 3.14159) return true;
-      return ux * cx + uy * cy + uz * cz >= ca * cb - sa * sb - 1e-12;
-    };
-    auto meets_p = [&](const CubePatch &p) { return meets(p.cx, p.cy, p.cz, p.rad, p.cb, p.sb); };
+    CgDisk k;
+    k.ux = sg * (vx / D), k.uy = sg * (vy / D), k.uz = sg * (vz / D);
+    k.alpha = alpha, k.ca = ca, k.sa = sa;
+    k.tlo = side ? float_down(-(D + R) * (1.0 + 1e-9)) : float_down((D - R) * (1.0 - 1e-9));
+    k.s = s;
+    const int di = 2 * t + side;
+    if (lane == 0) a.disks[di] = k;
     for (int b0 = 0; b0 < nb; b0 += 64) {
       const int b = b0 + lane;
-      bool m = false;
-      if (b < nb) m = meets_p(a.faces[b / (a.NB * a.NB)]) && meets_p(a.blocks[b]);
-      unsigned long long bm = __ballot(m);
-      while (bm) {
-        const int bb = b0 + __builtin_ctzll(bm);
-        bm &= bm - 1;
-        const int f = bb / (a.NB * a.NB), bj = (bb / a.NB) % a.NB, bi = bb % a.NB;
-        const int ti = bi * kCubeB + (lane & 7), tj = bj * kCubeB + (lane >> 3);
-        bool tm = false, inside = false;
-        if (ti < a.NT && tj < a.NT) {
-          const CubePatch tp = a.tiles[((size_t)f * a.NT + tj) * a.NT + ti];
-          tm = meets_p(tp);
-          inside = tm && alpha < 3.0 && alpha > tp.rad + 1e-3 &&
-                   ux * tp.cx + uy * tp.cy + uz * tp.cz >= cos(alpha - tp.rad - 1e-3);
-        }
-        unsigned long long tmask = __ballot(tm);
-        const unsigned long long imask = __ballot(inside);
-        while (tmask) {
-          const int tl = __builtin_ctzll(tmask);
-          tmask &= tmask - 1;
-          const bool tin = (imask >> tl) & 1ull;
-          const int i = (bi * kCubeB + (tl & 7)) * kCubeT + (lane & 7), j = (bj * kCubeB + (tl >> 3)) * kCubeT + (lane >> 3);
-          bool cm = false;
-          if (i < a.N && j < a.N) {
-            if (tin) {
-              cm = true;
-            } else {  // the cell's patch: centre formed as face_dir does, cos / sin of rad + slack from the table
-              const double fa = -1.0 + (2.0 * i + 1.0) / a.N, fb = -1.0 + (2.0 * j + 1.0) / a.N;
-              double dx, dy, dz;
-              switch (f) {
-                case 0: dx = 1.0, dy = fa, dz = fb; break;
-                case 1: dx = -1.0, dy = fa, dz = fb; break;
-                case 2: dx = fa, dy = 1.0, dz = fb; break;
-                case 3: dx = fa, dy = -1.0, dz = fb; break;
-                case 4: dx = fa, dy = fb, dz = 1.0; break;
-                default: dx = fa, dy = fb, dz = -1.0; break;
-              }
-              const double l = __builtin_sqrt(dx * dx + dy * dy + dz * dz);
-              const size_t ij = (size_t)j * a.N + i;
-              cm = meets(dx / l, dy / l, dz / l, wide ? 3.2 : 0.0, a.cell_cbsb[2 * ij], a.cell_cbsb[2 * ij + 1]);
-            }
-          }
-          if (cm) {
-            const long long gc = (long long)grid * cells + ((long long)f * a.N + j) * a.N + i;
-            const int slot = atomicAdd(&a.count[gc], 1);
-            if (slot < a.K) a.ent[gc * a.K + slot] = make_int2(s, __float_as_int(tlo));
-          }
-        }
-      }
+      const bool m = b < nb && cg_meets(k, a.faces[b / (a.NB * a.NB)]) && cg_meets(k, a.blocks[b]);
+      const unsigned long long bm = __ballot(m);
+      if (!bm) continue;
+      unsigned q0 = 0;
+      if (lane == 0) q0 = atomicAdd(&a.npairs[grid * kCgCntStride], (unsigned)__builtin_popcountll(bm));
+      q0 = (unsigned)__builtin_amdgcn_readfirstlane((int)q0);
+      if (m) a.pairs[(size_t)grid * a.maxp + q0 + (unsigned)__builtin_popcountll(bm & ((1ull << lane) - 1))] =
+          make_int2(di, b);
     }
   }
 }
 
+// Pass 2, a wave per quarter of a (disk, block) pair (a fixed grid of waves
+// walks the grids' pair lists): the block's 64 tiles (a tile well inside the
+// disk takes all its cells untested), then the cells of each tile of the
+// quarter it meets; each listed cell takes a slot (count) and, below K, the
+// entry (sphere, tlo).
+__global__ __launch_bounds__(64) void cg_bin_kernel(const CgBuild a) {
+  const int lane = (int)(threadIdx.x & 63);
+  const long long cells = 6LL * a.N * a.N;
+  unsigned incl = lane < a.ngrid ? 4u * a.npairs[lane * kCgCntStride] : 0u;  // work items per grid, then prefix
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
+  }
+  const unsigned total = __shfl(incl, 63, 64);
+  for (unsigned v = blockIdx.x; v < total; v += gridDim.x) {
+    const int grid = __builtin_popcountll(__ballot(incl <= v));
+    const unsigned item = v - (grid ? __shfl(incl, grid - 1, 64) : 0u);
+    const int2 pr = a.pairs[(size_t)grid * a.maxp + (item >> 2)];
+    const CgDisk k = a.disks[pr.x];
+    const bool wide = k.alpha + kLgSlack >= 3.0;
+    const int bb = pr.y;
+    const int f = bb / (a.NB * a.NB), bj = (bb / a.NB) % a.NB, bi = bb % a.NB;
+    const int ti = bi * kCubeB + (lane & 7), tj = bj * kCubeB + (lane >> 3);
+    bool tm = false, inside = false;
+    if (ti < a.NT && tj < a.NT) {
+      const CubePatch tp = a.tiles[((size_t)f * a.NT + tj) * a.NT + ti];
+      tm = cg_meets(k, tp);
+      inside = tm && k.alpha < 3.0 && k.alpha > tp.rad + 1e-3 &&
+               k.ux * tp.cx + k.uy * tp.cy + k.uz * tp.cz >= cos(k.alpha - tp.rad - 1e-3);
+    }
+    unsigned long long tmask = __ballot(tm) & (0xffffull << (16 * (item & 3)));
+    const unsigned long long imask = __ballot(inside);
+    while (tmask) {  // up to 4 tiles a round: their cells' slot atomics in flight together
+      int gcs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        gcs[u] = -1;
+        if (!tmask) continue;
+        const int tl = __builtin_ctzll(tmask);
+        tmask &= tmask - 1;
+        const bool tin = (imask >> tl) & 1ull;
+        const int i = (bi * kCubeB + (tl & 7)) * kCubeT + (lane & 7), j = (bj * kCubeB + (tl >> 3)) * kCubeT + (lane >> 3);
+        bool cm = false;
+        if (i < a.N && j < a.N) {
+          if (tin) {
+            cm = true;
+          } else {  // the cell's patch: centre formed as face_dir does, cos / sin of rad + slack from the table
+            const double fa = -1.0 + (2.0 * i + 1.0) / a.N, fb = -1.0 + (2.0 * j + 1.0) / a.N;
+            double dx, dy, dz;
+            switch (f) {
+              case 0: dx = 1.0, dy = fa, dz = fb; break;
+              case 1: dx = -1.0, dy = fa, dz = fb; break;
+              case 2: dx = fa, dy = 1.0, dz = fb; break;
+              case 3: dx = fa, dy = -1.0, dz = fb; break;
+              case 4: dx = fa, dy = fb, dz = 1.0; break;
+              default: dx = fa, dy = fb, dz = -1.0; break;
+            }
+            const double l = __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+            const size_t ij = (size_t)j * a.N + i;
+            cm = cg_meets(k, dx / l, dy / l, dz / l, wide ? 3.2 : 0.0, a.cell_cbsb[2 * ij], a.cell_cbsb[2 * ij + 1]);
+          }
+        }
+        if (cm) gcs[u] = (f * a.N + j) * a.N + i;
+      }
+      int slots[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) slots[u] = gcs[u] >= 0 ? atomicAdd(&a.count[(long long)grid * cells + gcs[u]], 1) : a.K;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (slots[u] < a.K)
+          a.ent[((long long)grid * cells + gcs[u]) * a.K + slots[u]] = make_int2(k.s, __float_as_int(k.tlo));
+    }
+  }
+}
+
+// Pass 3, a thread per cell: its list sorted by (tlo, index) in place (lists
+// are short: insertion sort; an overflowed cell's rays sweep, its list unread).
 __global__ __launch_bounds__(256) void cg_sort_kernel(const CgBuild a) {
   const long long cells = 6LL * a.N * a.N;
   const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gc >= cells * a.ngrid) return;
-  const int cnt = a.count[gc] < a.K ? a.count[gc] : a.K;
+  const int cnt = a.count[gc];
+  if (cnt > a.K) return;
   int2 *e = a.ent + gc * a.K;
-  for (int k = 1; k < cnt; ++k) {  // insertion sort by (tlo, index); lists are short
+  for (int k = 1; k < cnt; ++k) {
     const int2 x = e[k];
     const float tx = __int_as_float(x.y);
     int m = k - 1;
@@ -1430,13 +1473,19 @@ struct rt_ctx {
   // camera grids (rt_device.h CgArgs), built on the device per camera
   // position of a launch (cg_bin_kernel / cg_sort_kernel) and kept while the
   // positions and the scene stay the same
-  int cg_mode = 1;    // RT_HIP_CAM_GRID: 0 off, 1 (= 2) every launch of the kFast kernels
+  int cg_mode = 1;    // RT_HIP_CAM_GRID: 0 off, 1 auto (a one-frame launch at a new position sweeps), 2 every launch
   int cg_n_opt = 0;   // RT_HIP_CAM_GRID_N (tuning build); 0 = kCgNStatic / kCgNMoving
+  int cg_k = 48;      // entries per cell (RT_HIP_CAM_GRID_K, tuning build)
   int32_t *d_cg_count = nullptr, *d_cg_glist = nullptr, *d_cg_gcount = nullptr;
   int2 *d_cg_ent = nullptr;
-  size_t cg_count_cap = 0, cg_ent_cap = 0, cg_glist_cap = 0;  // bytes
-  int cg_n = 0, cg_ngrid = 0;
+  CgDisk *d_cg_disks = nullptr;
+  int2 *d_cg_pairs = nullptr;
+  unsigned *d_cg_npairs = nullptr;
+  size_t cg_count_cap = 0, cg_ent_cap = 0, cg_glist_cap = 0, cg_disks_cap = 0, cg_pairs_cap = 0, cg_npairs_cap = 0;  // bytes
+  int cg_n = 0, cg_ngrid = 0, cg_kb = 0;
   std::vector<double> cg_pos;          // the grids' points (3 per grid)
+  std::vector<double> cg_seen;         // the previous launch's camera positions
+  unsigned long long cg_seen_gen = ~0ull;
   unsigned long long cg_gen = ~0ull;   // scene_gen they were built for
   struct CgTables {                    // the cube map's patch tables of one N on the device
     int N = 0, NT = 0, NB = 0;
@@ -1713,7 +1762,6 @@ LgArgs lg_args(const rt_ctx *c) {
 // 0.1791, no grid 0.2177 / 0.1980): 256 for a launch at one position, 128 for
 // a grid per frame (a quarter of the cells to build)
 constexpr int kCgNStatic = 256, kCgNMoving = 128;
-constexpr int kCgSlots = 48;  // entries per cell; a cell with more has its rays sweep
 
 // The device patch tables of the cube map with N cells per face edge (two
 // kept; replacing one waits for the launches in flight).
@@ -1775,17 +1823,32 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
   for (int f = 1; f < ngrid; f++) pos.insert(pos.end(), c->fcams[f].position, c->fcams[f].position + 3);
   const int N = c->cg_n_opt ? c->cg_n_opt : (same ? kCgNStatic : kCgNMoving);
   const size_t cells = 6 * (size_t)N * N;
-  const bool cached = c->cg_gen == c->scene_gen && c->cg_n == N && c->cg_ngrid == ngrid && c->cg_pos == pos;
+  const bool cached = c->cg_gen == c->scene_gen && c->cg_n == N && c->cg_kb == c->cg_k && c->cg_ngrid == ngrid && c->cg_pos == pos;
+  if (!cached && nf == 1 && c->cg_mode == 1 && !(c->cg_seen_gen == c->scene_gen && c->cg_seen == pos)) {
+    // one frame from a position the previous launch did not use: the build
+    // (~0.05 ms) costs more than the grid saves that frame (profiles/r4j/);
+    // the position's next launch gets the grid
+    c->cg_seen = pos;
+    c->cg_seen_gen = c->scene_gen;
+    return RT_OK;
+  }
+  c->cg_seen = pos;
+  c->cg_seen_gen = c->scene_gen;
   if (!cached) {
     const auto t0 = std::chrono::steady_clock::now();
     const rt_ctx::CgTables *tab = nullptr;
     int rc = cg_tables(c, N, tab);
     if (rc != RT_OK) return rc;
     if ((rc = grow(c, c->d_cg_count, c->cg_count_cap, ngrid * cells * sizeof(int32_t))) != RT_OK ||
-        (rc = grow(c, c->d_cg_ent, c->cg_ent_cap, ngrid * cells * kCgSlots * sizeof(int2))) != RT_OK ||
-        (rc = grow(c, c->d_cg_glist, c->cg_glist_cap, (size_t)ngrid * (kCgMaxGlobal + 1) * sizeof(int32_t))) != RT_OK)
+        (rc = grow(c, c->d_cg_ent, c->cg_ent_cap, ngrid * cells * c->cg_k * sizeof(int2))) != RT_OK ||
+        (rc = grow(c, c->d_cg_glist, c->cg_glist_cap, (size_t)ngrid * (kCgMaxGlobal + 1) * sizeof(int32_t))) != RT_OK ||
+        (rc = grow(c, c->d_cg_npairs, c->cg_npairs_cap, (size_t)ngrid * kCgCntStride * sizeof(unsigned))) != RT_OK)
       return rc;
     c->d_cg_gcount = c->d_cg_glist + (size_t)ngrid * kCgMaxGlobal;
+    const long long nblocks = 6LL * tab->NB * tab->NB;
+    if ((rc = grow(c, c->d_cg_disks, c->cg_disks_cap, 2 * (size_t)c->nsph * ngrid * sizeof(CgDisk))) != RT_OK ||
+        (rc = grow(c, c->d_cg_pairs, c->cg_pairs_cap, 2 * (size_t)c->nsph * ngrid * nblocks * sizeof(int2))) != RT_OK)
+      return rc;
     CgBuild b{};
     b.geo = c->d_geo;
     b.rad = c->d_rad;
@@ -1797,11 +1860,15 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
     b.glist = c->d_cg_glist;
     b.gcount = c->d_cg_gcount;
     b.ent = c->d_cg_ent;
+    b.disks = c->d_cg_disks;
+    b.pairs = c->d_cg_pairs;
+    b.npairs = c->d_cg_npairs;
+    b.maxp = (int)(2 * c->nsph * nblocks);
     b.n = c->nsph;
     b.N = N;
     b.NT = tab->NT;
     b.NB = tab->NB;
-    b.K = kCgSlots;
+    b.K = c->cg_k;
     b.ngrid = ngrid;
     for (int g = 0; g < ngrid; g++) {
       b.px[g] = pos[3 * g];
@@ -1816,17 +1883,22 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
     }
     RT_TRY(c, hipMemsetAsync(c->d_cg_count, 0, ngrid * cells * sizeof(int32_t), c->stream));
     RT_TRY(c, hipMemsetAsync(c->d_cg_gcount, 0, ngrid * sizeof(int32_t), c->stream));
-    hipLaunchKernelGGL(cg_bin_kernel, dim3((unsigned)c->nsph, (unsigned)ngrid), dim3(64), 0, c->stream, b);
+    RT_TRY(c, hipMemsetAsync(c->d_cg_npairs, 0, ngrid * kCgCntStride * sizeof(unsigned), c->stream));
+    const int nthr = c->nsph * ngrid;
+    hipLaunchKernelGGL(cg_disk_kernel, dim3((unsigned)((nthr + 3) / 4)), dim3(256), 0, c->stream, b);
+    hipLaunchKernelGGL(cg_bin_kernel, dim3((unsigned)std::min<long long>(8192, 8LL * nthr * nblocks)), dim3(64), 0,
+                       c->stream, b);
     hipLaunchKernelGGL(cg_sort_kernel, dim3((unsigned)((ngrid * cells + 255) / 256)), dim3(256), 0, c->stream, b);
     RT_TRY(c, hipGetLastError());
     c->cg_gen = c->scene_gen;
     c->cg_n = N;
+    c->cg_kb = c->cg_k;
     c->cg_ngrid = ngrid;
     c->cg_pos = pos;
     c->cg_builds++;
     c->cg_build_ms += ms_since(t0);
   }
-  out = CgArgs{c->d_cg_count, c->d_cg_ent, c->d_cg_glist, c->d_cg_gcount, N, kCgSlots, 1, ngrid > 1 ? 1 : 0};
+  out = CgArgs{c->d_cg_count, c->d_cg_ent, c->d_cg_glist, c->d_cg_gcount, N, c->cg_k, 1, ngrid > 1 ? 1 : 0, ngrid};
   return RT_OK;
 }
 
@@ -2278,6 +2350,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(8, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_CAM_GRID_N")) c->cg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_CAM_GRID_K")) c->cg_k = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID")) c->sg_mode = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID_N")) c->sg_n_opt = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_BEHIND_GRID")) c->ug_mode = std::max(-1, std::min(1, std::atoi(e)));
@@ -2337,6 +2410,9 @@ void rt_destroy(rt_ctx *c) {
   if (c->d_cg_count) (void)hipFree(c->d_cg_count);
   if (c->d_cg_ent) (void)hipFree(c->d_cg_ent);
   if (c->d_cg_glist) (void)hipFree(c->d_cg_glist);  // d_cg_gcount lies inside it
+  if (c->d_cg_disks) (void)hipFree(c->d_cg_disks);
+  if (c->d_cg_pairs) (void)hipFree(c->d_cg_pairs);
+  if (c->d_cg_npairs) (void)hipFree(c->d_cg_npairs);
   for (auto &t : c->cg_tab) {
     if (t.faces) (void)hipFree(t.faces);
     if (t.blocks) (void)hipFree(t.blocks);

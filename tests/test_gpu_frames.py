@@ -200,3 +200,40 @@ def test_camera_grid_rotated_views_one_position(gpu_renderer):
         for k in total:
             total[k] += counts[k]
     assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (total["primary"], total["shadow"], total["reflect"])
+
+
+def test_camera_grid_one_frame_policy(gpu_renderer):
+    """One-frame launches (the drop-in's still frame): a position the previous
+    launch did not use sweeps (no grid build for one frame), the same
+    position's next launch builds and uses the device grid; both equal the
+    reference's image, and a new position sweeps again."""
+    name = "synth200_1920x1080_d4"
+    sc, m = _load(gpu_renderer, name)
+    W, H, D = m["width"], m["height"], m["depth"]
+    want = golden_rgb(name)
+    used = []
+    for k in (1, 0, 0, 0, 2):
+        rgb, _ = _single(gpu_renderer, _moved(sc.camera(), k), W, H, D)
+        used.append(gpu_renderer.info().cam_grid_last)
+        if k == 0:
+            assert rgb == want, diff_summary(rgb, want)
+    assert used == [0, 0, 1, 1, 0]
+
+
+@pytest.mark.parametrize("F", [2, 17, 32])
+def test_camera_grid_per_frame_device_grids(gpu_renderer, F):
+    """A moving camera: one device-built camera grid per frame of the launch
+    (every position distinct), each frame equal to its own one-frame render
+    (the sweep: a new position per launch) with identical ray counts."""
+    name = "complex_97x61_d4"
+    sc, m = _load(gpu_renderer, name)
+    W, H, D = m["width"], m["height"], m["depth"]
+    cams = [_moved(sc.camera(), 0.25 * k - 3) for k in range(F)]
+    frames, st, _ = _frames(gpu_renderer, cams, W, H, D)
+    assert gpu_renderer.info().cam_grid_last == 1
+    total = [0, 0, 0]
+    for f, cam in enumerate(cams):
+        want, s1 = _single(gpu_renderer, cam, W, H, D)
+        assert frames[f].tobytes() == want, f"frame {f}: {diff_summary(frames[f].tobytes(), want)}"
+        total = [total[0] + s1.rays_primary, total[1] + s1.rays_shadow, total[2] + s1.rays_reflect]
+    assert [st.rays_primary, st.rays_shadow, st.rays_reflect] == total
