@@ -1584,22 +1584,19 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
 // build_point_grid's cube map and lists, built on the device by
 // rt_kernel.hip's cg_*_kernel passes): the rays leave the grid's
 // point P exactly, so every sphere the reference's test can report lies on
-// the list of the cell of d or on the grid's global list (spheres containing
-// or nearly containing P, tlo = -inf); a cell's list ascends by a lower bound
-// tlo of the sphere's t, so the scan stops at the first entry whose bound
-// exceeds the best t found so far (every later entry can only give a larger t:
-// no strict-< win, no tie).  The result is the lexicographic (t, index)
-// minimum over all spheres, as sweep_closest's.  A lane whose direction cannot
-// be binned tests every sphere; a lane whose cell overflowed the builder's K
-// slots (or a
-// frame whose grid was refused: too many global spheres) is told to sweep.
-constexpr int kCgMaxGlobal = 32;  // spheres containing the camera (on every list); more: no grid
+// the list of the cell of d (spheres containing or nearly containing P are
+// on every list, tlo = -inf); a cell's list ascends by a lower bound tlo of
+// the sphere's t, so the scan stops at the first entry whose bound exceeds
+// the best t found so far (every later entry can only give a larger t: no
+// strict-< win, no tie).  The result is the lexicographic (t, index) minimum
+// over all spheres, as sweep_closest's.  A lane whose direction cannot be
+// binned tests every sphere; a lane whose cell overflowed the builder's K
+// slots is told to sweep.
+constexpr int kCgSlots = 48;  // entries per cell; a cell with more has its rays sweep
 struct CgArgs {
-  const int32_t *count;   // [grid][6N^2] entries of each cell (> K: overflowed, its rays sweep)
-  const int2 *ent;        // [grid][6N^2][K] (sphere, tlo bits), ascending by (tlo, index)
-  const int32_t *glist;   // [grid][kCgMaxGlobal] the global spheres, file order
-  const int32_t *gcount;  // [grid] how many (> kCgMaxGlobal: no grid for that frame)
-  int N, K;
+  const int32_t *count;   // [grid][6N^2] entries of each cell (> kCgSlots: overflowed, its rays sweep)
+  const int2 *ent;        // [grid][6N^2][kCgSlots] (sphere, tlo bits), ascending by (tlo, index)
+  int N;
   int on;         // the launch's frames have grids
   int per_frame;  // 1: frame f scans grid f; 0: every frame grid 0 (one camera position)
   int ngrid;      // (RT_CHECK bound)
@@ -1649,26 +1646,9 @@ __device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, 
   double bt = kInf, bn = __builtin_inf();
   int bi = -1;
   sweep = false;
-#ifdef RT_EXP_NOGLOB
-  const int ng = 0;
-#else
-  const int ng = __builtin_amdgcn_readfirstlane(cg.gcount[grid]);
-#endif
-  if (ng > kCgMaxGlobal) {  // this frame has no grid
-    sweep = act;
-    best_t = bt;
-    return bi;
-  }
   const bool fast = a2_ok(a2);
-  const long long cells = 6LL * cg.N * cg.N;
-  for (int k = 0; k < ng; ++k) {  // the global list: every lane, tlo = -inf
-    const int i = RT_CK(kCkSphere, cg.glist[(size_t)grid * kCgMaxGlobal + k], n);
-    if (act) {
-      work.exact += 1;
-      closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi);
-    }
-  }
-  long long cb = 0;
+  const int cells = 6 * cg.N * cg.N;  // the host keeps grid * cells * kCgSlots below 2^31
+  unsigned cb = 0;
   int len = 0;
   bool all = false;
   if (act) {
@@ -1677,13 +1657,13 @@ __device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, 
       all = true;
       len = n;
     } else {
-      const long long gc = (long long)RT_CK(kCkCgStart, grid, cg.ngrid) * cells + RT_CK(kCkCgStart, c, cells);
+      const unsigned gc = (unsigned)(RT_CK(kCkCgStart, grid, cg.ngrid) * cells + RT_CK(kCkCgStart, c, cells));
       len = cg.count[gc];
-      if (len > cg.K) {  // overflowed: this lane sweeps
+      if (len > kCgSlots) {  // overflowed: this lane sweeps
         sweep = true;
         len = 0;
       }
-      cb = gc * cg.K;
+      cb = gc * (unsigned)kCgSlots;
     }
   }
   int k = 0;
@@ -1692,7 +1672,7 @@ __device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, 
     const int i = all ? k : RT_CK(kCkSphere, e.x, n);
     if ((double)__int_as_float(e.y) > bt) break;
     ++k;
-    if (k < len && !all) e = cg.ent[cb + k];  // the next entry, loaded during this test
+    if (k < len && !all) e = cg.ent[cb + (unsigned)k];  // the next entry, loaded during this test
     work.exact += 1;
     closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi);
   }

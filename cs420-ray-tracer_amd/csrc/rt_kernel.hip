@@ -272,9 +272,6 @@ __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const d
     if (cam_pass) {
       const CgArgs &cg = kernarg_late<true, offsetof(RenderArgs, cg)>(CgArgs{});
       bi = cam_closest(g, n, alive, o, d, cg, cg.per_frame ? frame : 0, rest, bt, work);
-#ifdef RT_EXP_NOREST
-      rest = false;
-#endif
     } else if (kernarg_late<true, offsetof(RenderArgs, sg)>(SgArgs{}).on) {
       // reflection rays through the sphere grid of the sphere they leave; the
       // lanes whose origin fails the grid's check sweep as before
@@ -1248,18 +1245,20 @@ __global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__rest
 
 // ---------------------------------------------------------------------------
 // The camera grid, built on the device for each camera position of a launch:
-// build_point_grid (rt_lightgrid.cpp) on the GPU.  cg_bin_kernel (one wave per
-// grid and sphere) lists the sphere's two disks seen from the grid's point P
-// -- along +u with tlo = (D - R)(1 - 1e-9), along -u (the negative tangent
-// root, sphere.h:43-47) with -(D + R)(1 + 1e-9), R the light grids' grown
-// radius, each disk's angular radius asin(R / D) + kLgSlack -- in every cell
-// they meet, by the host builder's patch hierarchy and tests (faces, blocks of
-// 8 x 8 tiles, tiles of 8 x 8 cells -- a tile well inside a disk takes all its
-// cells untested -- cells against the per-(i, j) table), the same patches and
-// margins; a sphere that contains (or nearly contains) P, or has non-finite
-// data, goes to the grid's global list.  A cell keeps K entries; one that
-// overflows is marked by its count, and its rays sweep.  cg_sort_kernel (one
-// thread per cell) orders each list by (tlo, index).
+// build_point_grid (rt_lightgrid.cpp) on the GPU.  Every sphere's two disks
+// seen from the grid's point P -- along +u with tlo = (D - R)(1 - 1e-9), along
+// -u (the negative tangent root, sphere.h:43-47) with -(D + R)(1 + 1e-9), R
+// the light grids' grown radius, each disk's angular radius asin(R / D) +
+// kLgSlack -- are listed in every cell they meet, by the host builder's patch
+// hierarchy and tests (faces, blocks of 8 x 8 tiles, tiles of 8 x 8 cells -- a
+// tile well inside a disk takes all its cells untested -- cells against the
+// per-(i, j) table), the same patches and margins; a sphere that contains (or
+// nearly contains) P, or has non-finite data, is one disk of every direction
+// with tlo = -inf (on every list).  A cell keeps K entries; one that
+// overflows is marked by its count, and its rays sweep.  Passes:
+// cg_disk_kernel (a wave per grid and sphere: the disks and the (disk, block)
+// pairs they meet), cg_bin_kernel (a wave per quarter pair: tiles, cells,
+// slots), cg_sort_kernel (a thread per cell: (tlo, index) order).
 struct CgDisk {  // one side of a sphere seen from a grid's point
   double ux, uy, uz, alpha, ca, sa;
   float tlo;
@@ -1270,7 +1269,7 @@ struct CgBuild {
   const double *rad;
   const CubePatch *faces, *blocks, *tiles;
   const double *cell_cbsb;
-  int32_t *count, *glist, *gcount;
+  int32_t *count;
   int2 *ent;            // [grid][cell][K] the lists (count: their lengths)
   CgDisk *disks;        // [grid][sphere][side]
   int2 *pairs;          // [grid][maxp] (disk, block) pairs whose block the disk meets
@@ -1299,7 +1298,7 @@ __device__ __forceinline__ bool cg_meets(const CgDisk &k, const CubePatch &p) {
 }
 
 constexpr int kCgCntStride = 64;
-// Pass 1, a wave per (grid, sphere): its two disks (or the global list), and
+// Pass 1, a wave per (grid, sphere): its two disks (one for a global sphere), and
 // every (disk, block) pair whose face and block patches the disk meets (a
 // lane per block, one atomic on the grid's pair count per wave and side).
 __global__ __launch_bounds__(256) void cg_disk_kernel(const CgBuild a) {
@@ -1310,21 +1309,18 @@ __global__ __launch_bounds__(256) void cg_disk_kernel(const CgBuild a) {
   const double vx = sp.cx - a.px[grid], vy = sp.cy - a.py[grid], vz = sp.cz - a.pz[grid];
   const double D = __builtin_sqrt(vx * vx + vy * vy + vz * vz);
   const double R = a.rad[s] * (1.0 + 1e-6) + 1e-6 * (D + a.diam[grid]);
-  if (!__builtin_isfinite(D) || !__builtin_isfinite(R) || !(D > R)) {
-    if (lane == 0) {  // contains (or nearly contains) P, or non-finite: every direction, tlo = -inf
-      const int k = atomicAdd(&a.gcount[grid], 1);
-      if (k < kCgMaxGlobal) a.glist[(size_t)grid * kCgMaxGlobal + k] = s;
-    }
-    return;
-  }
-  const double alpha = asin(R / D) + kLgSlack, ca = cos(alpha), sa = sin(alpha);
+  // a sphere containing (or nearly containing) P, or non-finite: one disk of
+  // every direction (alpha >= pi meets every patch), tlo = -inf
+  const bool global = !__builtin_isfinite(D) || !__builtin_isfinite(R) || !(D > R);
+  const double alpha = global ? 4.0 : asin(R / D) + kLgSlack, ca = cos(alpha), sa = sin(alpha);
   const int nb = 6 * a.NB * a.NB;
-  for (int side = 0; side < 2; ++side) {
+  for (int side = 0; side < (global ? 1 : 2); ++side) {
     const double sg = side ? -1.0 : 1.0;
     CgDisk k;
-    k.ux = sg * (vx / D), k.uy = sg * (vy / D), k.uz = sg * (vz / D);
+    k.ux = global ? 1.0 : sg * (vx / D), k.uy = global ? 0.0 : sg * (vy / D), k.uz = global ? 0.0 : sg * (vz / D);
     k.alpha = alpha, k.ca = ca, k.sa = sa;
-    k.tlo = side ? float_down(-(D + R) * (1.0 + 1e-9)) : float_down((D - R) * (1.0 - 1e-9));
+    k.tlo = global ? -__builtin_inff()
+                   : (side ? float_down(-(D + R) * (1.0 + 1e-9)) : float_down((D - R) * (1.0 - 1e-9)));
     k.s = s;
     const int di = 2 * t + side;
     if (lane == 0) a.disks[di] = k;
@@ -1475,14 +1471,13 @@ struct rt_ctx {
   // positions and the scene stay the same
   int cg_mode = 1;    // RT_HIP_CAM_GRID: 0 off, 1 auto (a one-frame launch at a new position sweeps), 2 every launch
   int cg_n_opt = 0;   // RT_HIP_CAM_GRID_N (tuning build); 0 = kCgNStatic / kCgNMoving
-  int cg_k = 48;      // entries per cell (RT_HIP_CAM_GRID_K, tuning build)
-  int32_t *d_cg_count = nullptr, *d_cg_glist = nullptr, *d_cg_gcount = nullptr;
+  int32_t *d_cg_count = nullptr;
   int2 *d_cg_ent = nullptr;
   CgDisk *d_cg_disks = nullptr;
   int2 *d_cg_pairs = nullptr;
   unsigned *d_cg_npairs = nullptr;
-  size_t cg_count_cap = 0, cg_ent_cap = 0, cg_glist_cap = 0, cg_disks_cap = 0, cg_pairs_cap = 0, cg_npairs_cap = 0;  // bytes
-  int cg_n = 0, cg_ngrid = 0, cg_kb = 0;
+  size_t cg_count_cap = 0, cg_ent_cap = 0, cg_disks_cap = 0, cg_pairs_cap = 0, cg_npairs_cap = 0;  // bytes
+  int cg_n = 0, cg_ngrid = 0;
   std::vector<double> cg_pos;          // the grids' points (3 per grid)
   std::vector<double> cg_seen;         // the previous launch's camera positions
   unsigned long long cg_seen_gen = ~0ull;
@@ -1823,7 +1818,8 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
   for (int f = 1; f < ngrid; f++) pos.insert(pos.end(), c->fcams[f].position, c->fcams[f].position + 3);
   const int N = c->cg_n_opt ? c->cg_n_opt : (same ? kCgNStatic : kCgNMoving);
   const size_t cells = 6 * (size_t)N * N;
-  const bool cached = c->cg_gen == c->scene_gen && c->cg_n == N && c->cg_kb == c->cg_k && c->cg_ngrid == ngrid && c->cg_pos == pos;
+  if (ngrid * cells * kCgSlots >= (size_t(1) << 31)) return RT_OK;  // the scan's 32-bit slot index: no grid
+  const bool cached = c->cg_gen == c->scene_gen && c->cg_n == N && c->cg_ngrid == ngrid && c->cg_pos == pos;
   if (!cached && nf == 1 && c->cg_mode == 1 && !(c->cg_seen_gen == c->scene_gen && c->cg_seen == pos)) {
     // one frame from a position the previous launch did not use: the build
     // (~0.05 ms) costs more than the grid saves that frame (profiles/r4j/);
@@ -1840,11 +1836,9 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
     int rc = cg_tables(c, N, tab);
     if (rc != RT_OK) return rc;
     if ((rc = grow(c, c->d_cg_count, c->cg_count_cap, ngrid * cells * sizeof(int32_t))) != RT_OK ||
-        (rc = grow(c, c->d_cg_ent, c->cg_ent_cap, ngrid * cells * c->cg_k * sizeof(int2))) != RT_OK ||
-        (rc = grow(c, c->d_cg_glist, c->cg_glist_cap, (size_t)ngrid * (kCgMaxGlobal + 1) * sizeof(int32_t))) != RT_OK ||
+        (rc = grow(c, c->d_cg_ent, c->cg_ent_cap, ngrid * cells * kCgSlots * sizeof(int2))) != RT_OK ||
         (rc = grow(c, c->d_cg_npairs, c->cg_npairs_cap, (size_t)ngrid * kCgCntStride * sizeof(unsigned))) != RT_OK)
       return rc;
-    c->d_cg_gcount = c->d_cg_glist + (size_t)ngrid * kCgMaxGlobal;
     const long long nblocks = 6LL * tab->NB * tab->NB;
     if ((rc = grow(c, c->d_cg_disks, c->cg_disks_cap, 2 * (size_t)c->nsph * ngrid * sizeof(CgDisk))) != RT_OK ||
         (rc = grow(c, c->d_cg_pairs, c->cg_pairs_cap, 2 * (size_t)c->nsph * ngrid * nblocks * sizeof(int2))) != RT_OK)
@@ -1857,8 +1851,6 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
     b.tiles = tab->tiles;
     b.cell_cbsb = tab->cell;
     b.count = c->d_cg_count;
-    b.glist = c->d_cg_glist;
-    b.gcount = c->d_cg_gcount;
     b.ent = c->d_cg_ent;
     b.disks = c->d_cg_disks;
     b.pairs = c->d_cg_pairs;
@@ -1868,7 +1860,7 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
     b.N = N;
     b.NT = tab->NT;
     b.NB = tab->NB;
-    b.K = c->cg_k;
+    b.K = kCgSlots;
     b.ngrid = ngrid;
     for (int g = 0; g < ngrid; g++) {
       b.px[g] = pos[3 * g];
@@ -1882,7 +1874,6 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
       b.diam[g] = std::sqrt(d2);
     }
     RT_TRY(c, hipMemsetAsync(c->d_cg_count, 0, ngrid * cells * sizeof(int32_t), c->stream));
-    RT_TRY(c, hipMemsetAsync(c->d_cg_gcount, 0, ngrid * sizeof(int32_t), c->stream));
     RT_TRY(c, hipMemsetAsync(c->d_cg_npairs, 0, ngrid * kCgCntStride * sizeof(unsigned), c->stream));
     const int nthr = c->nsph * ngrid;
     hipLaunchKernelGGL(cg_disk_kernel, dim3((unsigned)((nthr + 3) / 4)), dim3(256), 0, c->stream, b);
@@ -1892,13 +1883,12 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
     RT_TRY(c, hipGetLastError());
     c->cg_gen = c->scene_gen;
     c->cg_n = N;
-    c->cg_kb = c->cg_k;
     c->cg_ngrid = ngrid;
     c->cg_pos = pos;
     c->cg_builds++;
     c->cg_build_ms += ms_since(t0);
   }
-  out = CgArgs{c->d_cg_count, c->d_cg_ent, c->d_cg_glist, c->d_cg_gcount, N, c->cg_k, 1, ngrid > 1 ? 1 : 0, ngrid};
+  out = CgArgs{c->d_cg_count, c->d_cg_ent, N, 1, ngrid > 1 ? 1 : 0, ngrid};
   return RT_OK;
 }
 
@@ -2350,7 +2340,6 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(8, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_CAM_GRID_N")) c->cg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
-  if (const char *e = std::getenv("RT_HIP_CAM_GRID_K")) c->cg_k = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID")) c->sg_mode = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID_N")) c->sg_n_opt = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_BEHIND_GRID")) c->ug_mode = std::max(-1, std::min(1, std::atoi(e)));
@@ -2409,7 +2398,6 @@ void rt_destroy(rt_ctx *c) {
   if (c->h_bperm) (void)hipHostFree(c->h_bperm);
   if (c->d_cg_count) (void)hipFree(c->d_cg_count);
   if (c->d_cg_ent) (void)hipFree(c->d_cg_ent);
-  if (c->d_cg_glist) (void)hipFree(c->d_cg_glist);  // d_cg_gcount lies inside it
   if (c->d_cg_disks) (void)hipFree(c->d_cg_disks);
   if (c->d_cg_pairs) (void)hipFree(c->d_cg_pairs);
   if (c->d_cg_npairs) (void)hipFree(c->d_cg_npairs);
