@@ -667,11 +667,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
 #pragma unroll
   for (int i = 0; i < (int)((kPixbufIds + 255) / 256); ++i)  // padding, depth 0 and deferred pixels: 0
     if ((size_t)(i * 256 + lane * 4) < kPixbufIds) reinterpret_cast<LdsU32 *>(pixbuf())[i * 64 + lane] = 0u;
-#ifdef RT_DRAIN
   const bool drain = kernarg_late<true, offsetof(RenderArgs, drain)>(a.drain) != 0;
-#else
-  constexpr bool drain = false;  // drain mode is an experimental build (-DRT_DRAIN)
-#endif
   if (lane < 2 * kMergeTiles) reinterpret_cast<LdsU32 *>(pixbuf() + kDefMaskOff)[lane] = 0u;
   const int depth = a.depth;
   const unsigned sstride = (unsigned)ca.npx;
@@ -1082,15 +1078,11 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
   if constexpr (kStack == kStackMerge) {
     // drain mode: the workgroups started, and (merge_tiles, or a padding one
     // here) done with their own tiles
-#ifdef RT_DRAIN
     if (a.drain && threadIdx.x == 0) atomicAdd(&a.counters[kStartedSlot], 1ull);
     if (slot >= a.nslots) {  // slot = this wave's group of tile slots (merge_tiles)
       if (a.drain && threadIdx.x == 0) atomicAdd(&a.counters[kDoneSlot], 1ull);
       return;
     }
-#else
-    if (slot >= a.nslots) return;  // slot = this wave's group of tile slots (merge_tiles)
-#endif
   } else {
     if (a.perm) {
       if (slot >= a.nslots) return;
@@ -2512,9 +2504,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH4")) c->bvh_wide = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0 ? 1 : 0;
-#ifdef RT_DRAIN
   if (const char *e = std::getenv("RT_HIP_DRAIN")) c->drain_mode = std::max(0, std::min(2, std::atoi(e)));
-#endif
   if (const char *e = std::getenv("RT_HIP_DEFER_WALK")) c->defer_walk = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_LEVEL")) c->defer_level = std::max(1, std::min(RT_MAX_DEPTH, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(8, std::min(64, std::atoi(e)));
