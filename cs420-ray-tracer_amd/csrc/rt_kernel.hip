@@ -699,28 +699,13 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
       unsigned long long avail = rfl64(__hip_atomic_load(&sc[kDeferSlot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       avail = avail < (unsigned long long)cap ? avail : (unsigned long long)cap;
       if (rfl64(__hip_atomic_load(&sc[kFetchSlot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= avail) continue;
-      // claim up to one entry per idle lane, never past the entries reserved
-      // so far (more may be reserved later: an over-claim would skip them)
       const unsigned long long idle = ~__ballot(act);
       const int fi = __builtin_ctzll(idle);
-      unsigned long long base = 0, take = 0;
-      if (lane == fi) {
-        unsigned long long f = __hip_atomic_load(&sc[kFetchSlot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (f < avail) {
-          const unsigned long long k = avail - f < (unsigned long long)__popcll(idle) ? avail - f : (unsigned long long)__popcll(idle);
-          if (__hip_atomic_compare_exchange_strong(&sc[kFetchSlot], &f, f + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)) {
-            base = f;
-            take = k;
-            break;
-          }
-        }
-      }
+      unsigned long long base = 0;
+      if (lane == fi) base = atomicAdd(&sc[kFetchSlot], (unsigned long long)__popcll(idle));
       base = __shfl(base, fi, 64);
-      take = __shfl(take, fi, 64);
-      const unsigned long long r = (unsigned long long)__popcll(idle & lt);
-      const unsigned long long i = base + r;
-      const bool got = !act && r < take;
+      const unsigned long long i = base + (unsigned long long)__popcll(idle & lt);
+      const bool got = !act && i < avail;
       if (got) {
         QRay *e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq) +
                   RT_CK(kCkDeferQ, (size_t)sh * (size_t)cap + i, (long long)kShards * cap);
