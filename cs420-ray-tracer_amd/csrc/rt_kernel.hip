@@ -100,9 +100,6 @@ struct RenderArgs {
   int rows_dword;                 // kStackMerge: every 8-pixel tile row starts dword aligned (flush_tile)
   int defer_level;                // kStackMerge: rays of this reflection level and deeper are deferred
   int xcd_frames;                 // multi-frame launches: every frame of a tile group on one XCD (render_kernel)
-  int drain;                      // kStackMerge + dq: merge_tiles waves run the deferred rays themselves (no
-                                  // render_deferred launch): queue shards per XCD, entries tagged by `tag`
-  unsigned tag;                   // this launch's deferred-entry tag (QRay::orig = tag << 8 | level)
 };
 // the whole struct is the kernel's argument block (kernarg segment, at most 4 KiB)
 static_assert(sizeof(RenderArgs) <= 4096, "RenderArgs exceeds the kernel-argument segment");
@@ -523,20 +520,11 @@ constexpr int kDeferSlot = 7;
 // merge_tiles' LDS: the finished pixels (RGB8, 192 B per tile), then the tile ids
 constexpr size_t kPixbufIds = (size_t)kMergeTiles * 64 * 3;
 constexpr size_t kPixbufBytes = kPixbufIds + (size_t)kMergeTiles * 8;  // + (tile id, row-0 offset) per tile
-constexpr size_t kPixbufAll = kPixbufBytes + (size_t)kMergeTiles * 8;  // + deferred-pixel masks (drain mode)
 // u64 slot of a counter shard: the deferred kernels' next queue entry of that
 // shard segment (lanes take entries dynamically; zeroed with the launch's counters)
 constexpr int kFetchSlot = 24;
-// drain mode (RenderArgs::drain): shard 0's u64 slots counting the launch's
-// workgroups that started and that finished their own tiles
-constexpr int kStartedSlot = 25, kDoneSlot = 26;
-constexpr size_t kDefMaskOff = kPixbufBytes;  // + the deferred pixels of each tile slot (u64), drain mode
 constexpr long long kSchedMinTiles = 1024;  // launches with fewer 8x8 tiles keep scanline order
 
-__device__ __forceinline__ unsigned long long rfl64(unsigned long long v) {  // lane 0's value, wave-uniform
-  return (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v) |
-         (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32)) << 32;
-}
 // A pixel's final colour quantised as write_ppm (main.cpp:85), packed r | g << 8 | b << 16.
 __device__ __forceinline__ unsigned pack_px(D3 c, unsigned &c_neg) {
   const int q0 = quantize(c.x), q1 = quantize(c.y), q2 = quantize(c.z);
@@ -593,28 +581,7 @@ __device__ __forceinline__ void put_px(uint8_t *p, unsigned v) {
 // 0 for render_deferred's or_px.
 typedef __attribute__((address_space(3))) unsigned char LdsU8;
 typedef __attribute__((address_space(3))) unsigned LdsU32;
-typedef __attribute__((address_space(3))) unsigned long long LdsU64;
-// Drain mode: a tile row dword (lane < 48: row lane / 6, dword lane % 6) whose
-// bytes include deferred pixels (dmask: bit y * 8 + x) keeps those bytes --
-// the deferred rays' put_px writes them, before or after this -- and takes
-// the others by atomics; a dword without deferred bytes is a plain store.
-__device__ __forceinline__ void store_row_dword(unsigned *p, unsigned v, unsigned long long dmask, int lane) {
-  unsigned bm = 0;
-  if (dmask) {
-    const int r = lane / 6, c = lane - 6 * (lane / 6);
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if ((dmask >> (r * 8 + (4 * c + b) / 3)) & 1ull) bm |= 0xFFu << (8 * b);
-  }
-  if (bm == 0) {
-    *p = v;
-  } else if (bm != 0xFFFFFFFFu) {
-    atomicAnd(p, bm | v);
-    atomicOr(p, v & ~bm);
-  }
-}
-__device__ __forceinline__ void flush_tile(const RenderArgs &a, int tile, int frame, const LdsU8 *pb,
-                                           unsigned long long dmask = 0) {
+__device__ __forceinline__ void flush_tile(const RenderArgs &a, int tile, int frame, const LdsU8 *pb) {
   const int lane = (int)(threadIdx.x & 63);
   const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
   const Rows &rows = kernarg_late<true, offsetof(RenderArgs, rows)>(a.rows);
@@ -628,9 +595,8 @@ __device__ __forceinline__ void flush_tile(const RenderArgs &a, int tile, int fr
   if (rows_dword && x0 + 8 <= W && ty * 8 + 8 <= rows.count) {  // wave-uniform: the usual case
     if (lane < 48) {  // lane: row lane / 6, dword lane % 6 = LDS dword lane
       const unsigned v = reinterpret_cast<const LdsU32 *>(pb)[lane];
-      store_row_dword(reinterpret_cast<unsigned *>(row_at(0) + (unsigned)(lane / 6) * (unsigned)W * 3u +
-                                                   4u * (unsigned)(lane - 6 * (lane / 6))),
-                      v, dmask, lane);
+      *reinterpret_cast<unsigned *>(row_at(0) + (unsigned)(lane / 6) * (unsigned)W * 3u +
+                                    4u * (unsigned)(lane - 6 * (lane / 6))) = v;
     }
     return;
   }
@@ -639,15 +605,14 @@ __device__ __forceinline__ void flush_tile(const RenderArgs &a, int tile, int fr
   };
   {
     const int r = lane / 6, c = lane - 6 * (lane / 6);  // lanes 0..47: row r, dword c = LDS dword lane
-    if (lane < 48 && whole(r))
-      store_row_dword(reinterpret_cast<unsigned *>(row_at(r)) + c, reinterpret_cast<const LdsU32 *>(pb)[lane], dmask, lane);
+    if (lane < 48 && whole(r)) reinterpret_cast<unsigned *>(row_at(r))[c] = reinterpret_cast<const LdsU32 *>(pb)[lane];
   }
   {
     // rows that are not whole (the image's right edge, odd widths): the
     // lane's own pixel into the dwords it shares with its neighbours (which
     // other waves may be writing): its bytes cleared and set by dword atomics
     const int r = lane >> 3, x = x0 + (lane & 7);
-    if (!whole(r) && ty * 8 + r < rows.count && x < W && !((dmask >> lane) & 1ull)) {
+    if (!whole(r) && ty * 8 + r < rows.count && x < W) {
       const LdsU8 *p = pb + lane * 3;
       put_px(row_at(r) + (lane & 7) * 3, (unsigned)p[0] | (unsigned)p[1] << 8 | (unsigned)p[2] << 16);
     }
@@ -667,8 +632,6 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
 #pragma unroll
   for (int i = 0; i < (int)((kPixbufIds + 255) / 256); ++i)  // padding, depth 0 and deferred pixels: 0
     if ((size_t)(i * 256 + lane * 4) < kPixbufIds) reinterpret_cast<LdsU32 *>(pixbuf())[i * 64 + lane] = 0u;
-  const bool drain = kernarg_late<true, offsetof(RenderArgs, drain)>(a.drain) != 0;
-  if (lane < 2 * kMergeTiles) reinterpret_cast<LdsU32 *>(pixbuf() + kDefMaskOff)[lane] = 0u;
   const int depth = a.depth;
   const unsigned sstride = (unsigned)ca.npx;
   int qn = 0;        // queued rays q[0 .. qn), wave-uniform, < Q between passes
@@ -679,55 +642,6 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
   int key = -1, dleft = 0, lev = 0;
   unsigned pix = 0;
   int lidx = 0;  // the pixel's place in the group: tile slot * 64 + y * 8 + x (pixbuf byte 3 * lidx)
-  bool gray = false;      // drain mode: this lane's ray came from the deferred queue (its pixel: pix + fpx)
-  bool draining = false;  // drain mode: the group's own tiles are done; the wave runs queued deferred rays
-  bool last_look = false;  // drain mode: every group is done; the queue's next empty look ends the wave
-  const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 7u;  // XCC_ID: this wave's XCD
-  unsigned ds = 0;        // drain mode: the next of the XCD's shard segments to take rays from
-  // drain mode: idle lanes take entries of this XCD's shard segments (shard
-  // xcc + 8 k): true when some lane got one.  An entry's fields are read from
-  // memory once its tag shows the writer finished it (merge_tiles' producers
-  // write the fields through to memory, wait for their completion, then the tag).
-  auto drain_fetch = [&]() -> bool {
-    const int cap = kernarg_late<true, offsetof(RenderArgs, dq_cap)>(a.dq_cap);
-    unsigned long long *ctr = kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters);
-    const unsigned tag = kernarg_late<true, offsetof(RenderArgs, tag)>(a.tag);
-    const unsigned ds0 = ds;
-    for (int k = 0; k < kShards / 8; ++k) {
-      const unsigned j = (ds0 + (unsigned)k) & (kShards / 8 - 1), sh = xcc + 8u * j;
-      unsigned long long *sc = ctr + (size_t)sh * kShardStride;
-      unsigned long long avail = rfl64(__hip_atomic_load(&sc[kDeferSlot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      avail = avail < (unsigned long long)cap ? avail : (unsigned long long)cap;
-      if (rfl64(__hip_atomic_load(&sc[kFetchSlot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= avail) continue;
-      const unsigned long long idle = ~__ballot(act);
-      const int fi = __builtin_ctzll(idle);
-      unsigned long long base = 0;
-      if (lane == fi) base = atomicAdd(&sc[kFetchSlot], (unsigned long long)__popcll(idle));
-      base = __shfl(base, fi, 64);
-      const unsigned long long i = base + (unsigned long long)__popcll(idle & lt);
-      const bool got = !act && i < avail;
-      if (got) {
-        QRay *e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq) +
-                  RT_CK(kCkDeferQ, (size_t)sh * (size_t)cap + i, (long long)kShards * cap);
-        auto ld = [](auto *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
-        unsigned t;
-        do {
-          t = (unsigned)ld(&e->orig);
-        } while ((t >> 8) != tag);
-        o = mk(ld(&e->ox), ld(&e->oy), ld(&e->oz));
-        d = mk(ld(&e->dx), ld(&e->dy), ld(&e->dz));
-        lev = (int)(t & 255u);
-        dleft = ld(&e->dleft);
-        key = ld(&e->key);
-        pix = (unsigned)ld(&e->pix) - ca.fpx;
-        gray = true;
-        act = true;
-      }
-      ds = j;
-      if (__ballot(got)) return true;
-    }
-    return false;
-  };
   // pops queued rays into the lanes without one (lanes ranked by lane id)
   auto refill = [&](unsigned long long busy) {
     const int take = (64 - __popcll(busy)) < qn ? (64 - __popcll(busy)) : qn;
@@ -808,32 +722,8 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         if (__ballot(act) == 0) continue;
       } else if (qn > 0) {
         refill(0ull);
-      } else if (!drain) {
+      } else {
         break;
-      } else if (!draining) {  // the group pushes no more: counted done once its pushes completed
-        draining = true;
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-        if (lane == 0) atomicAdd(&kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters)[kDoneSlot], 1ull);
-      }
-    }
-    // drain mode: idle lanes take queued deferred rays (one call site)
-    if (draining && ~__ballot(act)) {
-      const bool got = drain_fetch();
-      if (!got && __ballot(act) == 0) {
-        // nothing queued on this XCD: wait while every workgroup has started
-        // (then waiting blocks none) and some group may still push, else leave;
-        // once every group is done (done counts after its pushes), one last look
-        unsigned long long *ctr = kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters);
-        const unsigned long long total = gridDim.x;
-        if (last_look) break;
-        if (rfl64(__hip_atomic_load(&ctr[kDoneSlot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= total) {
-          last_look = true;
-        } else if (rfl64(__hip_atomic_load(&ctr[kStartedSlot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < total) {
-          break;
-        } else {
-          __builtin_amdgcn_s_sleep(16);
-        }
-        continue;
       }
     }
     int outcome = 0, nkey = 0;
@@ -857,7 +747,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         key = nkey;
         --dleft;
         ++c_reflect;
-        defer = !gray && lev >= kernarg_late<true, offsetof(RenderArgs, defer_level)>(a.defer_level);
+        defer = lev >= kernarg_late<true, offsetof(RenderArgs, defer_level)>(a.defer_level);
       } else {  // the chain ends: unwind its pixel's stack and store it
         D3 res = color;
         while (lev > 0) {
@@ -865,16 +755,8 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
           const StackEnt e = ca.gstack[RT_CK(kCkStack, sidx + (unsigned)lev * sstride, (long long)(depth - 1) * sstride)];
           res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
         }
-        const unsigned v = pack_px(res, c_neg);
-        if (gray) {  // a deferred ray's pixel: its bytes only (flush_tile leaves them alone)
-          const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
-          const unsigned npx_frame = (unsigned)((size_t)kernarg_late<true, offsetof(RenderArgs, rows)>(a.rows).count * od.xw);
-          const unsigned f = sidx / npx_frame;
-          put_px(static_cast<uint8_t *>(od.ptr) + (size_t)RT_CK(kCkOut, f, a.frames) * (size_t)od.fstride +
-                     (size_t)(sidx - f * npx_frame) * 3,
-                 v);
-          gray = false;
-        } else {
+        {
+          const unsigned v = pack_px(res, c_neg);
           LdsU8 *p = pixbuf() + 3 * RT_CK(kCkPixbuf, lidx, kMergeTiles * 64);
           p[0] = (unsigned char)v;
           p[1] = (unsigned char)(v >> 8);
@@ -891,30 +773,15 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
       if (cap > 0) {
         unsigned long long base = 0;
         const int first = __builtin_ctzll(dm);
-        // drain mode: this XCD's shard segments (xcc + 8 k), so the rays stay in its L2
-        const unsigned shard = drain ? xcc + 8u * ((blockIdx.x >> 3) & (unsigned)(kShards / 8 - 1)) : blockIdx.x % kShards;
-        unsigned long long *sc = kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters) + (size_t)shard * kShardStride;
-        if (lane == first) base = atomicAdd(&sc[kDeferSlot], (unsigned long long)__popcll(dm));
+        if (lane == first) base = atomicAdd(&counter_shard(kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters))[kDeferSlot],
+                                            (unsigned long long)__popcll(dm));
         base = __shfl(base, first, 64);
         const unsigned long long slot = base + (unsigned long long)__popcll(dm & lt);
         if (defer && slot < (unsigned long long)cap) {
-          QRay *dq = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq) +
-                     RT_CK(kCkDeferQ, (size_t)shard * (size_t)cap + slot, (long long)kShards * cap);
-          if (drain) {
-            // the fields, then (once they completed) the tag that releases the
-            // entry; system-scope stores go through to memory, so a reader on
-            // any XCD sees them whatever its L2 holds
-            auto st = [](auto *p, auto v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
-            st(&dq->ox, o.x), st(&dq->oy, o.y), st(&dq->oz, o.z), st(&dq->dx, d.x), st(&dq->dy, d.y), st(&dq->dz, d.z);
-            st(&dq->dleft, dleft), st(&dq->key, key), st(&dq->pix, (int)sidx);
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-            st(&dq->orig, (int)(kernarg_late<true, offsetof(RenderArgs, tag)>(a.tag) << 8 | (unsigned)lev));
-            // the pixel's bytes are the deferred ray's: the tile's flush skips them
-            __hip_atomic_fetch_or((LdsU64 *)(pixbuf() + kDefMaskOff) + (lidx >> 6), 1ull << (lidx & 63), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            *dq = QRay{o.x, o.y, o.z, d.x, d.y, d.z, lev, dleft, key, (int)sidx};
-          }
+          QRay *dq = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq);
+          const unsigned wg = blockIdx.x;
+          dq[RT_CK(kCkDeferQ, (size_t)(wg % kShards) * (size_t)cap + slot, (long long)kShards * cap)] =
+              QRay{o.x, o.y, o.z, d.x, d.y, d.z, lev, dleft, key, (int)sidx};
           act = false;
         }
       }
@@ -943,17 +810,15 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     for (int t = 0; t < kMergeTiles; ++t) {
       if (t >= next) break;
       const unsigned off = __builtin_amdgcn_readfirstlane(ids[2 * t + 1]);
-      const unsigned long long dmask = drain ? rfl64(reinterpret_cast<const LdsU64 *>(pixbuf() + kDefMaskOff)[t]) : 0ull;
       if (off != 0xFFFFFFFFu) {
         if (lane < 48) {
           const unsigned v = reinterpret_cast<const LdsU32 *>(pixbuf() + 192 * t)[lane];
-          store_row_dword(reinterpret_cast<unsigned *>(
-                              out + RT_CK(kCkOut, (size_t)off + roff,
-                                          (long long)(kernarg_late<true, offsetof(RenderArgs, rows)>(a.rows).count) * W * 3 - 3)),
-                          v, dmask, lane);
+          *reinterpret_cast<unsigned *>(
+              out + RT_CK(kCkOut, (size_t)off + roff,
+                          (long long)(kernarg_late<true, offsetof(RenderArgs, rows)>(a.rows).count) * W * 3 - 3)) = v;
         }
       } else {
-        flush_tile(a, (int)__builtin_amdgcn_readfirstlane(ids[2 * t]), frame, pixbuf() + 192 * t, dmask);
+        flush_tile(a, (int)__builtin_amdgcn_readfirstlane(ids[2 * t]), frame, pixbuf() + 192 * t);
       }
     }
   }
@@ -1061,13 +926,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
   }
   int tile = slot;
   if constexpr (kStack == kStackMerge) {
-    // drain mode: the workgroups started, and (merge_tiles, or a padding one
-    // here) done with their own tiles
-    if (a.drain && threadIdx.x == 0) atomicAdd(&a.counters[kStartedSlot], 1ull);
-    if (slot >= a.nslots) {  // slot = this wave's group of tile slots (merge_tiles)
-      if (a.drain && threadIdx.x == 0) atomicAdd(&a.counters[kDoneSlot], 1ull);
-      return;
-    }
+    if (slot >= a.nslots) return;  // slot = this wave's group of tile slots (merge_tiles)
   } else {
     if (a.perm) {
       if (slot >= a.nslots) return;
@@ -1112,7 +971,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
   if constexpr (kStack == kStackMerge && !kLdsGeo && kSamples == 1) {
     // the wave's ray queue sits where trace_wave parks colours, after the
     // finished-pixel bytes (launch_tiles)
-    QRay *q = reinterpret_cast<QRay *>(reinterpret_cast<unsigned char *>(ca.park) + kPixbufAll);
+    QRay *q = reinterpret_cast<QRay *>(reinterpret_cast<unsigned char *>(ca.park) + kPixbufBytes);
     merge_tiles<kCull, kFast>(g, rad, sm, slight, a, slot, frame, ca, q, work, sums);
   } else {
     trace_tile<kCull, kSamples, kStack, !kLdsGeo>(g, rad, sm, slight, a.n, a.nl, a.amb, kernarg_cam(frame), a.W, a.H,
@@ -1700,10 +1559,6 @@ struct rt_ctx {
   // without it, profiles/r3n/ab_knobs.log; 32-frame launches are 13 % slower
   // per frame without it)
   int defer = -1;
-  int drain_mode = 0;   // RT_HIP_DRAIN (tuning build): 0 render_deferred, 1 merged kernels drain multi-frame
-                        // launches' deferred rays, 2 every launch's (one-frame launches defer too)
-  int drain_last = 0;
-  unsigned long long dq_tag = 0;
   bool defer_walk = true;     // RT_HIP_DEFER_WALK: deferred rays of a scene whose closest hits always walk the BVH use render_deferred_walk
   int merge_q = 64;           // kStackMerge: the launch's LDS queue entries per wave (launch_render4 picks it)
   int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (8, 16, 32 or 64)
@@ -2213,7 +2068,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
   if (!kLds && kStack == kStackGlobal) lds += (size_t)kWg * 64 * sizeof(D3);  // parked colours (trace_wave)
   if (kStack == kStackMerge)  // the wave's ray queue and finished pixels (merge_tiles)
-    lds += (size_t)c->merge_q * sizeof(QRay) + kPixbufAll;
+    lds += (size_t)c->merge_q * sizeof(QRay) + kPixbufBytes;
   StackEnt *gstack = nullptr;
   if (depth > 1) {
     // the kernel indexes the stack with 32 bits: entry + level * npx < 2^32
@@ -2298,10 +2153,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.rows_dword = ((reinterpret_cast<uintptr_t>(od.ptr) | (uintptr_t)(3 * (size_t)W) | (uintptr_t)od.fstride) & 3) == 0;
   ra.defer_level = c->defer_level;
   ra.xcd_frames = xcd_frames ? 1 : 0;
-  ra.drain = 0;
-  ra.tag = (unsigned)(++c->dq_tag % 0xFFFFFFull) + 1u;  // a fresh tag per launch (0: never)
-  if (kStack == kStackMerge && (c->defer > 0 || (c->defer < 0 && (nf > 1 || c->drain_mode == 2))) &&
-      depth > c->defer_level) {
+  if (kStack == kStackMerge && (c->defer > 0 || (c->defer < 0 && nf > 1)) && depth > c->defer_level) {
     // room for 1/8 of the launch's pixels (deferred rays are ~2 % on synth200); a ray
     // that finds its shard segment full simply continues in its merge_tiles lane
     const size_t npx = (size_t)rows.count * od.xw * nf;
@@ -2313,7 +2165,6 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       c->dq_buf = nullptr;
       c->dq_bytes = 0;
       RT_TRY(c, hipMalloc(&c->dq_buf, need));
-      RT_TRY(c, hipMemsetAsync(c->dq_buf, 0, need, c->stream));  // tag 0: never a launch's
       c->dq_bytes = need;
     }
     if (cap < (size_t)1 << 30) {
@@ -2336,15 +2187,11 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       ra.sg = SgArgs{c->d_sg_start, c->d_sg_ent, c->d_sg_rho2, c->sg_n, 1, c->sg_nstart, c->sg_nent, c->nsph};
     c->cg_last = ra.cg.on != 0;
     c->cg_last_n = ra.cg.on ? ra.cg.N : 0;
-    // drain mode: the merged kernel's waves run the deferred rays as they run
-    // out of tiles, no second kernel
-    if (fast && ra.dq_cap > 0 && c->drain_mode > 0 && (nf > 1 || c->drain_mode == 2)) ra.drain = 1;
-    c->drain_last = ra.drain ? 2 : (ra.dq_cap > 0 ? 1 : 0);
     if (fast)
       hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, true>), grid, dim3(64 * kWg), lds, c->stream, ra);
     else
       hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
-    if (ra.dq_cap > 0 && !ra.drain) {  // 48 one-wave workgroups per shard segment
+    if (ra.dq_cap > 0) {  // 48 one-wave workgroups per shard segment
       // the walk kernel where every closest hit walks the BVH anyway (large
       // scenes: synth10k 12.2 -> 11.0 ms per 8-frame launch); small scenes keep
       // the cull sweeps (synth200 1 % slower on the walk kernel)
@@ -2357,7 +2204,6 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     }
   } else {
     RT_TRY(c, mark_start(c));
-    c->drain_last = ra.dq_cap > 0 ? 1 : 0;
     hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
     if constexpr (kStack == kStackMerge) {
       if (ra.dq_cap > 0)
@@ -2380,7 +2226,7 @@ int launch_render4(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dept
       const size_t stacks = bv.ordered ? (size_t)bv.odepth * 64 * sizeof(int2) : 0;
       if (od.fmt == RT_FB_RGB8 && !od.full && od.x0 == 0 && od.xw == W)
         for (int q = c->merge_q_max; q >= 8; q /= 2)  // the longest queue that keeps 12 waves per CU
-          if (12 * (stacks + (size_t)q * sizeof(QRay) + kPixbufAll + ((lds + 31) & ~(size_t)31)) <= 160 * 1024) {
+          if (12 * (stacks + (size_t)q * sizeof(QRay) + kPixbufBytes + ((lds + 31) & ~(size_t)31)) <= 160 * 1024) {
             c->merge_q = q;
             return launch_tiles<kLds, kCull, 1, kStackMerge>(c, lds, cam, W, H, depth, rows, od);
           }
@@ -2489,7 +2335,6 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH4")) c->bvh_wide = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0 ? 1 : 0;
-  if (const char *e = std::getenv("RT_HIP_DRAIN")) c->drain_mode = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER_WALK")) c->defer_walk = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_LEVEL")) c->defer_level = std::max(1, std::min(RT_MAX_DEPTH, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(8, std::min(64, std::atoi(e)));
@@ -3025,7 +2870,6 @@ int rt_get_info(rt_ctx *c, rt_info *out) {
   out->behind_grid_cells = c->ug_ok ? (uint64_t)c->ug.nx * (uint64_t)c->ug.ny * (uint64_t)c->ug.nz : 0;
   out->behind_grid_entries = c->ug_ok ? (uint64_t)c->ug_entries : 0;
   out->behind_grid_build_ms = c->ug_build_ms;
-  out->deferred_last = c->drain_last;
   return RT_OK;
 }
 

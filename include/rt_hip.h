@@ -52,9 +52,9 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 11 /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
+#define RT_HIP_ABI_VERSION 10 /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
                                    6: rt_render_tiles; 7: rt_get_info; 8: rt_info sphere-grid fields;
-                                   9: rt_info behind-grid fields; 10: RT_ERR_CHECK; 11: rt_info deferred_last */
+                                   9: rt_info behind-grid fields; 10: RT_ERR_CHECK */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -279,9 +279,6 @@ typedef struct rt_info {
     uint64_t behind_grid_cells;  /* its cells */
     uint64_t behind_grid_entries;  /* its list entries (20 bytes each) */
     double behind_grid_build_ms; /* host wall time of its build, part of upload_ms */
-    int32_t deferred_last;       /* the most recent launch's deep reflection rays: 0 not deferred, 1 a second
-                                    kernel (render_deferred), 2 run by the merged kernel's own waves */
-    int32_t reserved0;
 } rt_info;
 int rt_get_info(rt_ctx *ctx, rt_info *out);
 

@@ -12,9 +12,4 @@ if [ -n "$TIMELINE" ]; then
   RT_HIP_LIB=$PWD/build_variants/librt_hip_stamps.so RT_HIP_STAMPS_FILE=/tmp/tl.bin timeout -k 10 120 python scripts/timeline_frames.py synth200 1920 1080 4 1 > $O/timeline_synth200_f1.log 2>&1 || { echo tl-fail; tail -3 $O/timeline_synth200_f1.log; exit 1; }
   RT_HIP_LIB=$PWD/build_variants/librt_hip_stamps.so RT_HIP_STAMPS_FILE=/tmp/tl.bin timeout -k 10 120 python scripts/timeline_frames.py complex 3840 2160 4 1 > $O/timeline_complex4k_f1.log 2>&1 || { echo tl-fail; tail -3 $O/timeline_complex4k_f1.log; exit 1; }
 fi
-if [ -n "$TRACE10K" ]; then
-  R="$PWD"
-  (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/trace10k" -o run -- \
-    python3 "$R/bench.py" --no-cpu-baseline --no-also --no-extras --workload synth10k_3840x2160_d6 --steps 32 --warmup 16 > "$R/$O/trace10k.json" 2> "$R/$O/trace10k.err") || { echo trace10k-fail; tail -3 $O/trace10k.err; exit 1; }
-fi
 echo all-ok
