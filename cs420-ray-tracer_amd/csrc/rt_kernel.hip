@@ -28,6 +28,7 @@
 #pragma clang fp contract(off)
 
 #include "rt_device.h"
+#include "rt_cgbuild.h"
 #include "rt_sched.h"
 
 #include <chrono>
@@ -1259,11 +1260,6 @@ __global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__rest
 // cg_disk_kernel (a wave per grid and sphere: the disks and the (disk, block)
 // pairs they meet), cg_bin_kernel (a wave per quarter pair: tiles, cells,
 // slots), cg_sort_kernel (a thread per cell: (tlo, index) order).
-struct CgDisk {  // one side of a sphere seen from a grid's point
-  double ux, uy, uz, alpha, ca, sa;
-  float tlo;
-  int s;
-};
 struct CgBuild {
   const SphGeo *geo;
   const double *rad;
@@ -1279,24 +1275,6 @@ struct CgBuild {
 };
 static_assert(sizeof(CgBuild) <= 4096, "CgBuild exceeds the kernel-argument segment");
 
-__device__ __forceinline__ float float_down(double x) {  // x rounded down to fp32
-  float f = (float)x;
-  if ((double)f > x) {
-    const int b = __float_as_int(f);
-    f = f == 0.0f ? -0x1p-149f : __int_as_float(f > 0.0f ? b - 1 : b + 1);
-  }
-  return f;
-}
-// angle(u, patch centre) <= alpha + rad + slack (the host builder's meets())
-__device__ __forceinline__ bool cg_meets(const CgDisk &k, double cx, double cy, double cz, double rad, double cb,
-                                         double sb) {
-  if (k.alpha + rad + kLgSlack >= 3.14159) return true;
-  return k.ux * cx + k.uy * cy + k.uz * cz >= k.ca * cb - k.sa * sb - 1e-12;
-}
-__device__ __forceinline__ bool cg_meets(const CgDisk &k, const CubePatch &p) {
-  return cg_meets(k, p.cx, p.cy, p.cz, p.rad, p.cb, p.sb);
-}
-
 constexpr int kCgCntStride = 64;
 // Pass 1, a wave per (grid, sphere): its two disks (one for a global sphere), and
 // every (disk, block) pair whose face and block patches the disk meets (a
@@ -1306,27 +1284,15 @@ __global__ __launch_bounds__(256) void cg_disk_kernel(const CgBuild a) {
   if (t >= a.n * a.ngrid) return;
   const int grid = t / a.n, s = t - grid * a.n;
   const SphGeo sp = a.geo[s];
-  const double vx = sp.cx - a.px[grid], vy = sp.cy - a.py[grid], vz = sp.cz - a.pz[grid];
-  const double D = __builtin_sqrt(vx * vx + vy * vy + vz * vz);
-  const double R = a.rad[s] * (1.0 + 1e-6) + 1e-6 * (D + a.diam[grid]);
-  // a sphere containing (or nearly containing) P, or non-finite: one disk of
-  // every direction (alpha >= pi meets every patch), tlo = -inf
-  const bool global = !__builtin_isfinite(D) || !__builtin_isfinite(R) || !(D > R);
-  const double alpha = global ? 4.0 : asin(R / D) + kLgSlack, ca = cos(alpha), sa = sin(alpha);
+  const CgView v = cg_view(sp.cx, sp.cy, sp.cz, a.rad[s], a.px[grid], a.py[grid], a.pz[grid], a.diam[grid]);
   const int nb = 6 * a.NB * a.NB;
-  for (int side = 0; side < (global ? 1 : 2); ++side) {
-    const double sg = side ? -1.0 : 1.0;
-    CgDisk k;
-    k.ux = global ? 1.0 : sg * (vx / D), k.uy = global ? 0.0 : sg * (vy / D), k.uz = global ? 0.0 : sg * (vz / D);
-    k.alpha = alpha, k.ca = ca, k.sa = sa;
-    k.tlo = global ? -__builtin_inff()
-                   : (side ? float_down(-(D + R) * (1.0 + 1e-9)) : float_down((D - R) * (1.0 - 1e-9)));
-    k.s = s;
+  for (int side = 0; side < (v.global ? 1 : 2); ++side) {
+    const CgDisk k = cg_side(v, side, s);
     const int di = 2 * t + side;
     if (lane == 0) a.disks[di] = k;
     for (int b0 = 0; b0 < nb; b0 += 64) {
       const int b = b0 + lane;
-      const bool m = b < nb && cg_meets(k, a.faces[b / (a.NB * a.NB)]) && cg_meets(k, a.blocks[b]);
+      const bool m = b < nb && cg_block(k, a.faces, a.blocks, a.NB, b);
       const unsigned long long bm = __ballot(m);
       if (!bm) continue;
       unsigned q0 = 0;
@@ -1357,17 +1323,11 @@ __global__ __launch_bounds__(64) void cg_bin_kernel(const CgBuild a) {
     const unsigned item = v - (grid ? __shfl(incl, grid - 1, 64) : 0u);
     const int2 pr = a.pairs[(size_t)grid * a.maxp + (item >> 2)];
     const CgDisk k = a.disks[pr.x];
-    const bool wide = k.alpha + kLgSlack >= 3.0;
+    const bool wide = cg_wide(k);
     const int bb = pr.y;
     const int f = bb / (a.NB * a.NB), bj = (bb / a.NB) % a.NB, bi = bb % a.NB;
-    const int ti = bi * kCubeB + (lane & 7), tj = bj * kCubeB + (lane >> 3);
-    bool tm = false, inside = false;
-    if (ti < a.NT && tj < a.NT) {
-      const CubePatch tp = a.tiles[((size_t)f * a.NT + tj) * a.NT + ti];
-      tm = cg_meets(k, tp);
-      inside = tm && k.alpha < 3.0 && k.alpha > tp.rad + 1e-3 &&
-               k.ux * tp.cx + k.uy * tp.cy + k.uz * tp.cz >= cos(k.alpha - tp.rad - 1e-3);
-    }
+    bool tm, inside;
+    cg_tile(k, a.tiles, a.NT, f, bi, bj, lane, tm, inside);
     unsigned long long tmask = __ballot(tm) & (0xffffull << (16 * (item & 3)));
     const unsigned long long imask = __ballot(inside);
     while (tmask) {  // up to 4 tiles a round: their cells' slot atomics in flight together
@@ -1378,29 +1338,7 @@ __global__ __launch_bounds__(64) void cg_bin_kernel(const CgBuild a) {
         if (!tmask) continue;
         const int tl = __builtin_ctzll(tmask);
         tmask &= tmask - 1;
-        const bool tin = (imask >> tl) & 1ull;
-        const int i = (bi * kCubeB + (tl & 7)) * kCubeT + (lane & 7), j = (bj * kCubeB + (tl >> 3)) * kCubeT + (lane >> 3);
-        bool cm = false;
-        if (i < a.N && j < a.N) {
-          if (tin) {
-            cm = true;
-          } else {  // the cell's patch: centre formed as face_dir does, cos / sin of rad + slack from the table
-            const double fa = -1.0 + (2.0 * i + 1.0) / a.N, fb = -1.0 + (2.0 * j + 1.0) / a.N;
-            double dx, dy, dz;
-            switch (f) {
-              case 0: dx = 1.0, dy = fa, dz = fb; break;
-              case 1: dx = -1.0, dy = fa, dz = fb; break;
-              case 2: dx = fa, dy = 1.0, dz = fb; break;
-              case 3: dx = fa, dy = -1.0, dz = fb; break;
-              case 4: dx = fa, dy = fb, dz = 1.0; break;
-              default: dx = fa, dy = fb, dz = -1.0; break;
-            }
-            const double l = __builtin_sqrt(dx * dx + dy * dy + dz * dz);
-            const size_t ij = (size_t)j * a.N + i;
-            cm = cg_meets(k, dx / l, dy / l, dz / l, wide ? 3.2 : 0.0, a.cell_cbsb[2 * ij], a.cell_cbsb[2 * ij + 1]);
-          }
-        }
-        if (cm) gcs[u] = (f * a.N + j) * a.N + i;
+        gcs[u] = cg_cell(k, wide, a.cell_cbsb, a.N, f, bi, bj, tl, lane, (imask >> tl) & 1ull);
       }
       int slots[4];
 #pragma unroll

@@ -150,6 +150,27 @@ def test_camera_grid_lists_and_scan(tmp_path):
     assert w[4] == "0" and w[6] == "0", out.stdout
 
 
+def test_camera_grid_device_builder(tmp_path):
+    """The device camera-grid builder's per-lane functions (csrc/rt_cgbuild.h,
+    shared with rt_kernel.hip's cg_disk / cg_bin kernels) run lane by lane in
+    the kernels' pass structure on the CPU, 1-3 grids per scene
+    (tests/native/cg_device_check.cpp): every cell within its 48 slots lists
+    exactly build_point_grid's entries in (tlo, index) order, every sphere the
+    reference's test reports on a camera ray (either sign of t) is on the
+    looked-up list with tlo <= t, and cam_closest's early-exit scan returns
+    find_intersection's (t, index) -- the same random scenes, cameras and
+    silhouette rays as the host-builder check."""
+    exe = tmp_path / "cg_device_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-o", str(exe),
+                    os.path.join(REPO, "tests", "native", "cg_device_check.cpp"),
+                    os.path.join(CSRC, "rt_lightgrid.cpp"), "-lpthread"], check=True)
+    out = subprocess.run([str(exe), "60"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    w = out.stdout.split()
+    assert w[0] == "checked" and int(w[1]) > 100000 and int(w[2]) > 200000 and int(w[4]) > 5000000, out.stdout
+    assert w[8] == "0" and w[10] == "0" and w[12] == "0", out.stdout
+
+
 CAM_SCENES = dict(GRID_SCENES)
 CAM_SCENES.update({
     # the camera inside a mirror sphere that holds the other spheres
