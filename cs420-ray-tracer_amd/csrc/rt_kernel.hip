@@ -1778,6 +1778,9 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
         (rc = grow(c, c->d_cg_npairs, c->cg_npairs_cap, (size_t)ngrid * kCgCntStride * sizeof(unsigned))) != RT_OK)
       return rc;
     const long long nblocks = 6LL * tab->NB * tab->NB;
+    // pass 2 counts 4 work items per (disk, block) pair in 32 bits: no grid past that
+    if (4 * (unsigned long long)ngrid * 2 * (unsigned long long)c->nsph * (unsigned long long)nblocks >= (1ull << 32))
+      return RT_OK;
     if ((rc = grow(c, c->d_cg_disks, c->cg_disks_cap, 2 * (size_t)c->nsph * ngrid * sizeof(CgDisk))) != RT_OK ||
         (rc = grow(c, c->d_cg_pairs, c->cg_pairs_cap, 2 * (size_t)c->nsph * ngrid * nblocks * sizeof(int2))) != RT_OK)
       return rc;
