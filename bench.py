@@ -639,8 +639,11 @@ def main():
         fp64_pf = pmc_rec.get("fp64_flops_per_frame") if pmc_ok else None
         if fp64_pf is not None:
             achieved, flops_source = fp64_pf / k_s / 1e12, "pmc"
-        else:  # no current PMC record: the exact/cull tests the device counters saw
-            achieved, flops_source = test_tflops, "device work counters (exact + cull tests)"
+        else:
+            # no PMC record taken on these kernel sources: no hardware fraction is
+            # claimed (the device's exact/cull test counters undercount the executed
+            # work -- walks, shading, normalisation -- and stay under `executed`)
+            achieved, flops_source = None, "none: no PMC record matches the kernel sources"
         traffic = None
         if pmc_ok and "fetch_bytes" in pmc_rec and "write_bytes" in pmc_rec:
             # FETCH_SIZE x 2: MI355X_MICROARCH.md's gfx950 correction; per launch of `batch` frames
@@ -698,15 +701,22 @@ def main():
             # in-stream kernel time per frame: a hardware fraction of the fp64
             # VALU peak.  One launch renders `batch` frames; rates per launch =
             # per frame.  SURVEY 8(d)'s brute-force count is algorithmic_equivalent.
-            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 4),
+            "roofline": {"bound": "valu",
+                         "achieved": round(achieved, 3) if achieved is not None else None,
+                         "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 4) if achieved is not None else None,
                          "traffic": traffic,
                          "kernel": "rtk::render_kernel + rtk::render_deferred (fp64 VALU; no dense contraction, "
                                    "so no MFMA roof)",
                          "flops_source": flops_source,
                          "fp64_flops_per_frame": fp64_pf,
                          "fp64_flops_per_launch": fp64_pf * batch if fp64_pf is not None else None,
-                         "per_unit": "executed fp64 FLOPs per frame (PMC) x frames per launch",
+                         "per_unit": ("fp64 FLOPs the render kernels executed per frame: rocprofv3 PMC "
+                                      "64 x (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions, "
+                                      "profiles/pmc_traffic.json on these kernel sources; x frames per launch"
+                                      if fp64_pf is not None else
+                                      "none counted: no PMC record on these kernel sources (achieved / frac null; "
+                                      "the device's exact + cull test counts are under executed.test_tflops)"),
                          "valu_busy": pmc_rec.get("valu_busy") if pmc_ok else None,
                          "fp64_share_of_valu_insts": pmc_rec.get("fp64_share_of_valu_insts") if pmc_ok else None,
                          "valu_lane_utilization": pmc_rec.get("valu_lane_utilization") if pmc_ok else None,
@@ -724,7 +734,11 @@ def main():
                              "flops_per_frame": FLOP_PER_TEST * m["spheres"] * m["rank_rays"],
                              "flops_per_launch": FLOP_PER_TEST * m["spheres"] * m["rank_rays"] * batch},
                          "executed": {"exact_tests": m["tests_exact"], "cull_tests": m["tests_cull"],
+                                      # a lower bound of the executed fp64 work: 25 FLOP per exact test
+                                      # + 34 per cull test (device counters), nothing for walks / shading
                                       "test_tflops": round(test_tflops, 3),
+                                      "test_tflops_what": f"lower bound: ({FLOP_PER_TEST} x exact + "
+                                                          f"{FLOP_PER_CULL} x cull tests) per frame / kernel time",
                                       "frac_of_brute_force_tests": round(
                                           m["tests_exact"] / max(1, m["spheres"] * m["rank_rays"]), 6)},
                          "culling": m["cull"],

@@ -61,6 +61,7 @@ enum CkSite {
   kCkLdsQueue,    // merge_tiles' LDS ray-queue slot
   kCkPixbuf,      // merge_tiles' LDS finished-pixel slot
   kCkOut,         // framebuffer byte offset of a tile row or deferred pixel
+  kCkCgBuild,     // camera-grid build: disk, (disk, block) pair, cell count and list slot
   kCkSites
 };
 #ifdef RT_CHECK
@@ -1667,12 +1668,14 @@ __device__ __forceinline__ int cam_closest(const SphGeo *__restrict__ g, int n, 
     }
   }
   int k = 0;
-  int2 e = (len > 0 && !all) ? cg.ent[cb] : make_int2(0, (int)0xff800000u);  // -inf
+  int2 e = (len > 0 && !all) ? cg.ent[RT_CK(kCkCgEnt, cb, (long long)cg.ngrid * cells * kCgSlots)]
+                              : make_int2(0, (int)0xff800000u);  // -inf
   while (k < len) {
     const int i = all ? k : RT_CK(kCkSphere, e.x, n);
     if ((double)__int_as_float(e.y) > bt) break;
     ++k;
-    if (k < len && !all) e = cg.ent[cb + (unsigned)k];  // the next entry, loaded during this test
+    if (k < len && !all)  // the next entry, loaded during this test
+      e = cg.ent[RT_CK(kCkCgEnt, cb + (unsigned)k, (long long)cg.ngrid * cells * kCgSlots)];
     work.exact += 1;
     closest_test(g[i], i, o, d, a4, a2, fast, bt, bn, bi);
   }

@@ -1289,7 +1289,7 @@ __global__ __launch_bounds__(256) void cg_disk_kernel(const CgBuild a) {
   for (int side = 0; side < (v.global ? 1 : 2); ++side) {
     const CgDisk k = cg_side(v, side, s);
     const int di = 2 * t + side;
-    if (lane == 0) a.disks[di] = k;
+    if (lane == 0) a.disks[RT_CK(kCkCgBuild, di, 2LL * a.n * a.ngrid)] = k;
     for (int b0 = 0; b0 < nb; b0 += 64) {
       const int b = b0 + lane;
       const bool m = b < nb && cg_block(k, a.faces, a.blocks, a.NB, b);
@@ -1298,7 +1298,10 @@ __global__ __launch_bounds__(256) void cg_disk_kernel(const CgBuild a) {
       unsigned q0 = 0;
       if (lane == 0) q0 = atomicAdd(&a.npairs[grid * kCgCntStride], (unsigned)__builtin_popcountll(bm));
       q0 = (unsigned)__builtin_amdgcn_readfirstlane((int)q0);
-      if (m) a.pairs[(size_t)grid * a.maxp + q0 + (unsigned)__builtin_popcountll(bm & ((1ull << lane) - 1))] =
+      // a grid whose pairs exceed maxp keeps the first maxp; cg_sort_kernel
+      // then marks all its cells overflowed (its rays sweep)
+      const unsigned qi = q0 + (unsigned)__builtin_popcountll(bm & ((1ull << lane) - 1));
+      if (m && qi < (unsigned)a.maxp) a.pairs[RT_CK(kCkCgBuild, (size_t)grid * a.maxp + qi, (long long)a.ngrid * a.maxp)] =
           make_int2(di, b);
     }
   }
@@ -1312,7 +1315,8 @@ __global__ __launch_bounds__(256) void cg_disk_kernel(const CgBuild a) {
 __global__ __launch_bounds__(64) void cg_bin_kernel(const CgBuild a) {
   const int lane = (int)(threadIdx.x & 63);
   const long long cells = 6LL * a.N * a.N;
-  unsigned incl = lane < a.ngrid ? 4u * a.npairs[lane * kCgCntStride] : 0u;  // work items per grid, then prefix
+  // work items per grid (4 per stored pair; the host keeps 4 ngrid maxp < 2^32), then their prefix
+  unsigned incl = lane < a.ngrid ? 4u * min(a.npairs[lane * kCgCntStride], (unsigned)a.maxp) : 0u;
   for (int off = 1; off < 64; off <<= 1) {
     const unsigned v = __shfl_up(incl, off, 64);
     if (lane >= off) incl += v;
@@ -1321,8 +1325,8 @@ __global__ __launch_bounds__(64) void cg_bin_kernel(const CgBuild a) {
   for (unsigned v = blockIdx.x; v < total; v += gridDim.x) {
     const int grid = __builtin_popcountll(__ballot(incl <= v));
     const unsigned item = v - (grid ? __shfl(incl, grid - 1, 64) : 0u);
-    const int2 pr = a.pairs[(size_t)grid * a.maxp + (item >> 2)];
-    const CgDisk k = a.disks[pr.x];
+    const int2 pr = a.pairs[RT_CK(kCkCgBuild, (size_t)grid * a.maxp + (item >> 2), (long long)a.ngrid * a.maxp)];
+    const CgDisk k = a.disks[RT_CK(kCkCgBuild, pr.x, 2LL * a.n * a.ngrid)];
     const bool wide = cg_wide(k);
     const int bb = pr.y;
     const int f = bb / (a.NB * a.NB), bj = (bb / a.NB) % a.NB, bi = bb % a.NB;
@@ -1342,11 +1346,14 @@ __global__ __launch_bounds__(64) void cg_bin_kernel(const CgBuild a) {
       }
       int slots[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) slots[u] = gcs[u] >= 0 ? atomicAdd(&a.count[(long long)grid * cells + gcs[u]], 1) : a.K;
+      for (int u = 0; u < 4; ++u)
+        slots[u] = gcs[u] >= 0 ? atomicAdd(&a.count[RT_CK(kCkCgBuild, (long long)grid * cells + gcs[u], a.ngrid * cells)], 1)
+                               : a.K;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (slots[u] < a.K)
-          a.ent[((long long)grid * cells + gcs[u]) * a.K + slots[u]] = make_int2(k.s, __float_as_int(k.tlo));
+          a.ent[RT_CK(kCkCgBuild, ((long long)grid * cells + gcs[u]) * a.K + slots[u], a.ngrid * cells * a.K)] =
+              make_int2(k.s, __float_as_int(k.tlo));
     }
   }
 }
@@ -1357,6 +1364,10 @@ __global__ __launch_bounds__(256) void cg_sort_kernel(const CgBuild a) {
   const long long cells = 6LL * a.N * a.N;
   const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gc >= cells * a.ngrid) return;
+  if (a.npairs[(gc / cells) * kCgCntStride] > (unsigned)a.maxp) {  // pass 1 dropped pairs: the grid is incomplete
+    a.count[gc] = a.K + 1;                                           // every cell overflowed, its rays sweep
+    return;
+  }
   const int cnt = a.count[gc];
   if (cnt > a.K) return;
   int2 *e = a.ent + gc * a.K;
@@ -1409,6 +1420,8 @@ struct rt_ctx {
   // positions and the scene stay the same
   int cg_mode = 1;    // RT_HIP_CAM_GRID: 0 off, 1 auto (a one-frame launch at a new position sweeps), 2 every launch
   int cg_n_opt = 0;   // RT_HIP_CAM_GRID_N (tuning build); 0 = kCgNStatic / kCgNMoving
+  long long cg_budget_opt = -1;  // RT_HIP_CAM_GRID_BUDGET (tuning build): bytes for a launch's grids; -1 = kCgBudgetBytes
+  long long cg_maxp_opt = -1;    // RT_HIP_CAM_GRID_MAXP (tuning build): pairs per grid kept; -1 = the pair budget
   int32_t *d_cg_count = nullptr;
   int2 *d_cg_ent = nullptr;
   CgDisk *d_cg_disks = nullptr;
@@ -1742,12 +1755,50 @@ int grow(rt_ctx *c, T *&p, size_t &cap, size_t bytes) {
   return RT_OK;
 }
 
-// The camera grids of this launch (cg.on = 0: the launch sweeps as before):
-// one grid when every frame shares the camera position, else one per frame,
-// enqueued on the context's stream ahead of the render kernel; kept while
-// the positions and the scene stay the same.
-int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
-  out = CgArgs{};
+// grow-only device buffer that may fail softly: false (error cleared, buffer
+// freed) when the memory is not there -- for optional structures
+template <class T>
+bool grow_soft(rt_ctx *c, T *&p, size_t &cap, size_t bytes) {
+  if (cap >= bytes) return true;
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return false;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  if (hipMalloc(&p, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    p = nullptr;
+    return false;
+  }
+  cap = bytes;
+  return true;
+}
+
+// Camera-grid memory: the (disk, block) pair lists of one launch's grids take
+// at most kCgPairBytes (a grid with more pairs is marked overflowed on the
+// device and its rays sweep), and all of a launch's grid buffers at most
+// kCgBudgetBytes and half the device's free memory -- the grid is a speed-up,
+// so past that (or when an allocation fails) the launch sweeps (RT_OK).
+constexpr size_t kCgPairBytes = size_t(128) << 20;
+constexpr size_t kCgBudgetBytes = size_t(2) << 30;
+
+// What cam_grid_prepare decided for a launch.
+struct CgPlan {
+  bool use = false;    // the launch scans grids
+  bool build = false;  // ... built by cam_grid_enqueue first
+  int N = 0, ngrid = 0, maxp = 0;
+  long long nblocks = 0;
+  std::vector<double> pos;
+  const rt_ctx::CgTables *tab = nullptr;
+};
+
+// The camera grids of this launch (plan.use = false: the launch sweeps as
+// before): one grid when every frame shares the camera position, else one per
+// frame; kept while the positions and the scene stay the same.  The host part
+// -- policy, tables, buffers (which may wait for the stream) -- runs before
+// the launch's start event; cam_grid_enqueue puts the device passes on the
+// stream ahead of the render kernel.
+int cam_grid_prepare(rt_ctx *c, const Cam &cam, int nf, CgPlan &p) {
+  p = CgPlan{};
   if (c->cg_mode == 0 || !c->cull || c->nsph == 0) return RT_OK;
   std::vector<double> pos{cam.px, cam.py, cam.pz};
   bool same = true;
@@ -1768,22 +1819,61 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
   }
   c->cg_seen = pos;
   c->cg_seen_gen = c->scene_gen;
-  if (!cached) {
+  if (cached) {
+    p.use = true;
+    p.N = N;
+    p.ngrid = ngrid;
+    return RT_OK;
+  }
+  // from here the buffers change: the cached grids are gone whatever happens
+  c->cg_gen = ~0ull;
+  const rt_ctx::CgTables *tab = nullptr;
+  int rc = cg_tables(c, N, tab);
+  if (rc != RT_OK) return rc;
+  const long long nblocks = 6LL * tab->NB * tab->NB;
+  // pairs per grid: every (disk, block) pair at most, within the pair budget
+  // (a grid past it is marked overflowed on the device), and 4 work items per
+  // pair of all grids countable in 32 bits (cg_bin_kernel)
+  const unsigned long long worst = 2ull * (unsigned long long)c->nsph * (unsigned long long)nblocks;
+  const unsigned long long cap32 = ((1ull << 32) - 1) / (4ull * (unsigned long long)ngrid);
+  const unsigned long long budget = std::max<unsigned long long>(1, kCgPairBytes / sizeof(int2) / ngrid);
+  int maxp = (int)std::min({worst, cap32, budget, (unsigned long long)INT32_MAX});
+  if (c->cg_maxp_opt >= 0) maxp = (int)std::max<long long>(1, std::min<long long>(maxp, c->cg_maxp_opt));
+  const size_t b_count = ngrid * cells * sizeof(int32_t), b_ent = ngrid * cells * kCgSlots * sizeof(int2),
+               b_np = (size_t)ngrid * kCgCntStride * sizeof(unsigned),
+               b_disks = 2 * (size_t)c->nsph * ngrid * sizeof(CgDisk), b_pairs = (size_t)ngrid * maxp * sizeof(int2);
+  const size_t total = b_count + b_ent + b_np + b_disks + b_pairs;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+    (void)hipGetLastError();
+    free_b = 0;
+  }
+  // what the grids hold now counts as available: growing frees it first
+  const size_t held = c->cg_count_cap + c->cg_ent_cap + c->cg_npairs_cap + c->cg_disks_cap + c->cg_pairs_cap;
+  const size_t limit = c->cg_budget_opt >= 0 ? (size_t)c->cg_budget_opt : kCgBudgetBytes;
+  if (total > limit || total > (free_b + held) / 2) return RT_OK;
+  if (!grow_soft(c, c->d_cg_count, c->cg_count_cap, b_count) || !grow_soft(c, c->d_cg_ent, c->cg_ent_cap, b_ent) ||
+      !grow_soft(c, c->d_cg_npairs, c->cg_npairs_cap, b_np) || !grow_soft(c, c->d_cg_disks, c->cg_disks_cap, b_disks) ||
+      !grow_soft(c, c->d_cg_pairs, c->cg_pairs_cap, b_pairs))
+    return RT_OK;  // no memory for the grid: this launch sweeps
+  p.use = p.build = true;
+  p.N = N;
+  p.ngrid = ngrid;
+  p.maxp = maxp;
+  p.nblocks = nblocks;
+  p.pos = std::move(pos);
+  p.tab = tab;
+  return RT_OK;
+}
+
+int cam_grid_enqueue(rt_ctx *c, const CgPlan &p, CgArgs &out) {
+  out = CgArgs{};
+  if (!p.use) return RT_OK;
+  const size_t cells = 6 * (size_t)p.N * p.N;
+  if (p.build) {
     const auto t0 = std::chrono::steady_clock::now();
-    const rt_ctx::CgTables *tab = nullptr;
-    int rc = cg_tables(c, N, tab);
-    if (rc != RT_OK) return rc;
-    if ((rc = grow(c, c->d_cg_count, c->cg_count_cap, ngrid * cells * sizeof(int32_t))) != RT_OK ||
-        (rc = grow(c, c->d_cg_ent, c->cg_ent_cap, ngrid * cells * kCgSlots * sizeof(int2))) != RT_OK ||
-        (rc = grow(c, c->d_cg_npairs, c->cg_npairs_cap, (size_t)ngrid * kCgCntStride * sizeof(unsigned))) != RT_OK)
-      return rc;
-    const long long nblocks = 6LL * tab->NB * tab->NB;
-    // pass 2 counts 4 work items per (disk, block) pair in 32 bits: no grid past that
-    if (4 * (unsigned long long)ngrid * 2 * (unsigned long long)c->nsph * (unsigned long long)nblocks >= (1ull << 32))
-      return RT_OK;
-    if ((rc = grow(c, c->d_cg_disks, c->cg_disks_cap, 2 * (size_t)c->nsph * ngrid * sizeof(CgDisk))) != RT_OK ||
-        (rc = grow(c, c->d_cg_pairs, c->cg_pairs_cap, 2 * (size_t)c->nsph * ngrid * nblocks * sizeof(int2))) != RT_OK)
-      return rc;
+    const rt_ctx::CgTables *tab = p.tab;
+    const int ngrid = p.ngrid;
     CgBuild b{};
     b.geo = c->d_geo;
     b.rad = c->d_rad;
@@ -1796,20 +1886,20 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
     b.disks = c->d_cg_disks;
     b.pairs = c->d_cg_pairs;
     b.npairs = c->d_cg_npairs;
-    b.maxp = (int)(2 * c->nsph * nblocks);
+    b.maxp = p.maxp;
     b.n = c->nsph;
-    b.N = N;
+    b.N = p.N;
     b.NT = tab->NT;
     b.NB = tab->NB;
     b.K = kCgSlots;
     b.ngrid = ngrid;
     for (int g = 0; g < ngrid; g++) {
-      b.px[g] = pos[3 * g];
-      b.py[g] = pos[3 * g + 1];
-      b.pz[g] = pos[3 * g + 2];
+      b.px[g] = p.pos[3 * g];
+      b.py[g] = p.pos[3 * g + 1];
+      b.pz[g] = p.pos[3 * g + 2];
       double d2 = 0.0;  // the scene's extent with the point (the grown radius' margin)
       for (int k = 0; k < 3; k++) {
-        const double l = std::min(c->lo[k], pos[3 * g + k]), h = std::max(c->hi[k], pos[3 * g + k]);
+        const double l = std::min(c->lo[k], p.pos[3 * g + k]), h = std::max(c->hi[k], p.pos[3 * g + k]);
         d2 += (h - l) * (h - l);
       }
       b.diam[g] = std::sqrt(d2);
@@ -1818,18 +1908,19 @@ int cam_grid(rt_ctx *c, const Cam &cam, int nf, CgArgs &out) {
     RT_TRY(c, hipMemsetAsync(c->d_cg_npairs, 0, ngrid * kCgCntStride * sizeof(unsigned), c->stream));
     const int nthr = c->nsph * ngrid;
     hipLaunchKernelGGL(cg_disk_kernel, dim3((unsigned)((nthr + 3) / 4)), dim3(256), 0, c->stream, b);
-    hipLaunchKernelGGL(cg_bin_kernel, dim3((unsigned)std::min<long long>(8192, 8LL * nthr * nblocks)), dim3(64), 0,
+    hipLaunchKernelGGL(cg_bin_kernel, dim3((unsigned)std::min<long long>(8192, 8LL * nthr * p.nblocks)), dim3(64), 0,
                        c->stream, b);
     hipLaunchKernelGGL(cg_sort_kernel, dim3((unsigned)((ngrid * cells + 255) / 256)), dim3(256), 0, c->stream, b);
     RT_TRY(c, hipGetLastError());
+    // the grids are valid for later launches only once their passes are on the stream
     c->cg_gen = c->scene_gen;
-    c->cg_n = N;
+    c->cg_n = p.N;
     c->cg_ngrid = ngrid;
-    c->cg_pos = pos;
+    c->cg_pos = p.pos;
     c->cg_builds++;
     c->cg_build_ms += ms_since(t0);
   }
-  out = CgArgs{c->d_cg_count, c->d_cg_ent, N, 1, ngrid > 1 ? 1 : 0, ngrid};
+  out = CgArgs{c->d_cg_count, c->d_cg_ent, p.N, 1, p.ngrid > 1 ? 1 : 0, p.ngrid};
   return RT_OK;
 }
 
@@ -2117,11 +2208,17 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     // the default configuration (ordered 4-wide BVH walk, light grids) has kernels
     // compiled with only those paths (kFast): no registers held for the others
     const bool fast = bv.ordered && bv.wide && lg.on;
-    // the launch's timing starts here: the camera grids are built on the
-    // device ahead of the render kernel, part of the launch
-    RT_TRY(c, mark_start(c));
+    // the camera grids' host part (policy, tables, buffers) first; the
+    // launch's timing starts after it: the grids' device passes ahead of the
+    // render kernel are part of the launch
+    CgPlan plan;
     if (fast && kCull) {
-      const int rc = cam_grid(c, cam, nf, ra.cg);
+      const int rc = cam_grid_prepare(c, cam, nf, plan);
+      if (rc != RT_OK) return rc;
+    }
+    RT_TRY(c, mark_start(c));
+    {
+      const int rc = cam_grid_enqueue(c, plan, ra.cg);
       if (rc != RT_OK) return rc;
     }
     if (fast && kCull && c->sg_ok)
@@ -2281,6 +2378,8 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(8, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_CAM_GRID_N")) c->cg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_CAM_GRID_BUDGET")) c->cg_budget_opt = std::max(0LL, std::atoll(e));
+  if (const char *e = std::getenv("RT_HIP_CAM_GRID_MAXP")) c->cg_maxp_opt = std::max(1LL, std::atoll(e));
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID")) c->sg_mode = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SPHERE_GRID_N")) c->sg_n_opt = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_BEHIND_GRID")) c->ug_mode = std::max(-1, std::min(1, std::atoi(e)));
@@ -2654,7 +2753,7 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
         "camera/sphere-grid list slot", "sphere-grid start", "sphere-grid key", "uniform-grid cell",
         "uniform-grid overflow slot", "BVH node reference", "BVH leaf slot", "tile order slot / tile id",
         "deferred-queue slot", "reflection-stack slot", "LDS ray-queue slot", "LDS pixel slot",
-        "framebuffer offset"};
+        "framebuffer offset", "camera-grid build slot"};
     CheckRec rec{};
     RT_TRY(c, hipMemcpyFromSymbol(&rec, HIP_SYMBOL(g_check), sizeof rec));
     if (rec.count) {

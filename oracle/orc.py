@@ -65,6 +65,8 @@ def lib():
         L.orc_intersect.argtypes = [C.POINTER(orc_sphere), orc_vec3, orc_vec3, C.POINTER(C.c_double)]
         L.orc_render.argtypes = [C.POINTER(orc_scene), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.c_void_p, C.c_void_p, C.POINTER(orc_counts), C.c_int]
+        L.orc_render_cam.argtypes = [C.POINTER(orc_scene), C.POINTER(orc_camera), C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(orc_counts), C.c_int]
         L.orc_render_aa.argtypes = [C.POINTER(orc_scene), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                     C.c_void_p, C.POINTER(orc_counts), C.c_int]
         L.orc_quantize.argtypes = [C.c_double]
@@ -97,15 +99,27 @@ class OracleScene:
         lib().orc_make_camera(C.byref(self.s), C.byref(c))
         return c
 
-    def render(self, W, H, depth, band=1, first=0, stride=1, count=None, threads=1, want_fb=False):
-        """Returns (rgb bytes, counts dict, seconds[, fb doubles])."""
+    def render(self, W, H, depth, band=1, first=0, stride=1, count=None, threads=1, want_fb=False, camera=None):
+        """Returns (rgb bytes, counts dict, seconds[, fb doubles]).  `camera`: any
+        object with position/forward/right/up (3 doubles) and scale (an
+        rt_hip.rt_camera), else the scene's camera."""
         count = H if count is None else count
         rgb = (C.c_uint8 * (count * W * 3))()
         fb = (C.c_double * (count * W * 3))() if want_fb else None
         cnt = orc_counts()
         t0 = time.perf_counter()
-        rc = lib().orc_render(C.byref(self.s), W, H, depth, band, first, stride, count, C.cast(rgb, C.c_void_p),
-                              C.cast(fb, C.c_void_p) if fb is not None else None, C.byref(cnt), threads)
+        cam = None
+        if isinstance(camera, orc_camera):
+            cam = camera
+        elif camera is not None:
+            cam = orc_camera()
+            for f in ("position", "forward", "right", "up"):
+                v = getattr(camera, f)
+                getattr(cam, f).x, getattr(cam, f).y, getattr(cam, f).z = v[0], v[1], v[2]
+            cam.scale = camera.scale
+        rc = lib().orc_render_cam(C.byref(self.s), C.byref(cam) if cam is not None else None, W, H, depth, band,
+                                  first, stride, count, C.cast(rgb, C.c_void_p),
+                                  C.cast(fb, C.c_void_p) if fb is not None else None, C.byref(cnt), threads)
         dt = time.perf_counter() - t0
         if rc != 0:
             raise ValueError("orc_render rejected its arguments")

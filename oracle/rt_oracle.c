@@ -196,11 +196,17 @@ int orc_quantize(double c) {
     return (int)m;
 }
 
-int orc_render(const orc_scene *s, int W, int H, int depth, int band, int first, int stride, int row_count,
-               uint8_t *rgb, double *fb, orc_counts *counts, int nthreads) {
+/* The pixel loop (main.cpp:146-157) over the rows of one shard; `camp` is an
+ * explicit camera basis (a moved view, as a caller builds with Camera
+ * directly), NULL for the scene's (main.cpp:132). */
+int orc_render_cam(const orc_scene *s, const orc_camera *camp, int W, int H, int depth, int band, int first,
+                   int stride, int row_count, uint8_t *rgb, double *fb, orc_counts *counts, int nthreads) {
     if (W <= 0 || H <= 0 || band <= 0 || stride <= 0 || first < 0 || row_count < 0) return -1;
     orc_camera cam;
-    orc_make_camera(s, &cam);
+    if (camp)
+        cam = *camp;
+    else
+        orc_make_camera(s, &cam);
     orc_counts total = {0, 0, 0, 0};
     long long npx = (long long)row_count * W;
     if (nthreads < 1) nthreads = 1;
@@ -242,6 +248,11 @@ int orc_render(const orc_scene *s, int W, int H, int depth, int band, int first,
     }
     if (counts) *counts = total;
     return 0;
+}
+
+int orc_render(const orc_scene *s, int W, int H, int depth, int band, int first, int stride, int row_count,
+               uint8_t *rgb, double *fb, orc_counts *counts, int nthreads) {
+    return orc_render_cam(s, NULL, W, H, depth, band, first, stride, row_count, rgb, fb, counts, nthreads);
 }
 
 /* The reference GPU's antialias mode (src/main_gpu.cu:249-333) restated in the

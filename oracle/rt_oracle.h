@@ -91,6 +91,9 @@ int orc_intersect(const orc_sphere *s, orc_vec3 ro, orc_vec3 rd, double *t);
 int orc_render(const orc_scene *s, int W, int H, int depth,
                int band, int first, int stride, int row_count,
                uint8_t *rgb, double *fb, orc_counts *counts, int nthreads);
+/* The same with an explicit camera basis (NULL: the scene's camera). */
+int orc_render_cam(const orc_scene *s, const orc_camera *cam, int W, int H, int depth, int band, int first,
+                   int stride, int row_count, uint8_t *rgb, double *fb, orc_counts *counts, int nthreads);
 
 /* Antialias mode of src/main_gpu.cu:249-333 in serial fp64 semantics: samples
  * = 1 or 4, full frame in PPM row order (see rt_oracle.c). */

@@ -9,6 +9,7 @@ SRC="$ROOT/gpurun_out/prof_$TAG"
 DST="$ROOT/profiles/$TAG"
 mkdir -p "$DST"
 cp "$SRC/bench.json" "$DST/"
+[ -f "$SRC/kernel_src_sha.txt" ] && cp "$SRC/kernel_src_sha.txt" "$DST/"
 cp "$SRC"/trace/run_kernel_stats.csv "$DST/kernel_stats.csv"
 python3 "$ROOT/scripts/prof_summary.py" "$SRC/trace/run_kernel_trace.csv" --labels synth200 > "$DST/trace_summary.json"
 cp "$SRC/trace_bench.json" "$DST/trace_bench.json"

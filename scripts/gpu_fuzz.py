@@ -7,7 +7,9 @@ the C-ABI at small sizes and random depths, against the oracle byte for byte
 and ray count for ray count; every third scene is also rendered as three
 frames of one launch (rt_render_frames_async: the deferred kernel and, for
 scenes with the uniform grid, the XCD frame mapping), each frame against the
-same oracle image.  Knobs (RT_HIP_*) apply as set in the environment, e.g.
+same oracle image, and as three frames from three camera positions (a
+device-built camera grid per frame when the launch builds grids), each
+against the oracle at its camera.  Knobs (RT_HIP_*) apply as set in the environment, e.g.
 RT_HIP_BEHIND_GRID=1 RT_HIP_BVH_ALWAYS=1 puts every scene on the uniform
 grid.  Prints one line per scene and a summary; exits non-zero on the first
 mismatch.
@@ -58,7 +60,7 @@ def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 300.0
     rng = random.Random(int(sys.argv[2]) if len(sys.argv) > 2 else 20261016)
     r = rt_hip.Renderer(0)
-    t0, k, px, frames = time.time(), 0, 0, 0
+    t0, k, px, frames, moving = time.time(), 0, 0, 0, 0
     try:
         while time.time() - t0 < budget:
             text = scene(rng)
@@ -78,6 +80,26 @@ def main():
                 host = bytes(buf.cpu().numpy())
                 ok = all(host[f * stride:(f + 1) * stride] == ref for f in range(F))
                 frames += F
+                if ok:  # three frames from three camera positions: a device camera grid per frame
+                    cams = []
+                    for f in range(F):
+                        c = rt_hip.rt_camera.from_buffer_copy(sc.camera())
+                        for a in range(3):
+                            c.position[a] += rng.uniform(-1.0, 1.0) * rng.choice([1e-3, 0.1, 1.0])
+                        cams.append(c)
+                    buf.fill_(77)
+                    torch.cuda.synchronize()
+                    r.render_frames_async(cams, W, H, D, None, buf.data_ptr(), stride)
+                    st3 = r.stats()
+                    host = bytes(buf.cpu().numpy())
+                    oref = orc.OracleScene(text=text)
+                    tot = [0, 0, 0]
+                    for f in range(F):
+                        want, c3, _ = oref.render(W, H, D, threads=16, camera=cams[f])
+                        ok = ok and host[f * stride:(f + 1) * stride] == want
+                        tot = [tot[0] + c3["primary"], tot[1] + c3["shadow"], tot[2] + c3["reflect"]]
+                    ok = ok and [st3.rays_primary, st3.rays_shadow, st3.rays_reflect] == tot
+                    moving += F
             k += 1
             px += W * H
             if not ok:
@@ -91,8 +113,8 @@ def main():
                 print("%d scenes ok (%d pixels), %.0f s" % (k, px, time.time() - t0), flush=True)
     finally:
         r.close()
-    print("fuzz: %d scenes, %d pixels (+ %d frames of 3-frame launches), all byte-identical to the oracle"
-          % (k, px, frames))
+    print("fuzz: %d scenes, %d pixels (+ %d frames of 3-frame launches at one position, %d frames of 3-frame "
+          "launches at three positions), all byte-identical to the oracle" % (k, px, frames, moving))
     return 0
 
 

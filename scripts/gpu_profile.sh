@@ -9,6 +9,8 @@ TAG="${TAG:-r2}"
 OUT="$ROOT/gpurun_out/prof_$TAG"
 WORKLOADS="${WORKLOADS:-synth200_1920x1080_d4 complex_1920x1080_d4 complex_3840x2160_d4 synth10k_3840x2160_d6}"
 mkdir -p "$OUT"
+# the kernel sources these runs measure (make_pmc_json.py records it with the PMC)
+python3 -c "import sys; sys.path.insert(0, '$ROOT'); import bench; print(bench.kernel_source_sha())" > "$OUT/kernel_src_sha.txt"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail -5 "$OUT/bench.err"; exit 1; }

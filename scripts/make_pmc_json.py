@@ -83,7 +83,11 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench  # noqa: E402  (the source hash bench.py checks)
 
-    out["kernel_src_sha"] = bench.kernel_source_sha()
+    # the hash of the kernel sources the passes ran on: gpu_profile.sh records it
+    # beside them (kernel_src_sha.txt); else the tree this runs in
+    rec = [os.path.join(base, q, "kernel_src_sha.txt") for q in (".", "..", "../..")]
+    rec = [q for q in rec if os.path.exists(q)]
+    out["kernel_src_sha"] = open(rec[0]).read().strip() if rec else bench.kernel_source_sha()
     out["source"] = os.path.relpath(base, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     out["counters"] = {k: round(v, 1) for k, v in sorted(vals.items())}
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")

@@ -59,6 +59,43 @@ def test_checked_multi_frame_launch(check_renderer, name, F):
         assert host[f].tobytes() == want, f"frame {f}: {diff_summary(host[f].tobytes(), want)}"
 
 
+@pytest.mark.parametrize("name,F", [("synth200_1920x1080_d4", 32), ("complex_97x61_d4", 5)])
+def test_checked_moving_camera_launch(check_renderer, name, F):
+    """A moving camera in the checked build: F camera positions in one launch,
+    so the device builds a camera grid per frame (cg_disk / cg_bin / cg_sort,
+    their pair, count and slot indices checked) and every frame's scan reads
+    its own grid; each frame equals the oracle at its camera (every 24th row
+    at 1080p)."""
+    import orc
+    import rt_hip
+    import torch
+
+    m = manifest()[name]
+    W, H, D = m["width"], m["height"], m["depth"]
+    sc = rt_hip.Scene.load(scene_path(m["scene"]))
+    check_renderer.upload(sc)
+    cams = []
+    for f in range(F):
+        c = rt_hip.rt_camera.from_buffer_copy(sc.camera())
+        c.position[0] += 0.05 * (f + 1)
+        c.position[2] -= 0.03 * f
+        cams.append(c)
+    buf = torch.empty((F, H, W, 3), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    check_renderer.render_frames_async(cams, W, H, D, None, buf.data_ptr(), H * W * 3)
+    check_renderer.stats()  # raises on RT_ERR_CHECK
+    assert check_renderer.info().cam_grid_last == 1
+    host = buf.cpu().numpy()
+    ref = orc.OracleScene(scene_path(m["scene"]))
+    step = 24 if H > 200 else 1
+    count = (H + step - 1) // step
+    for f in (0, F // 2, F - 1):
+        rgb, _, _ = ref.render(W, H, D, stride=step, count=count, threads=16, camera=cams[f])
+        want = np.frombuffer(rgb, np.uint8).reshape(count, W, 3)
+        for i in range(count):
+            assert host[f][i * step].tobytes() == want[i].tobytes(), f"frame {f} row {i * step}"
+
+
 def test_checked_deferred_queue_overflow(monkeypatch):
     """A camera inside a cloud of mirrors (test_gpu_parity._mirror_cloud):
     level-2 rays overflow the deferred queue; every 31st row vs the oracle."""

@@ -237,3 +237,76 @@ def test_camera_grid_per_frame_device_grids(gpu_renderer, F):
         assert frames[f].tobytes() == want, f"frame {f}: {diff_summary(frames[f].tobytes(), want)}"
         total = [total[0] + s1.rays_primary, total[1] + s1.rays_shadow, total[2] + s1.rays_reflect]
     assert [st.rays_primary, st.rays_shadow, st.rays_reflect] == total
+
+
+@pytest.mark.parametrize("step", [1e-3, 0.21])
+def test_camera_grid_moving_bench_shape_vs_oracle(gpu_renderer, step):
+    """The bench's moving_camera shape pinned to the oracle: synth200 1920x1080
+    d4 as ONE 32-frame launch of 32 distinct camera positions (the scene's
+    basis, the position moved `step` further along x per frame, as bench.py's
+    moved(); step 1e-3 is bench.py's own sequence), so 32 camera grids of N =
+    128 are built on the device in the launch (camera.h:17-25 rays from each
+    position, scene.h:41-61 closest hits).  Every 16th row of frames 0, 7, 19
+    and 31 equals the oracle's render at that camera, and the launch's ray
+    counts equal the oracle's full-frame counts summed over the 32 frames."""
+    import orc
+    import rt_hip
+
+    name = "synth200_1920x1080_d4"
+    sc, m = _load(gpu_renderer, name)
+    W, H, D = m["width"], m["height"], m["depth"]
+    F = rt_hip.MAX_FRAMES
+    base = sc.camera()
+    cams = []
+    for f in range(F):
+        c = rt_hip.rt_camera.from_buffer_copy(base)
+        c.position[0] = base.position[0] + step * (f + 1)
+        cams.append(c)
+    frames, st, _ = _frames(gpu_renderer, cams, W, H, D)
+    info = gpu_renderer.info()
+    assert info.cam_grid_last == 1 and info.cam_grid_n == 128, (info.cam_grid_last, info.cam_grid_n)
+    ref = orc.OracleScene(scene_path("synth200"))
+    first, stride = 0, 16
+    count = (H - first + stride - 1) // stride
+    for f in (0, 7, 19, 31):
+        rgb, _, _ = ref.render(W, H, D, band=1, first=first, stride=stride, count=count, threads=16, camera=cams[f])
+        want = np.frombuffer(rgb, np.uint8).reshape(count, W, 3)
+        for i in range(count):
+            y = first + i * stride
+            assert frames[f][y].tobytes() == want[i].tobytes(), \
+                f"frame {f} row {y}: {diff_summary(frames[f][y].tobytes(), want[i].tobytes())}"
+    total = [0, 0, 0]
+    for f in range(F):
+        _, cnt, _ = ref.render(W, H, D, threads=16, camera=cams[f])
+        total = [total[0] + cnt["primary"], total[1] + cnt["shadow"], total[2] + cnt["reflect"]]
+    assert [st.rays_primary, st.rays_shadow, st.rays_reflect] == total
+
+
+@pytest.mark.parametrize("env", [{"RT_HIP_CAM_GRID_BUDGET": "0"}, {"RT_HIP_CAM_GRID_MAXP": "3"}],
+                         ids=["no_budget", "pairs_dropped"])
+def test_camera_grid_fallbacks(monkeypatch, env):
+    """The camera grid is only a speed-up: with no memory budget for it the
+    launch sweeps (no grid), and a grid whose (disk, block) pair list is cut
+    short on the device is marked overflowed cell by cell (its rays sweep) --
+    for a static view and a moving camera both, every frame equals the
+    reference's image / its own one-frame render."""
+    import rt_hip
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    r = rt_hip.Renderer(0, variant="tuning")
+    try:
+        name = "complex_97x61_d4"
+        sc, m = _load(r, name)
+        W, H, D = m["width"], m["height"], m["depth"]
+        frames, _, _ = _frames(r, [sc.camera()] * 4, W, H, D)
+        assert r.info().cam_grid_last == (0 if "RT_HIP_CAM_GRID_BUDGET" in env else 1)
+        for f in range(4):
+            assert frames[f].tobytes() == golden_rgb(name), f
+        cams = [_moved(sc.camera(), 0.25 * k - 1) for k in range(5)]
+        frames, _, _ = _frames(r, cams, W, H, D)
+        for f, cam in enumerate(cams):
+            want, _ = _single(r, cam, W, H, D)
+            assert frames[f].tobytes() == want, f"frame {f}: {diff_summary(frames[f].tobytes(), want)}"
+    finally:
+        r.close()
