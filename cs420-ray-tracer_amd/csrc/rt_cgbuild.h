@@ -44,16 +44,19 @@ RT_HD inline bool cg_meets(const CgDisk &k, const CubePatch &p) { return cg_meet
 // A sphere (centre c, |radius| r) seen from P: its direction v = c - P,
 // distance D and the light grids' grown radius R; `global` -- P inside (or
 // nearly inside) it, or non-finite data -- makes it one disk of every
-// direction (alpha >= pi meets every patch) with tlo = -inf.
+// direction (alpha >= pi meets every patch) with tlo = -inf.  rho > 0: seen
+// from anywhere in the ball B(P, rho) (the sphere grids, build_sphere_grids:
+// R grows by rho, the Minkowski sum).
 struct CgView {
   double vx, vy, vz, D, R, alpha, ca, sa;
   bool global;
 };
-RT_HD inline CgView cg_view(double cx, double cy, double cz, double r, double px, double py, double pz, double diam) {
+RT_HD inline CgView cg_view(double cx, double cy, double cz, double r, double px, double py, double pz, double diam,
+                            double rho = 0.0) {
   CgView v;
   v.vx = cx - px, v.vy = cy - py, v.vz = cz - pz;
   v.D = __builtin_sqrt(v.vx * v.vx + v.vy * v.vy + v.vz * v.vz);
-  v.R = r * (1.0 + 1e-6) + 1e-6 * (v.D + diam);
+  v.R = r * (1.0 + 1e-6) + 1e-6 * (v.D + diam) + rho;
   v.global = !__builtin_isfinite(v.D) || !__builtin_isfinite(v.R) || !(v.D > v.R);
   v.alpha = v.global ? 4.0 : asin(v.R / v.D) + kLgSlack;
   v.ca = cos(v.alpha);

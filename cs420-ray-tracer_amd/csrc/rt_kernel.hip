@@ -1383,6 +1383,204 @@ __global__ __launch_bounds__(256) void cg_sort_kernel(const CgBuild a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The sphere grids (build_sphere_grids, rt_lightgrid.cpp) built on the device
+// at upload: one cube-map grid per reflective sphere s, seen from the ball
+// B(C_s, rho_s) that holds the origins of the reflection rays leaving s
+// (main.cpp:46), with the camera grid's per-lane disk / block / tile / cell
+// tests (rt_cgbuild.h, cg_view with rho) and the host builder's CSR layout:
+// grid s's cell c is ent[start[s (6N^2 + 1) + c] .. start[... + c + 1]),
+// entries (sphere, tlo bits) ascending by (tlo, index).  Grids go through in
+// batches (their disks and pair lists are scratch); passes:
+//   sg_disk_kernel   a wave per (grid, sphere): its disks and (disk, block) pairs
+//                    (pairs past maxp and global spheres counted per grid; the
+//                    host refuses a grid with more than kSgMaxGlobal globals or
+//                    dropped pairs, as build_sphere_grids refuses it)
+//   sg_bin_kernel    a wave per quarter pair, as cg_bin_kernel: <count> adds
+//                    1 per listed cell, <fill> takes a slot there and writes
+//                    the entry at the cell's CSR offset
+//   scan_*           the exclusive prefix of the counts (CSR offsets)
+//   sg_sort_kernel   a thread per cell: (tlo, index) order
+struct SgBuild {
+  const SphGeo *geo;
+  const double *rad;
+  const double *rho;     // [n] origin-ball radius per sphere (< 0: no grid)
+  const int *gsph;       // [ng] the batch's grid spheres
+  const CubePatch *faces, *blocks, *tiles;
+  const double *cell_cbsb;
+  CgDisk *disks;         // [ng][n][2]
+  int2 *pairs;           // [ng][maxp]
+  unsigned *npairs;      // [ng * 16]: pairs per grid (one 64-B line each)
+  unsigned *nglob;       // [ng * 16]: global spheres per grid
+  const unsigned *woff;  // [ng + 1]: work items (4 per kept pair) before grid j; refused grids have none
+  int *cnt;              // [ng][cells] (count pass: list lengths; fill pass: slots taken)
+  const int *off;        // [(g0 + j) cells + c]: the CSR offset of the batch's grid j's cell c
+  int2 *ent;
+  long long nent;        // entries of all grids (the fill pass's bound)
+  int n, ng, g0, N, NT, NB, maxp;
+  double diam;
+};
+static_assert(sizeof(SgBuild) <= 4096, "SgBuild exceeds the kernel-argument segment");
+constexpr int kSgCntStride = 16;
+
+__global__ __launch_bounds__(256) void sg_disk_kernel(const SgBuild a) {
+  const int t = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6), lane = (int)(threadIdx.x & 63);
+  if (t >= a.n * a.ng) return;
+  const int j = t / a.n, i = t - j * a.n;
+  const int gs = a.gsph[j];
+  const SphGeo P = a.geo[RT_CK(kCkCgBuild, gs, a.n)], sp = a.geo[i];
+  const CgView v = cg_view(sp.cx, sp.cy, sp.cz, a.rad[i], P.cx, P.cy, P.cz, a.diam, a.rho[gs]);
+  if (v.global && lane == 0) atomicAdd(&a.nglob[j * kSgCntStride], 1u);
+  const int nb = 6 * a.NB * a.NB;
+  for (int side = 0; side < (v.global ? 1 : 2); ++side) {
+    const CgDisk k = cg_side(v, side, i);
+    const int di = 2 * t + side;
+    if (lane == 0) a.disks[RT_CK(kCkCgBuild, di, 2LL * a.n * a.ng)] = k;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+      const int b = b0 + lane;
+      const bool m = b < nb && cg_block(k, a.faces, a.blocks, a.NB, b);
+      const unsigned long long bm = __ballot(m);
+      if (!bm) continue;
+      unsigned q0 = 0;
+      if (lane == 0) q0 = atomicAdd(&a.npairs[j * kSgCntStride], (unsigned)__builtin_popcountll(bm));
+      q0 = (unsigned)__builtin_amdgcn_readfirstlane((int)q0);
+      const unsigned qi = q0 + (unsigned)__builtin_popcountll(bm & ((1ull << lane) - 1));
+      if (m && qi < (unsigned)a.maxp)
+        a.pairs[RT_CK(kCkCgBuild, (size_t)j * a.maxp + qi, (long long)a.ng * a.maxp)] = make_int2(di, b);
+    }
+  }
+}
+
+template <bool kFill>
+__global__ __launch_bounds__(64) void sg_bin_kernel(const SgBuild a) {
+  const int lane = (int)(threadIdx.x & 63);
+  const long long cells = 6LL * a.N * a.N;
+  const unsigned total = a.woff[a.ng];
+  for (unsigned v = blockIdx.x; v < total; v += gridDim.x) {
+    int lo = 0, hi = a.ng;  // the grid of work item v: woff[j] <= v < woff[j + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (a.woff[mid] <= v) lo = mid; else hi = mid;
+    }
+    const int j = lo;
+    const unsigned item = v - a.woff[j];
+    const int2 pr = a.pairs[RT_CK(kCkCgBuild, (size_t)j * a.maxp + (item >> 2), (long long)a.ng * a.maxp)];
+    const CgDisk k = a.disks[RT_CK(kCkCgBuild, pr.x, 2LL * a.n * a.ng)];
+    const bool wide = cg_wide(k);
+    const int bb = pr.y;
+    const int f = bb / (a.NB * a.NB), bj = (bb / a.NB) % a.NB, bi = bb % a.NB;
+    bool tm, inside;
+    cg_tile(k, a.tiles, a.NT, f, bi, bj, lane, tm, inside);
+    unsigned long long tmask = __ballot(tm) & (0xffffull << (16 * (item & 3)));
+    const unsigned long long imask = __ballot(inside);
+    while (tmask) {
+      const int tl = __builtin_ctzll(tmask);
+      tmask &= tmask - 1;
+      const int gc = cg_cell(k, wide, a.cell_cbsb, a.N, f, bi, bj, tl, lane, (imask >> tl) & 1ull);
+      if (gc >= 0) {
+        const long long ci = RT_CK(kCkCgBuild, (long long)j * cells + gc, a.ng * cells);
+        const int slot = atomicAdd(&a.cnt[ci], 1);
+        if (kFill)
+          a.ent[RT_CK(kCkCgBuild, (long long)a.off[(long long)a.g0 * cells + ci] + slot, a.nent)] =
+              make_int2(k.s, __float_as_int(k.tlo));
+      }
+    }
+  }
+}
+
+// Exclusive prefix sum of n ints (x -> y, y[n] = the total), in chunks of
+// kScanChunk per 256-thread block: chunk sums, their prefix (one block), then
+// each chunk's prefix from its base.
+constexpr int kScanChunk = 4096;
+__device__ __forceinline__ int block_excl_scan256(int x, int *sh, int &total) {
+  const int t = (int)threadIdx.x;
+  sh[t] = x;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int v = t >= o ? sh[t - o] : 0;
+    __syncthreads();
+    sh[t] += v;
+    __syncthreads();
+  }
+  total = sh[255];
+  const int incl = sh[t];
+  __syncthreads();
+  return incl - x;
+}
+__global__ __launch_bounds__(256) void scan_chunk_sums(const int *x, long long n, int *bsum) {
+  __shared__ int sh[256];
+  const long long b0 = (long long)blockIdx.x * kScanChunk;
+  int s = 0;
+  for (int k = threadIdx.x; k < kScanChunk; k += 256)
+    if (b0 + k < n) s += x[b0 + k];
+  int tot;
+  (void)block_excl_scan256(s, sh, tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(256) void scan_sums(int *bsum, int nb) {  // in place, exclusive; bsum[nb] = total
+  __shared__ int sh[256];
+  int base = 0;
+  for (int c0 = 0; c0 < nb; c0 += 256) {
+    const int k = c0 + (int)threadIdx.x;
+    const int x = k < nb ? bsum[k] : 0;
+    int tot;
+    const int e = block_excl_scan256(x, sh, tot);
+    if (k < nb) bsum[k] = base + e;
+    base += tot;
+  }
+  if (threadIdx.x == 0) bsum[nb] = base;
+}
+__global__ __launch_bounds__(256) void scan_apply(const int *x, long long n, const int *bsum, int *y) {
+  __shared__ int sh[256];
+  constexpr int kPer = kScanChunk / 256;
+  const long long b0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kPer;
+  int v[kPer], s = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    v[k] = b0 + k < n ? x[b0 + k] : 0;
+    s += v[k];
+  }
+  int tot;
+  int run = bsum[blockIdx.x] + block_excl_scan256(s, sh, tot);
+#pragma unroll
+  for (int k = 0; k < kPer; ++k)
+    if (b0 + k < n) {
+      y[b0 + k] = run;
+      run += v[k];
+    }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) y[n] = bsum[gridDim.x];
+}
+
+// Sphere s's row of CSR starts (every sphere has one, as on the host): its
+// grid's offsets, or an empty list everywhere (no grid / refused).
+__global__ __launch_bounds__(256) void sg_start_kernel(const int *gidx, const unsigned char *ok, const int *off,
+                                                       int n, long long cells, int *start) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x, row = cells + 1;
+  if (k >= (long long)n * row) return;
+  const int s = (int)(k / row);
+  const long long c = k - (long long)s * row;
+  const int j = gidx[s];
+  start[k] = (j >= 0 && ok[j]) ? off[(long long)j * cells + c] : 0;
+}
+
+// A thread per cell of every grid: its list in (tlo, index) order (insertion sort).
+__global__ __launch_bounds__(256) void sg_sort_kernel(const int *off, long long ncells, int2 *ent) {
+  const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gc >= ncells) return;
+  int2 *e = ent + off[gc];
+  const int cnt = off[gc + 1] - off[gc];
+  for (int k = 1; k < cnt; ++k) {
+    const int2 x = e[k];
+    const float tx = __int_as_float(x.y);
+    int m = k - 1;
+    while (m >= 0 && cg_before(tx, x.x, __int_as_float(e[m].y), e[m].x)) {
+      e[m + 1] = e[m];
+      --m;
+    }
+    e[m + 1] = x;
+  }
+}
+
 }  // namespace rtk
 
 using namespace rtk;
@@ -1709,6 +1907,9 @@ LgArgs lg_args(const rt_ctx *c) {
 // a grid per frame (a quarter of the cells to build)
 constexpr int kCgNStatic = 256, kCgNMoving = 128;
 
+void free_tables(rt_ctx::CgTables &t);
+int upload_tables(rt_ctx *c, int N, rt_ctx::CgTables &t);
+
 // The device patch tables of the cube map with N cells per face edge (two
 // kept; replacing one waits for the launches in flight).
 int cg_tables(rt_ctx *c, int N, const rt_ctx::CgTables *&out) {
@@ -1720,9 +1921,21 @@ int cg_tables(rt_ctx *c, int N, const rt_ctx::CgTables *&out) {
   rt_ctx::CgTables &t = c->cg_tab[c->cg_tab_next];
   c->cg_tab_next ^= 1;
   RT_TRY(c, hipStreamSynchronize(c->stream));
+  free_tables(t);
+  const int rc = upload_tables(c, N, t);
+  if (rc != RT_OK) return rc;
+  out = &t;
+  return RT_OK;
+}
+
+void free_tables(rt_ctx::CgTables &t) {
   for (void *p : {(void *)t.faces, (void *)t.blocks, (void *)t.tiles, (void *)t.cell})
     if (p) (void)hipFree(p);
   t = rt_ctx::CgTables{};
+}
+
+// The cube map's patch tables for N cells per face edge, on the device.
+int upload_tables(rt_ctx *c, int N, rt_ctx::CgTables &t) {
   std::vector<CubePatch> faces, blocks, tiles;
   std::vector<double> cell;
   int NT = 0, NB = 0;
@@ -1738,7 +1951,6 @@ int cg_tables(rt_ctx *c, int N, const rt_ctx::CgTables *&out) {
   t.N = N;
   t.NT = NT;
   t.NB = NB;
-  out = &t;
   return RT_OK;
 }
 
@@ -1937,49 +2149,220 @@ constexpr size_t kSgMaxEntries = size_t(64) << 20;
 // sphere's centre up to the rounding of the hit point; the ball is grown by a
 // relative 1e-6 and the device checks every ray against it).  No grids (and
 // RT_OK) when disabled, too large, or refused.
+// device scratch of one upload-time build, freed on every exit path
+struct DevScratch {
+  std::vector<void *> p;
+  template <class T>
+  hipError_t alloc(T *&out, size_t bytes) {
+    out = nullptr;
+    void *q = nullptr;
+    const hipError_t e = hipMalloc(&q, bytes ? bytes : 1);
+    if (e == hipSuccess) {
+      p.push_back(q);
+      out = static_cast<T *>(q);
+    }
+    return e;
+  }
+  ~DevScratch() {
+    for (void *q : p) (void)hipFree(q);
+  }
+};
+
+// The exclusive prefix sum of x[0 .. n) into y[0 .. n] (y[n] = the total) on the stream.
+int device_scan(rt_ctx *c, const int *x, long long n, int *y) {
+  const long long nb = std::max(1LL, (n + kScanChunk - 1) / kScanChunk);
+  DevScratch sc;
+  int *bsum = nullptr;
+  RT_TRY(c, sc.alloc(bsum, sizeof(int) * (size_t)(nb + 1)));
+  hipLaunchKernelGGL(scan_chunk_sums, dim3((unsigned)nb), dim3(256), 0, c->stream, x, n, bsum);
+  hipLaunchKernelGGL(scan_sums, dim3(1), dim3(256), 0, c->stream, bsum, (int)nb);
+  hipLaunchKernelGGL(scan_apply, dim3((unsigned)nb), dim3(256), 0, c->stream, x, n, bsum, y);
+  RT_TRY(c, hipGetLastError());
+  RT_TRY(c, hipStreamSynchronize(c->stream));  // bsum is freed on return
+  return RT_OK;
+}
+
+// Sphere grids for the reflective spheres of the scene being uploaded (the
+// origins of reflection rays, main.cpp:46, lie within |r| + 0.001 of their
+// sphere's centre up to the rounding of the hit point; the ball is grown by a
+// relative 1e-6 and the device checks every ray against it), built on the
+// device (sg_*_kernel; the geometry is on the device already).  No grids (and
+// RT_OK) when disabled, too large, or refused.
 int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
   const int n = s->num_spheres;
   if (c->sg_mode == 0 || (c->sg_mode < 0 && n > kSgMaxSpheres) || n == 0 || !std::isfinite(diam)) return RT_OK;
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<double> rho((size_t)n, -1.0);
+  std::vector<int> gsph, gidx((size_t)n, -1);
   for (int i = 0; i < n; i++) {
     const rt_sphere &sp = s->spheres[i];
     const double r = std::fabs(sp.radius);
     const double mag = std::fabs(sp.center[0]) + std::fabs(sp.center[1]) + std::fabs(sp.center[2]);
     if (sp.reflectivity > 0.0 && std::isfinite(r) && std::isfinite(mag))  // main.cpp:43
       rho[(size_t)i] = (r + kEps) * (1.0 + 1e-6) + 1e-12 * mag + 1e-9 * diam;
+    if (rho[(size_t)i] >= 0.0 && std::isfinite(rho[(size_t)i])) {  // (build_sphere_grids: a finite ball)
+      gidx[(size_t)i] = (int)gsph.size();
+      gsph.push_back(i);
+    }
   }
   const int N = c->sg_n_opt ? c->sg_n_opt : (n <= kSgFineSpheres ? kSgNFine : kSgN);
   // the device indexes grid key's starts at key * (6 N^2 + 1) in 32 bits, and
   // every sphere has its row of starts: refuse grids that would overflow it
   // or hold more than 1 GiB of starts
-  const size_t nstart = (size_t)n * (6 * (size_t)N * N + 1);
+  const long long cells = 6LL * N * N;
+  const size_t nstart = (size_t)n * (size_t)(cells + 1);
   if (nstart > (size_t)INT32_MAX || nstart * sizeof(int32_t) > ((size_t)1 << 30)) return RT_OK;
-  std::vector<int32_t> start, ent;
-  std::vector<uint8_t> ok;
-  const size_t entries = build_sphere_grids(c->h_sx.data(), c->h_sy.data(), c->h_sz.data(), c->h_sr.data(), n,
-                                            rho.data(), diam, N, kSgMaxGlobal, kSgMaxEntries, start, ent, ok);
-  std::vector<double> rho2((size_t)n);
+  const int ng = (int)gsph.size();
+  c->sg_grids = 0;
+  c->sg_entries = 0;
+  if (ng == 0) {
+    c->sg_build_ms = ms_since(t0);
+    return RT_OK;
+  }
+  if ((long long)ng * cells >= INT32_MAX) return RT_OK;  // 32-bit CSR offsets
+  rt_ctx::CgTables tab;
+  int rc = upload_tables(c, N, tab);
+  struct TabGuard {
+    rt_ctx::CgTables &t;
+    ~TabGuard() { free_tables(t); }
+  } tab_guard{tab};
+  if (rc != RT_OK) return rc;
+  const long long nblocks = 6LL * tab.NB * tab.NB;
+  // pairs kept per grid (a grid with more is refused, as one past the host
+  // builder's entry cap); grids in batches whose disks and pairs fit kSgScratch
+  constexpr size_t kSgScratch = size_t(128) << 20;
+  const long long maxp = std::min<long long>(2LL * n * nblocks, 1 << 22);
+  const size_t per_grid = 2 * (size_t)n * sizeof(CgDisk) + (size_t)maxp * sizeof(int2);
+  const int batch = (int)std::max<long long>(
+      1, std::min<long long>({(long long)ng, (long long)(kSgScratch / per_grid),
+                              (long long)(((1ull << 32) - 1) / (4ull * (unsigned long long)maxp))}));
+  DevScratch sc;
+  double *d_rho = nullptr;
+  int *d_gsph = nullptr, *d_gidx = nullptr, *d_cnt = nullptr, *d_off = nullptr;
+  unsigned char *d_ok = nullptr;
+  CgDisk *d_disks = nullptr;
+  int2 *d_pairs = nullptr;
+  unsigned *d_np = nullptr, *d_woff = nullptr;
+  RT_TRY(c, sc.alloc(d_rho, sizeof(double) * (size_t)n));
+  RT_TRY(c, sc.alloc(d_gsph, sizeof(int) * (size_t)ng));
+  RT_TRY(c, sc.alloc(d_gidx, sizeof(int) * (size_t)n));
+  RT_TRY(c, sc.alloc(d_ok, (size_t)ng));
+  RT_TRY(c, sc.alloc(d_cnt, sizeof(int) * (size_t)(ng * cells)));
+  RT_TRY(c, sc.alloc(d_off, sizeof(int) * (size_t)(ng * cells + 1)));
+  RT_TRY(c, sc.alloc(d_disks, 2 * (size_t)n * batch * sizeof(CgDisk)));
+  RT_TRY(c, sc.alloc(d_pairs, (size_t)maxp * batch * sizeof(int2)));
+  RT_TRY(c, sc.alloc(d_np, 2 * sizeof(unsigned) * kSgCntStride * (size_t)batch));
+  RT_TRY(c, sc.alloc(d_woff, sizeof(unsigned) * (size_t)(batch + 1)));
+  RT_TRY(c, hipMemcpy(d_rho, rho.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
+  RT_TRY(c, hipMemcpy(d_gsph, gsph.data(), sizeof(int) * (size_t)ng, hipMemcpyHostToDevice));
+  RT_TRY(c, hipMemcpy(d_gidx, gidx.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice));
+  RT_TRY(c, hipMemsetAsync(d_cnt, 0, sizeof(int) * (size_t)(ng * cells), c->stream));
+  SgBuild b{};
+  b.geo = c->d_geo;
+  b.rad = c->d_rad;
+  b.rho = d_rho;
+  b.faces = tab.faces;
+  b.blocks = tab.blocks;
+  b.tiles = tab.tiles;
+  b.cell_cbsb = tab.cell;
+  b.disks = d_disks;
+  b.pairs = d_pairs;
+  b.npairs = d_np;
+  b.nglob = d_np + kSgCntStride * (size_t)batch;
+  b.woff = d_woff;
+  b.off = d_off;
+  b.n = n;
+  b.N = N;
+  b.NT = tab.NT;
+  b.NB = tab.NB;
+  b.maxp = (int)maxp;
+  b.diam = diam;
+  std::vector<unsigned char> ok((size_t)ng, 0);
+  std::vector<std::vector<unsigned>> woffs;
+  // one batch of grids: disks and pairs (pass 1), and on the count pass the
+  // grids' refusals and work offsets; then the bin pass (count or fill)
+  auto run_batch = [&](int g0, bool fill) -> int {
+    const int nbg = std::min(batch, ng - g0);
+    b.gsph = d_gsph + g0;
+    b.ng = nbg;
+    b.g0 = g0;
+    b.cnt = d_cnt + (size_t)g0 * cells;
+    RT_TRY(c, hipMemsetAsync(d_np, 0, 2 * sizeof(unsigned) * kSgCntStride * (size_t)batch, c->stream));
+    const long long waves = (long long)n * nbg;
+    hipLaunchKernelGGL(sg_disk_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, c->stream, b);
+    RT_TRY(c, hipGetLastError());
+    if (!fill) {
+      std::vector<unsigned> hn(2 * kSgCntStride * (size_t)batch);
+      RT_TRY(c, hipMemcpyAsync(hn.data(), d_np, sizeof(unsigned) * hn.size(), hipMemcpyDeviceToHost, c->stream));
+      RT_TRY(c, hipStreamSynchronize(c->stream));
+      std::vector<unsigned> wo((size_t)nbg + 1, 0);
+      for (int j = 0; j < nbg; j++) {
+        const unsigned np = hn[(size_t)j * kSgCntStride], nglob = hn[((size_t)batch + j) * kSgCntStride];
+        const bool g_ok = nglob <= (unsigned)kSgMaxGlobal && np <= (unsigned)maxp;
+        ok[(size_t)(g0 + j)] = g_ok ? 1 : 0;
+        wo[(size_t)j + 1] = wo[(size_t)j] + (g_ok ? 4u * np : 0u);
+      }
+      woffs.push_back(wo);
+    }
+    const std::vector<unsigned> &wo = woffs[(size_t)(g0 / batch)];
+    RT_TRY(c, hipMemcpyAsync(d_woff, wo.data(), sizeof(unsigned) * wo.size(), hipMemcpyHostToDevice, c->stream));
+    const unsigned items = wo.back();
+    if (items) {
+      const dim3 grid((unsigned)std::min<unsigned>(items, 16384u));
+      if (fill)
+        hipLaunchKernelGGL(sg_bin_kernel<true>, grid, dim3(64), 0, c->stream, b);
+      else
+        hipLaunchKernelGGL(sg_bin_kernel<false>, grid, dim3(64), 0, c->stream, b);
+      RT_TRY(c, hipGetLastError());
+    }
+    // the host copy of the work offsets is read by the stream: wait before the next batch rewrites them
+    RT_TRY(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+  };
+  for (int g0 = 0; g0 < ng; g0 += batch)
+    if ((rc = run_batch(g0, false)) != RT_OK) return rc;
+  if ((rc = device_scan(c, d_cnt, (long long)ng * cells, d_off)) != RT_OK) return rc;
+  int total = 0;
+  RT_TRY(c, hipMemcpy(&total, d_off + (size_t)(ng * cells), sizeof(int), hipMemcpyDeviceToHost));
   int grids = 0;
+  for (int j = 0; j < ng; j++) grids += ok[(size_t)j];
+  if ((size_t)total > kSgMaxEntries || grids == 0) {  // as build_sphere_grids past max_entries: no grids
+    c->sg_build_ms = ms_since(t0);
+    return RT_OK;
+  }
+  int2 *d_ent = nullptr;
+  int32_t *d_start = nullptr;
+  double *d_rho2 = nullptr;
+  RT_TRY(c, hipMalloc(&d_ent, sizeof(int2) * ((size_t)total + 1)));
+  c->d_sg_ent = d_ent;  // owned by the context from here (free_scene)
+  RT_TRY(c, hipMalloc(&d_start, sizeof(int32_t) * nstart));
+  c->d_sg_start = d_start;
+  RT_TRY(c, hipMalloc(&d_rho2, sizeof(double) * (size_t)n));
+  c->d_sg_rho2 = d_rho2;
+  b.ent = d_ent;
+  b.nent = total;
+  RT_TRY(c, hipMemsetAsync(d_cnt, 0, sizeof(int) * (size_t)(ng * cells), c->stream));
+  for (int g0 = 0; g0 < ng; g0 += batch)
+    if ((rc = run_batch(g0, true)) != RT_OK) return rc;
+  hipLaunchKernelGGL(sg_sort_kernel, dim3((unsigned)((ng * cells + 255) / 256)), dim3(256), 0, c->stream, d_off,
+                     (long long)(ng * cells), d_ent);
+  RT_TRY(c, hipMemcpy(d_ok, ok.data(), (size_t)ng, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(sg_start_kernel, dim3((unsigned)((nstart + 255) / 256)), dim3(256), 0, c->stream, d_gidx, d_ok,
+                     d_off, n, cells, d_start);
+  RT_TRY(c, hipGetLastError());
+  std::vector<double> rho2((size_t)n);
   for (int i = 0; i < n; i++) {
-    rho2[(size_t)i] = ok[(size_t)i] ? rho[(size_t)i] * rho[(size_t)i] : -1.0;
-    grids += ok[(size_t)i] ? 1 : 0;
+    const int j = gidx[(size_t)i];
+    rho2[(size_t)i] = (j >= 0 && ok[(size_t)j]) ? rho[(size_t)i] * rho[(size_t)i] : -1.0;
   }
-  if (grids > 0) {
-    RT_TRY(c, hipMalloc(&c->d_sg_start, sizeof(int32_t) * start.size()));
-    RT_TRY(c, hipMalloc(&c->d_sg_ent, sizeof(int32_t) * ent.size() + sizeof(int2)));
-    RT_TRY(c, hipMalloc(&c->d_sg_rho2, sizeof(double) * (size_t)n));
-    RT_TRY(c, hipMemcpy(c->d_sg_start, start.data(), sizeof(int32_t) * start.size(), hipMemcpyHostToDevice));
-    if (!ent.empty())
-      RT_TRY(c, hipMemcpy(c->d_sg_ent, ent.data(), sizeof(int32_t) * ent.size(), hipMemcpyHostToDevice));
-    RT_TRY(c, hipMemcpy(c->d_sg_rho2, rho2.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
-    c->sg_n = N;
-    c->sg_nstart = (long long)start.size();
-    c->sg_nent = (long long)ent.size() / 2;
-    c->sg_ok = true;
-  }
+  RT_TRY(c, hipMemcpy(d_rho2, rho2.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
+  RT_TRY(c, hipStreamSynchronize(c->stream));  // the scratch is freed on return
+  c->sg_n = N;
+  c->sg_nstart = (long long)nstart;
+  c->sg_nent = total;
+  c->sg_ok = true;
   c->sg_grids = grids;
-  c->sg_entries = entries;
+  c->sg_entries = (size_t)total;
   c->sg_build_ms = ms_since(t0);
   return RT_OK;
 }
@@ -2617,6 +3000,7 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
   c->bvh_depth = depth2;
   c->bvh4_root = root4;
   c->bvh4_stack = stack4;
+  double scene_diam = 0.0;
   {
     double d2 = 0.0;
     for (int k = 0; k < 3; k++) d2 += (hi[k] - lo[k]) * (hi[k] - lo[k]);
@@ -2656,14 +3040,7 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
       delete[] hl;
       return rc;
     }
-    if ((rc = sphere_grids(c, s, diam)) != RT_OK) {
-      free_scene(c);
-      delete[] hg;
-      delete[] hr;
-      delete[] hm;
-      delete[] hl;
-      return rc;
-    }
+    scene_diam = diam;
   }
   for (int k = 0; k < 3; k++) {
     c->c0[k] = c0[k];
@@ -2680,6 +3057,8 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
       (e = hipMemcpy(c->d_mat, hm, sizeof(SphMat) * n, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMemcpy(c->d_lights, hl, sizeof(LightD) * nl, hipMemcpyHostToDevice)) != hipSuccess) {
     rc = fail(c, e, "rt_upload_scene");
+    free_scene(c);
+  } else if ((rc = sphere_grids(c, s, scene_diam)) != RT_OK) {  // built on the device from d_geo / d_rad
     free_scene(c);
   } else {
     c->nsph = n;

@@ -171,6 +171,27 @@ def test_camera_grid_device_builder(tmp_path):
     assert w[8] == "0" and w[10] == "0" and w[12] == "0", out.stdout
 
 
+def test_sphere_grid_device_builder_matches_host(tmp_path):
+    """The device sphere-grid builder (rt_kernel.hip sg_disk / sg_bin / scan /
+    sg_sort / sg_start kernels, per-lane functions shared through
+    csrc/rt_cgbuild.h) run lane by lane in its pass structure on the CPU
+    (tests/native/sg_device_check.cpp) gives, on 120 random scenes (scales
+    0.1-1000, far from the origin, negative and tiny radii, a ground-sized
+    sphere, dense clusters whose grids exceed the global-sphere cap), the same
+    grid spheres, the same refusals and, for every cell of every grid, exactly
+    build_sphere_grids' list (sphere, tlo bits) in the same order -- so the
+    host builder's proofs (tests/native/sg_check.cpp) carry over."""
+    exe = tmp_path / "sg_device_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-o", str(exe),
+                    os.path.join(REPO, "tests", "native", "sg_device_check.cpp"),
+                    os.path.join(CSRC, "rt_lightgrid.cpp"), "-lpthread"], check=True)
+    out = subprocess.run([str(exe), "120"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    w = out.stdout.split()
+    assert w[0] == "scenes" and int(w[3]) > 3000 and int(w[5]) > 500 and int(w[9]) > 10000000, out.stdout
+    assert w[11] == "0", out.stdout
+
+
 CAM_SCENES = dict(GRID_SCENES)
 CAM_SCENES.update({
     # the camera inside a mirror sphere that holds the other spheres
