@@ -290,6 +290,7 @@ def end_to_end(rt_hip, scene_file, W, H, D, device, runs=3):
     import time as _t
 
     parts = {k: [] for k in ("parse_ms", "create_ms", "upload_ms", "render_ms", "write_p3_ms", "total_ms")}
+    up_parts = {k: [] for k in ("bvh_ms", "light_grids_ms", "sphere_grids_ms", "behind_grid_ms")}
     with tempfile.TemporaryDirectory() as tmp:
         out = os.path.join(tmp, "output_gpu.ppm")
         for _ in range(runs):
@@ -301,6 +302,11 @@ def end_to_end(rt_hip, scene_file, W, H, D, device, runs=3):
             t.append(_t.perf_counter())
             r.upload(sc)
             t.append(_t.perf_counter())
+            info = info_or_none(r)
+            if info is not None:  # rt_upload_scene's builds (host wall time, inside upload_ms)
+                for k, v in zip(up_parts, (info.bvh_build_ms, info.light_grid_build_ms, info.sphere_grid_build_ms,
+                                           info.behind_grid_build_ms)):
+                    up_parts[k].append(v)
             rgb, st = r.render(cam, W, H, D)
             t.append(_t.perf_counter())
             rt_hip.write_ppm(out, rgb, W, H)
@@ -312,6 +318,8 @@ def end_to_end(rt_hip, scene_file, W, H, D, device, runs=3):
             kernel_ms, rays = st.kernel_ms, st.rays
         size = os.path.getsize(out)
     res = {k: round(median(v), 3) for k, v in parts.items()}
+    if all(up_parts.values()):
+        res["upload_parts_ms"] = {k: round(median(v), 3) for k, v in up_parts.items()}
     res.update({"kernel_ms": round(kernel_ms, 4), "rays": rays, "p3_bytes": size, "runs": runs,
                 "mrays_per_s_end_to_end": round(rays / median(parts["total_ms"]) / 1e3, 1)})
     return res

@@ -8,6 +8,7 @@
 // last ambient/camera wins; malformed records are skipped with a warning;
 // trailing tokens are ignored.  Numbers go through std::istream >> double, the
 // same extractor the reference uses, so parsed doubles are identical.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +18,9 @@
 #include <sstream>
 #include <string>
 #include <vector>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 
 #include "rt_hip.h"
 
@@ -207,24 +211,58 @@ int rt_write_ppm(const char *path, const uint8_t *rgb, int width, int height, in
       }
     };
     static const Tab T;
-    const auto &tab = T.s;
-    const auto &len = T.n;
-    const size_t chunk_px = 1 << 16;
-    std::vector<char> buf(chunk_px * 12);
-    for (size_t p0 = 0; p0 < n && rc == RT_OK; p0 += chunk_px) {
-      size_t p1 = p0 + chunk_px < n ? p0 + chunk_px : n;
-      char *o = buf.data();
+    // pixel ranges formatted in parallel (each into its own buffer, at most
+    // 12 bytes per pixel), then written in order: the bytes are the serial
+    // writer's (main.cpp:69-91: rows as given, "r g b\n" per pixel)
+    auto format = [&](size_t p0, size_t p1, std::vector<char> &out) {
+      out.resize((p1 - p0) * 12);
+      char *o = out.data();
       for (size_t p = p0; p < p1; p++) {
         for (int c = 0; c < 3; c++) {
-          unsigned v = rgb[3 * p + c];
-          std::memcpy(o, tab[v], 4);
-          o += len[v];
+          const unsigned v = rgb[3 * p + c];
+          std::memcpy(o, T.s[v], 4);
+          o += T.n[v];
           *o++ = c == 2 ? '\n' : ' ';
         }
       }
-      size_t bytes = (size_t)(o - buf.data());
-      if (std::fwrite(buf.data(), 1, bytes, f) != bytes) rc = RT_ERR_IO;
+      out.resize((size_t)(o - out.data()));
+    };
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t nthr = n < ((size_t)1 << 16) ? 1 : std::max<size_t>(1, std::min<size_t>(hw ? hw : 1, 16));
+    const size_t nchunk = nthr * 4;  // a few per thread: the first write starts while the rest are formatted
+    std::vector<std::vector<char>> bufs(nchunk);
+    std::vector<unsigned char> done(nchunk, 0);
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t next = 0;
+    auto worker = [&]() {
+      for (;;) {
+        size_t k;
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          if (next >= nchunk) return;
+          k = next++;
+        }
+        format(n * k / nchunk, n * (k + 1) / nchunk, bufs[k]);
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          done[k] = 1;
+        }
+        cv.notify_all();
+      }
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nthr; t++) th.emplace_back(worker);
+    if (nthr == 1) worker();
+    for (size_t k = 0; k < nchunk; k++) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done[k] != 0; });
+      }
+      if (rc == RT_OK && std::fwrite(bufs[k].data(), 1, bufs[k].size(), f) != bufs[k].size()) rc = RT_ERR_IO;
+      std::vector<char>().swap(bufs[k]);
     }
+    for (auto &t : th) t.join();
   }
   if (std::fclose(f) != 0) rc = RT_ERR_IO;
   return rc;

@@ -1507,30 +1507,34 @@ __device__ __forceinline__ int block_excl_scan256(int x, int *sh, int &total) {
   __syncthreads();
   return incl - x;
 }
-__global__ __launch_bounds__(256) void scan_chunk_sums(const int *x, long long n, int *bsum) {
-  __shared__ int sh[256];
+__global__ __launch_bounds__(256) void scan_chunk_sums(const int *x, long long n, long long *bsum) {
+  __shared__ long long sh[256];
   const long long b0 = (long long)blockIdx.x * kScanChunk;
-  int s = 0;
+  long long s = 0;
   for (int k = threadIdx.x; k < kScanChunk; k += 256)
     if (b0 + k < n) s += x[b0 + k];
-  int tot;
-  (void)block_excl_scan256(s, sh, tot);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
-}
-__global__ __launch_bounds__(256) void scan_sums(int *bsum, int nb) {  // in place, exclusive; bsum[nb] = total
-  __shared__ int sh[256];
-  int base = 0;
-  for (int c0 = 0; c0 < nb; c0 += 256) {
-    const int k = c0 + (int)threadIdx.x;
-    const int x = k < nb ? bsum[k] : 0;
-    int tot;
-    const int e = block_excl_scan256(x, sh, tot);
-    if (k < nb) bsum[k] = base + e;
-    base += tot;
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
   }
-  if (threadIdx.x == 0) bsum[nb] = base;
+  if (threadIdx.x == 0) bsum[blockIdx.x] = sh[0];
 }
-__global__ __launch_bounds__(256) void scan_apply(const int *x, long long n, const int *bsum, int *y) {
+// in place, exclusive, in 64 bits (bsum[nb] = the total: the caller refuses
+// totals past 32 bits before using the offsets); a few thousand chunk sums at
+// most, serially in one thread
+__global__ __launch_bounds__(64) void scan_sums(long long *bsum, int nb) {
+  if (threadIdx.x != 0) return;
+  long long run = 0;
+  for (int k = 0; k < nb; ++k) {
+    const long long v = bsum[k];
+    bsum[k] = run;
+    run += v;
+  }
+  bsum[nb] = run;
+}
+__global__ __launch_bounds__(256) void scan_apply(const int *x, long long n, const long long *bsum, int *y) {
   __shared__ int sh[256];
   constexpr int kPer = kScanChunk / 256;
   const long long b0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kPer;
@@ -1541,14 +1545,14 @@ __global__ __launch_bounds__(256) void scan_apply(const int *x, long long n, con
     s += v[k];
   }
   int tot;
-  int run = bsum[blockIdx.x] + block_excl_scan256(s, sh, tot);
+  int run = (int)bsum[blockIdx.x] + block_excl_scan256(s, sh, tot);
 #pragma unroll
   for (int k = 0; k < kPer; ++k)
     if (b0 + k < n) {
       y[b0 + k] = run;
       run += v[k];
     }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) y[n] = bsum[gridDim.x];
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) y[n] = (int)bsum[gridDim.x];
 }
 
 // Sphere s's row of CSR starts (every sphere has one, as on the host): its
@@ -1652,6 +1656,7 @@ struct rt_ctx {
   bool sg_ok = false;
   size_t sg_entries = 0;
   double sg_build_ms = 0.0;
+  double bvh_build_ms = 0.0, lg_build_ms = 0.0;  // rt_upload_scene's host builds (rt_info)
   // behind grid (rt_bvh.h build_ugrid): the backward half of the ordered
   // walks' closest-hit lines (rt_device.h behind_cells), built at upload
   int ug_mode = -1;  // RT_HIP_BEHIND_GRID: -1 auto (scenes above kBvhAlwaysAbove spheres), 0 off, 1 on
@@ -2142,7 +2147,7 @@ int cam_grid_enqueue(rt_ctx *c, const CgPlan &p, CgArgs &out) {
 constexpr int kSgN = 16, kSgNFine = 32, kSgFineSpheres = 512;
 constexpr int kSgMaxSpheres = 2048;     // RT_HIP_SPHERE_GRID=-1: larger scenes keep the BVH walks
 constexpr int kSgMaxGlobal = 32;        // spheres overlapping an origin ball (on every list of its grid)
-constexpr size_t kSgMaxEntries = size_t(64) << 20;
+constexpr size_t kSgMaxEntries = size_t(256) << 20;  // 2 GiB of lists (built on the device)
 
 // Sphere grids for the reflective spheres of the scene being uploaded (the
 // origins of reflection rays, main.cpp:46, lie within |r| + 0.001 of their
@@ -2168,16 +2173,18 @@ struct DevScratch {
   }
 };
 
-// The exclusive prefix sum of x[0 .. n) into y[0 .. n] (y[n] = the total) on the stream.
-int device_scan(rt_ctx *c, const int *x, long long n, int *y) {
+// The exclusive prefix sum of x[0 .. n) into y[0 .. n] (y[n] = the total) on
+// the stream; `total` the sum in 64 bits (y holds it only when below 2^31).
+int device_scan(rt_ctx *c, const int *x, long long n, int *y, long long &total) {
   const long long nb = std::max(1LL, (n + kScanChunk - 1) / kScanChunk);
   DevScratch sc;
-  int *bsum = nullptr;
-  RT_TRY(c, sc.alloc(bsum, sizeof(int) * (size_t)(nb + 1)));
+  long long *bsum = nullptr;
+  RT_TRY(c, sc.alloc(bsum, sizeof(long long) * (size_t)(nb + 1)));
   hipLaunchKernelGGL(scan_chunk_sums, dim3((unsigned)nb), dim3(256), 0, c->stream, x, n, bsum);
-  hipLaunchKernelGGL(scan_sums, dim3(1), dim3(256), 0, c->stream, bsum, (int)nb);
+  hipLaunchKernelGGL(scan_sums, dim3(1), dim3(64), 0, c->stream, bsum, (int)nb);
   hipLaunchKernelGGL(scan_apply, dim3((unsigned)nb), dim3(256), 0, c->stream, x, n, bsum, y);
   RT_TRY(c, hipGetLastError());
+  RT_TRY(c, hipMemcpyAsync(&total, bsum + nb, sizeof(long long), hipMemcpyDeviceToHost, c->stream));
   RT_TRY(c, hipStreamSynchronize(c->stream));  // bsum is freed on return
   return RT_OK;
 }
@@ -2321,9 +2328,8 @@ int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
   };
   for (int g0 = 0; g0 < ng; g0 += batch)
     if ((rc = run_batch(g0, false)) != RT_OK) return rc;
-  if ((rc = device_scan(c, d_cnt, (long long)ng * cells, d_off)) != RT_OK) return rc;
-  int total = 0;
-  RT_TRY(c, hipMemcpy(&total, d_off + (size_t)(ng * cells), sizeof(int), hipMemcpyDeviceToHost));
+  long long total = 0;
+  if ((rc = device_scan(c, d_cnt, (long long)ng * cells, d_off, total)) != RT_OK) return rc;
   int grids = 0;
   for (int j = 0; j < ng; j++) grids += ok[(size_t)j];
   if ((size_t)total > kSgMaxEntries || grids == 0) {  // as build_sphere_grids past max_entries: no grids
@@ -2909,6 +2915,7 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     br[i] = s->spheres[i].radius;
   }
   const bool big = n > kBvhAlwaysAbove;
+  const auto t_bvh = std::chrono::steady_clock::now();
   // leaves of 2 spheres (+0.6..0.9 % over 4 on synth200 with the merged levels);
   // 1 above kBvhAlwaysAbove, where every closest hit walks (synth10k 4.37 -> 4.16 ms)
   c->bvh_leaf = c->bvh_leaf_opt ? c->bvh_leaf_opt : (big ? 1 : 2);
@@ -2955,6 +2962,7 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     delete[] hl;
     return rc;
   }
+  c->bvh_build_ms = ms_since(t_bvh);
   if (c->ug_mode > 0 || (c->ug_mode < 0 && big)) {
     const auto t_ug = std::chrono::steady_clock::now();
     UgridHost ug;
@@ -3016,6 +3024,7 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
       ly[i] = s->lights[i].position[1];
       lz[i] = s->lights[i].position[2];
     }
+    const auto t_lg = std::chrono::steady_clock::now();
     std::vector<int32_t> lg_start, lg_ids;
     build_light_grid(sx.data(), sy.data(), sz.data(), br.data(), n, lx.data(), ly.data(), lz.data(), nl, diam,
                      c->lg_n, lg_start, lg_ids);
@@ -3040,6 +3049,7 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
       delete[] hl;
       return rc;
     }
+    c->lg_build_ms = ms_since(t_lg);
     scene_diam = diam;
   }
   for (int k = 0; k < 3; k++) {
@@ -3289,6 +3299,8 @@ int rt_get_info(rt_ctx *c, rt_info *out) {
   out->behind_grid_cells = c->ug_ok ? (uint64_t)c->ug.nx * (uint64_t)c->ug.ny * (uint64_t)c->ug.nz : 0;
   out->behind_grid_entries = c->ug_ok ? (uint64_t)c->ug_entries : 0;
   out->behind_grid_build_ms = c->ug_build_ms;
+  out->bvh_build_ms = c->bvh_build_ms;
+  out->light_grid_build_ms = c->lg_build_ms;
   return RT_OK;
 }
 

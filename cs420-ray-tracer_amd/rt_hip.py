@@ -28,7 +28,7 @@ VARIANTS = {"tuning": os.path.join(HERE, "variants", "librt_hip_tuning.so"),
             "check": os.path.join(HERE, "variants", "librt_hip_check.so")}
 
 RT_MAX_DEPTH = 64
-ABI_VERSION = 10  # RT_HIP_ABI_VERSION in include/rt_hip.h
+ABI_VERSION = 11  # RT_HIP_ABI_VERSION in include/rt_hip.h
 MAX_FRAMES = 32  # RT_MAX_FRAMES
 
 
@@ -67,7 +67,8 @@ class rt_info(C.Structure):
                 ("sphere_grids", C.c_int32), ("sphere_grid_n", C.c_int32), ("sphere_grid_entries", C.c_uint64),
                 ("sphere_grid_build_ms", C.c_double), ("behind_grid", C.c_int32), ("behind_grid_last", C.c_int32),
                 ("behind_grid_cells", C.c_uint64), ("behind_grid_entries", C.c_uint64),
-                ("behind_grid_build_ms", C.c_double)]
+                ("behind_grid_build_ms", C.c_double), ("bvh_build_ms", C.c_double),
+                ("light_grid_build_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

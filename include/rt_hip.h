@@ -52,9 +52,10 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 10 /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
+#define RT_HIP_ABI_VERSION 11 /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
                                    6: rt_render_tiles; 7: rt_get_info; 8: rt_info sphere-grid fields;
-                                   9: rt_info behind-grid fields; 10: RT_ERR_CHECK */
+                                   9: rt_info behind-grid fields; 10: RT_ERR_CHECK;
+                                   11: rt_info BVH / light-grid build times */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -279,6 +280,8 @@ typedef struct rt_info {
     uint64_t behind_grid_cells;  /* its cells */
     uint64_t behind_grid_entries;  /* its list entries (20 bytes each) */
     double behind_grid_build_ms; /* host wall time of its build, part of upload_ms */
+    double bvh_build_ms;         /* host wall time of the BVH build and upload, part of upload_ms */
+    double light_grid_build_ms;  /* host wall time of the light grids' build and upload, part of upload_ms */
 } rt_info;
 int rt_get_info(rt_ctx *ctx, rt_info *out);
 

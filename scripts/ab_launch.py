@@ -6,7 +6,8 @@ and a byte check that every setting renders the same image.
   python scripts/ab_launch.py VAR=v1,v2,... [workload ...]
   python scripts/ab_launch.py "A=1+B=0;A=2;default" [workload ...]   (settings of several knobs)
 Every setting runs on the tuning build (variants/librt_hip_tuning.so), the
-default one included, so the A/B compares one library."""
+default one included, so the A/B compares one library -- or on the library
+RT_HIP_LIB names, when set (scripts/ab_libs.sh)."""
 import os
 import sys
 
@@ -27,13 +28,18 @@ def run(workload, env, reps=3):
     try:
         sc = rt_hip.Scene.load(os.path.join(bench.PKG, "scenes", name + ".txt"))
         cam = sc.camera()
-        r = rt_hip.Renderer(0, variant="tuning")
+        # the tuning build, unless RT_HIP_LIB names a library (scripts/ab_libs.sh's A/B of builds)
+        r = rt_hip.Renderer(0, variant=None if os.environ.get("RT_HIP_LIB") else "tuning")
         r.upload(sc)
+        info = bench.info_or_none(r)
         rows = rt_hip.rt_rows(1, 0, 1, H)
         F = 32
         buf = torch.empty((F, H, W, 3), dtype=torch.uint8, device="cuda:0")
         one = bench.single_frame(rt_hip, r, cam, W, H, D, rows, buf[0].data_ptr(), samples=7)
         res = {"single_ms": one["kernel_ms"], "single_wall": one["wall_ms"]}
+        if info is not None:
+            res.update(upload_ms=round(info.upload_ms, 2), sphere_grids=info.sphere_grids,
+                       sg_entries=info.sphere_grid_entries, sg_build_ms=round(info.sphere_grid_build_ms, 2))
         for nf in (32, 20, 8):
             cams = [cam] * nf
             r.render_frames_async(cams, W, H, D, rows, buf.data_ptr(), H * W * 3)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Fold gpu_pmc.sh counter passes into profiles/pmc_traffic.json (read by bench.py).
+"""Fold scripts/gpu_profile.sh counter passes into profiles/pmc_traffic.json (read by bench.py).
 
   python scripts/make_pmc_json.py WORKLOAD PMC_DIR [KERNEL_SUBSTR]
 
