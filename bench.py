@@ -506,7 +506,7 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
         torch.cuda.synchronize()
         assembled_ok = bool(torch.equal(full, image))
     info_timed = info_or_none(r)  # None: an RT_HIP_LIB diagnostic build without rt_get_info
-    camera_grid = sphere_grids = behind_grid = None
+    camera_grid = sphere_grids = behind_grid = scratch = None
     if info_timed is not None and info_warm is not None:
         camera_grid = {"used_by_timed_launches": bool(info_timed.cam_grid_last),
                        "cells_per_face_edge": info_timed.cam_grid_n,
@@ -520,6 +520,9 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
                         "entries": info_timed.sphere_grid_entries,
                         "build_ms": round(info_timed.sphere_grid_build_ms, 2)}
         # uniform grid (closest hits of scenes above 1,024 spheres), built by rt_upload_scene
+        scratch = {"bytes": int(info_timed.scratch_bytes),
+                   "what": "device scratch of the context after the timed launches: reflection-stack homes, the "
+                           "deferred queue with its slots' stacks, the camera grid, the tile order (rt_info)"}
         behind_grid = {"built": bool(info_timed.behind_grid),
                        "used_by_timed_launches": bool(info_timed.behind_grid_last),
                        "cells": info_timed.behind_grid_cells, "entries": info_timed.behind_grid_entries,
@@ -551,7 +554,8 @@ def measure(rt_hip, torch, dist, workload, steps, warmup, world, rank, device, c
             "rank_kernel_ms_per_frame": rank_kernel_ms, "world_size_seen": seen_world,
             "warmup_frames_rendered": max(warmup, F) + (1 + warm_extra) * F,
             "launch_frames": rt_frames.batch_sizes(steps, F),
-            "camera_grid": camera_grid, "sphere_grids": sphere_grids, "behind_grid": behind_grid, **extra}
+            "camera_grid": camera_grid, "sphere_grids": sphere_grids, "behind_grid": behind_grid,
+            "scratch": scratch, **extra}
 
 
 def main():
@@ -702,7 +706,7 @@ def main():
                        # single_frame / moving_camera are the rates without that assumption
                        "view": "static camera: every frame the scene file's view",
                        "camera_grid": m["camera_grid"], "sphere_grids": m["sphere_grids"],
-                       "behind_grid": m["behind_grid"]},
+                       "behind_grid": m["behind_grid"], "scratch": m["scratch"]},
             # achieved = the fp64 FLOPs the render kernels EXECUTE per frame
             # (rocprofv3 PMC, 64 x (ADD + MUL + 2 FMA + TRANS)_F64 wave-instructions,
             # profiles/pmc_traffic.json taken with these kernel sources) over the

@@ -84,7 +84,11 @@ struct RenderArgs {
   CgArgs cg;  // camera grid of the launch's (shared) camera position; cg.on = 0: none
   SgArgs sg;  // sphere grids (reflection rays); sg.on = 0: none
   OutDesc od;
-  StackEnt *gstack;
+  StackEnt *gstack;               // kStackGlobal: [depth-1][launch pixels]
+  StackEnt *homes;                // kStackMerge: [home][depth-1][kMergeTiles * 64] (a wave's group of tiles)
+  unsigned long long *home_bits;  // kStackMerge: the homes taken (a bit each)
+  int home_words;                 // kStackMerge: 64-bit words of home_bits
+  StackEnt *dstack;               // kStackMerge: deferred rays' stacks, [depth-1][kShards * dq_cap]
   unsigned long long *counters;
   int ntx, ntiles;
   int nslots;                     // wave slots per frame: kStackMerge tile groups, kStackGlobal with perm
@@ -620,6 +624,43 @@ __device__ __forceinline__ void flush_tile(const RenderArgs &a, int tile, int fr
   }
 }
 
+// A merged wave's reflection stack lives in a "home": [depth-1][kMergeTiles *
+// 64] entries, one per pixel of its group (lidx) and level, taken from the
+// context's pool when the wave's first reflection ray spawns and returned
+// when the wave ends.  The pool has twice as many homes as waves can be
+// resident on the device (the host sizes it by the occupancy API), so a free
+// one exists whenever a wave asks; the bitmap is searched from a word picked
+// by the workgroup id, one atomic OR per try.  The stack memory of a launch
+// is bounded by the pool, not by its pixels (kStackGlobal keeps the
+// per-pixel stack).
+constexpr int kHomePx = kMergeTiles * 64;
+__device__ __forceinline__ int home_acquire(unsigned long long *bits, int nwords) {
+  int h = -1;
+  if ((threadIdx.x & 63) == 0) {
+    int w = (int)(blockIdx.x % (unsigned)nwords);
+    unsigned long long cur = 0ull;  // a guess: the first try learns the word
+    while (h < 0) {
+      while (~cur) {
+        const int bit = __builtin_ctzll(~cur);
+        const unsigned long long old = atomicOr(bits + w, 1ull << bit);
+        if (!((old >> bit) & 1ull)) {
+          h = w * 64 + bit;
+          break;
+        }
+        cur = old | (1ull << bit);
+      }
+      if (h < 0) {
+        w = w + 1 == nwords ? 0 : w + 1;
+        cur = 0ull;
+      }
+    }
+  }
+  return __shfl(h, 0, 64);
+}
+__device__ __forceinline__ void home_release(unsigned long long *bits, int h) {
+  if ((threadIdx.x & 63) == 0) atomicAnd(bits + (h >> 6), ~(1ull << (h & 63)));
+}
+
 template <bool kCull, bool kFast>
 __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                             const SphMat *__restrict__ mat, const LightD *__restrict__ slight,
@@ -634,7 +675,6 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
   for (int i = 0; i < (int)((kPixbufIds + 255) / 256); ++i)  // padding, depth 0 and deferred pixels: 0
     if ((size_t)(i * 256 + lane * 4) < kPixbufIds) reinterpret_cast<LdsU32 *>(pixbuf())[i * 64 + lane] = 0u;
   const int depth = a.depth;
-  const unsigned sstride = (unsigned)ca.npx;
   int qn = 0;        // queued rays q[0 .. qn), wave-uniform, < Q between passes
   const int Q = kernarg_late<true, offsetof(RenderArgs, merge_q)>(a.merge_q);
   int next = 0;      // next tile of the group
@@ -643,6 +683,13 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
   int key = -1, dleft = 0, lev = 0;
   unsigned pix = 0;
   int lidx = 0;  // the pixel's place in the group: tile slot * 64 + y * 8 + x (pixbuf byte 3 * lidx)
+  int home = -1;  // the group's stack home (home_acquire), once a reflection ray spawned
+  auto hs = [&]() {
+    return kernarg_late<true, offsetof(RenderArgs, homes)>(a.homes) + (size_t)home * (size_t)(depth - 1) * kHomePx;
+  };
+  auto hslot = [&](int l) {
+    return RT_CK(kCkStack, (size_t)l * kHomePx + (size_t)lidx, (long long)(depth - 1) * kHomePx);
+  };
   // pops queued rays into the lanes without one (lanes ranked by lane id)
   auto refill = [&](unsigned long long busy) {
     const int take = (64 - __popcll(busy)) < qn ? (64 - __popcll(busy)) : qn;
@@ -738,10 +785,12 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
                                   work, c_shadow, outcome, color, refl, no, nd, nkey);
     const unsigned sidx = pix + ca.fpx;
     bool defer = false;
+    if (home < 0 && __ballot(act && outcome == kSpawned))
+      home = home_acquire(kernarg_late<true, offsetof(RenderArgs, home_bits)>(a.home_bits),
+                          kernarg_late<true, offsetof(RenderArgs, home_words)>(a.home_words));
     if (act) {
       if (outcome == kSpawned) {
-        ca.gstack[RT_CK(kCkStack, sidx + (unsigned)lev * sstride, (long long)(depth - 1) * sstride)] =
-            StackEnt{color.x, color.y, color.z, refl};
+        hs()[hslot(lev)] = StackEnt{color.x, color.y, color.z, refl};
         ++lev;
         o = no;
         d = nd;
@@ -753,7 +802,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         D3 res = color;
         while (lev > 0) {
           --lev;
-          const StackEnt e = ca.gstack[RT_CK(kCkStack, sidx + (unsigned)lev * sstride, (long long)(depth - 1) * sstride)];
+          const StackEnt e = hs()[hslot(lev)];
           res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
         }
         {
@@ -781,8 +830,13 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
         if (defer && slot < (unsigned long long)cap) {
           QRay *dq = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq);
           const unsigned wg = blockIdx.x;
-          dq[RT_CK(kCkDeferQ, (size_t)(wg % kShards) * (size_t)cap + slot, (long long)kShards * cap)] =
-              QRay{o.x, o.y, o.z, d.x, d.y, d.z, lev, dleft, key, (int)sidx};
+          const size_t gslot = RT_CK(kCkDeferQ, (size_t)(wg % kShards) * (size_t)cap + slot, (long long)kShards * cap);
+          dq[gslot] = QRay{o.x, o.y, o.z, d.x, d.y, d.z, lev, dleft, key, (int)sidx};
+          // its stack entries so far go with it: render_deferred continues the chain at its queue slot
+          StackEnt *ds = kernarg_late<true, offsetof(RenderArgs, dstack)>(a.dstack);
+          const size_t dtot = (size_t)kShards * (size_t)cap;
+          for (int l = 0; l < lev; ++l)
+            ds[RT_CK(kCkStack, (size_t)l * dtot + gslot, (long long)(depth - 1) * (long long)dtot)] = hs()[hslot(l)];
           act = false;
         }
       }
@@ -823,6 +877,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
       }
     }
   }
+  if (home >= 0) home_release(kernarg_late<true, offsetof(RenderArgs, home_bits)>(a.home_bits), home);
   sums[0] += wave_sum(c_prim);
   sums[1] += wave_sum(c_shadow);
   sums[2] += wave_sum(c_reflect);
@@ -994,8 +1049,9 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
 // workgroup b serves shard segment b % kShards and takes its chunks of 64
 // rays b / kShards, + gridDim / kShards, ...  Each lane runs its ray's chain
 // to the end exactly as merge_tiles would have (bounce, stack entries at its
-// pixel's [level][pixel] slots), unwinds the pixel's whole stack -- the
-// levels merge_tiles wrote first -- and stores the pixel.
+// queue slot's [level][slot] entries of dstack), unwinds the chain's whole
+// stack -- the levels merge_tiles copied there at the deferral first -- and
+// stores the pixel.
 template <bool kCull, bool kFast = false>
 __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const RenderArgs a) {
   const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards;
@@ -1005,7 +1061,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
   if (first * 64u >= n_dq) return;
   const int lane = (int)(threadIdx.x & 63);
   const unsigned npx_frame = (unsigned)((size_t)a.rows.count * a.od.xw);
-  const unsigned sstride = npx_frame * (unsigned)a.frames;
+  const unsigned sstride = (unsigned)kShards * (unsigned)cap;  // the chain's stack: dstack[level][queue slot]
   Work work;
   unsigned c_shadow = 0, c_reflect = 0, c_neg = 0;
   // Lanes without a ray take the shard segment's next entries (one
@@ -1016,7 +1072,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
   bool act = false, more = true;
   D3 o = mk(0.0, 0.0, 0.0), d = o;
   int key = -1, dleft = 0, lev = 0;
-  unsigned pixg = 0;
+  unsigned pixg = 0, qslot = 0;  // the ray's output pixel (launch index) and queue slot
   unsigned long long *fetch = kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters) +
                               (size_t)shard * kShardStride + kFetchSlot;
   while (true) {
@@ -1036,6 +1092,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
         dleft = e.dleft;
         key = e.key;
         pixg = (unsigned)e.pix;
+        qslot = shard * (unsigned)cap + (unsigned)i;
         act = true;
       }
     }
@@ -1047,9 +1104,9 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
       bounce<kCull, true, kFast>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft,
                           work, c_shadow, outcome, color, refl, no, nd, nkey);
       if (act) {
-        StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, gstack)>(a.gstack);
+        StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, dstack)>(a.dstack);
         if (outcome == kSpawned) {
-          gs[RT_CK(kCkStack, pixg + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)] =
+          gs[RT_CK(kCkStack, qslot + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)] =
               StackEnt{color.x, color.y, color.z, refl};
           ++lev;
           o = no;
@@ -1061,7 +1118,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
           D3 res = color;
           while (lev > 0) {  // main.cpp:54, innermost first
             --lev;
-            const StackEnt e = gs[RT_CK(kCkStack, pixg + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)];
+            const StackEnt e = gs[RT_CK(kCkStack, qslot + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)];
             res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
           }
           const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
@@ -1101,7 +1158,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
   if (first * 64u >= n_dq) return;
   const int lane = (int)(threadIdx.x & 63);
   const unsigned npx_frame = (unsigned)((size_t)a.rows.count * a.od.xw);
-  const unsigned sstride = npx_frame * (unsigned)a.frames;
+  const unsigned sstride = (unsigned)kShards * (unsigned)cap;  // the chain's stack: dstack[level][queue slot]
   Work work;
   unsigned c_shadow = 0, c_reflect = 0, c_neg = 0;
   const unsigned long long lt = (1ull << lane) - 1ull;
@@ -1110,7 +1167,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
                               (size_t)shard * kShardStride + kFetchSlot;  // as render_deferred
   D3 o = mk(0.0, 0.0, 0.0), d = o;
   int key = -1, dleft = 0, lev = 0;
-  unsigned pixg = 0;
+  unsigned pixg = 0, qslot = 0;  // the ray's output pixel (launch index) and queue slot
   // the walk of this lane's ray: pending reference and stack depth, the best
   // hit so far (t, numerator, sphere) and the fp32 prune bound
   int ref = 0, sp = 0, bi = -1;
@@ -1142,6 +1199,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
           dleft = e.dleft;
           key = e.key;
           pixg = (unsigned)e.pix;
+          qslot = shard * (unsigned)cap + (unsigned)i;
           act = true;
           begin(kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv));
         }
@@ -1186,9 +1244,9 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
                                    dleft, bi, bt, work, c_shadow, outcome, color, refl, no, nd, nkey);
       bool spawned = false;
       if (ready) {
-        StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, gstack)>(a.gstack);
+        StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, dstack)>(a.dstack);
         if (outcome == kSpawned) {
-          gs[RT_CK(kCkStack, pixg + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)] =
+          gs[RT_CK(kCkStack, qslot + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)] =
               StackEnt{color.x, color.y, color.z, refl};
           ++lev;
           o = no;
@@ -1201,7 +1259,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
           D3 res = color;
           while (lev > 0) {  // main.cpp:54, innermost first
             --lev;
-            const StackEnt e = gs[RT_CK(kCkStack, pixg + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)];
+            const StackEnt e = gs[RT_CK(kCkStack, qslot + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)];
             res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
           }
           const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
@@ -1384,28 +1442,37 @@ __global__ __launch_bounds__(256) void cg_sort_kernel(const CgBuild a) {
 }
 
 // ---------------------------------------------------------------------------
-// The sphere grids (build_sphere_grids, rt_lightgrid.cpp) built on the device
-// at upload: one cube-map grid per reflective sphere s, seen from the ball
-// B(C_s, rho_s) that holds the origins of the reflection rays leaving s
-// (main.cpp:46), with the camera grid's per-lane disk / block / tile / cell
-// tests (rt_cgbuild.h, cg_view with rho) and the host builder's CSR layout:
-// grid s's cell c is ent[start[s (6N^2 + 1) + c] .. start[... + c + 1]),
-// entries (sphere, tlo bits) ascending by (tlo, index).  Grids go through in
+// Point grids built on the device at upload: the sphere grids
+// (build_sphere_grids, rt_lightgrid.cpp) -- one cube-map grid per reflective
+// sphere s, seen from the ball B(C_s, rho_s) that holds the origins of the
+// reflection rays leaving s (main.cpp:46), both disks of every sphere, the
+// spheres within reach of the ball (global) on every list, entries (sphere,
+// tlo) ascending by (tlo, index) -- and the light grids (build_light_grid)
+// -- one grid per light, seen from the light (rho = 0), the disk ahead only,
+// global spheres on a separate list (the grid's slot `cells`), ids
+// ascending.  The camera grid's per-lane disk / block / tile / cell tests
+// (rt_cgbuild.h) and the host builders' CSR layouts.  Grids go through in
 // batches (their disks and pair lists are scratch); passes:
-//   sg_disk_kernel   a wave per (grid, sphere): its disks and (disk, block) pairs
-//                    (pairs past maxp and global spheres counted per grid; the
-//                    host refuses a grid with more than kSgMaxGlobal globals or
-//                    dropped pairs, as build_sphere_grids refuses it)
-//   sg_bin_kernel    a wave per quarter pair, as cg_bin_kernel: <count> adds
+//   pg_disk_kernel   a wave per (grid, sphere): its disks and (disk, block)
+//                    pairs (pairs past maxp and global spheres counted per
+//                    grid: the host refuses a sphere grid with more than
+//                    kSgMaxGlobal globals or dropped pairs, as
+//                    build_sphere_grids refuses it); a light grid's global
+//                    sphere goes to its global list (counted, then filled)
+//   pg_bin_kernel    a wave per quarter pair, as cg_bin_kernel: <count> adds
 //                    1 per listed cell, <fill> takes a slot there and writes
 //                    the entry at the cell's CSR offset
 //   scan_*           the exclusive prefix of the counts (CSR offsets)
-//   sg_sort_kernel   a thread per cell: (tlo, index) order
+//   sg_sort_kernel / ids_sort_kernel   a thread per list: (tlo, index) / index order
+//   sg_start_kernel / lg_start_kernel  the host builders' start arrays
+struct GridPt {  // a grid's point and origin-ball radius
+  double x, y, z, rho;
+};
 struct SgBuild {
   const SphGeo *geo;
   const double *rad;
-  const double *rho;     // [n] origin-ball radius per sphere (< 0: no grid)
-  const int *gsph;       // [ng] the batch's grid spheres
+  const GridPt *pts;             // [ng] the batch's grids
+  const unsigned char *allglob;  // [ng] or nullptr: 1 = every sphere global (a non-finite light)
   const CubePatch *faces, *blocks, *tiles;
   const double *cell_cbsb;
   CgDisk *disks;         // [ng][n][2]
@@ -1413,26 +1480,49 @@ struct SgBuild {
   unsigned *npairs;      // [ng * 16]: pairs per grid (one 64-B line each)
   unsigned *nglob;       // [ng * 16]: global spheres per grid
   const unsigned *woff;  // [ng + 1]: work items (4 per kept pair) before grid j; refused grids have none
-  int *cnt;              // [ng][cells] (count pass: list lengths; fill pass: slots taken)
-  const int *off;        // [(g0 + j) cells + c]: the CSR offset of the batch's grid j's cell c
-  int2 *ent;
+  int *cnt;              // [ng][row] (count pass: list lengths; fill pass: slots taken)
+  const int *off;        // [(g0 + j) row + c]: the CSR offset of the batch's grid j's list c
+  int2 *ent;             // sphere grids: (sphere, tlo bits)
+  int32_t *ids;          // light grids: sphere ids
   long long nent;        // entries of all grids (the fill pass's bound)
   int n, ng, g0, N, NT, NB, maxp;
+  int row;               // lists per grid: 6 N^2 cells (+ 1 global list: light grids)
+  int sides;             // 2: both disks (sphere grids), 1: the disk ahead (light grids)
+  int globlist;          // 1: global spheres on the grid's list `row - 1`, not in every cell
+  int fill;              // the pass: 0 count, 1 fill
   double diam;
 };
 static_assert(sizeof(SgBuild) <= 4096, "SgBuild exceeds the kernel-argument segment");
 constexpr int kSgCntStride = 16;
 
-__global__ __launch_bounds__(256) void sg_disk_kernel(const SgBuild a) {
+// a list entry: at the CSR offset of list ci (batch-local) plus its slot
+__device__ __forceinline__ void pg_put(const SgBuild &a, long long ci, int slot, int s, float tlo) {
+  const long long e = RT_CK(kCkCgBuild, (long long)a.off[(long long)a.g0 * a.row + ci] + slot, a.nent);
+  if (a.ids)
+    a.ids[e] = s;
+  else
+    a.ent[e] = make_int2(s, __float_as_int(tlo));
+}
+
+__global__ __launch_bounds__(256) void pg_disk_kernel(const SgBuild a) {
   const int t = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6), lane = (int)(threadIdx.x & 63);
   if (t >= a.n * a.ng) return;
   const int j = t / a.n, i = t - j * a.n;
-  const int gs = a.gsph[j];
-  const SphGeo P = a.geo[RT_CK(kCkCgBuild, gs, a.n)], sp = a.geo[i];
-  const CgView v = cg_view(sp.cx, sp.cy, sp.cz, a.rad[i], P.cx, P.cy, P.cz, a.diam, a.rho[gs]);
-  if (v.global && lane == 0) atomicAdd(&a.nglob[j * kSgCntStride], 1u);
+  const GridPt P = a.pts[j];
+  const SphGeo sp = a.geo[i];
+  CgView v = cg_view(sp.cx, sp.cy, sp.cz, a.rad[i], P.x, P.y, P.z, a.diam, P.rho);
+  if (a.allglob && a.allglob[j]) v = cg_view(0.0, 0.0, 0.0, __builtin_inf(), 0.0, 0.0, 0.0, 0.0);  // global
+  if (v.global && lane == 0) {
+    atomicAdd(&a.nglob[j * kSgCntStride], 1u);
+    if (a.globlist) {  // the grid's global list
+      const long long ci = RT_CK(kCkCgBuild, (long long)j * a.row + a.row - 1, (long long)a.ng * a.row);
+      const int slot = atomicAdd(&a.cnt[ci], 1);
+      if (a.fill) pg_put(a, ci, slot, i, -__builtin_inff());
+    }
+  }
+  if (v.global && a.globlist) return;
   const int nb = 6 * a.NB * a.NB;
-  for (int side = 0; side < (v.global ? 1 : 2); ++side) {
+  for (int side = 0; side < (v.global ? 1 : a.sides); ++side) {
     const CgDisk k = cg_side(v, side, i);
     const int di = 2 * t + side;
     if (lane == 0) a.disks[RT_CK(kCkCgBuild, di, 2LL * a.n * a.ng)] = k;
@@ -1451,10 +1541,8 @@ __global__ __launch_bounds__(256) void sg_disk_kernel(const SgBuild a) {
   }
 }
 
-template <bool kFill>
-__global__ __launch_bounds__(64) void sg_bin_kernel(const SgBuild a) {
+__global__ __launch_bounds__(64) void pg_bin_kernel(const SgBuild a) {
   const int lane = (int)(threadIdx.x & 63);
-  const long long cells = 6LL * a.N * a.N;
   const unsigned total = a.woff[a.ng];
   for (unsigned v = blockIdx.x; v < total; v += gridDim.x) {
     int lo = 0, hi = a.ng;  // the grid of work item v: woff[j] <= v < woff[j + 1]
@@ -1478,11 +1566,9 @@ __global__ __launch_bounds__(64) void sg_bin_kernel(const SgBuild a) {
       tmask &= tmask - 1;
       const int gc = cg_cell(k, wide, a.cell_cbsb, a.N, f, bi, bj, tl, lane, (imask >> tl) & 1ull);
       if (gc >= 0) {
-        const long long ci = RT_CK(kCkCgBuild, (long long)j * cells + gc, a.ng * cells);
+        const long long ci = RT_CK(kCkCgBuild, (long long)j * a.row + gc, (long long)a.ng * a.row);
         const int slot = atomicAdd(&a.cnt[ci], 1);
-        if (kFill)
-          a.ent[RT_CK(kCkCgBuild, (long long)a.off[(long long)a.g0 * cells + ci] + slot, a.nent)] =
-              make_int2(k.s, __float_as_int(k.tlo));
+        if (a.fill) pg_put(a, ci, slot, k.s, k.tlo);
       }
     }
   }
@@ -1565,6 +1651,32 @@ __global__ __launch_bounds__(256) void sg_start_kernel(const int *gidx, const un
   const long long c = k - (long long)s * row;
   const int j = gidx[s];
   start[k] = (j >= 0 && ok[j]) ? off[(long long)j * cells + c] : 0;
+}
+
+// A light grid's start row (build_light_grid: stride 6N^2 + 2, the global
+// list last): the CSR offsets of its 6N^2 + 1 lists and their end.
+__global__ __launch_bounds__(256) void lg_start_kernel(const int *off, int nl, long long cells, int *start) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x, row = cells + 2;
+  if (k >= (long long)nl * row) return;
+  const long long l = k / row, c = k - l * row;
+  start[k] = off[l * (cells + 1) + c];  // c = cells + 1: the next light's first offset (or the total)
+}
+
+// A thread per list: ascending ids (insertion sort).
+__global__ __launch_bounds__(256) void ids_sort_kernel(const int *off, long long nlists, int32_t *ids) {
+  const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gc >= nlists) return;
+  int32_t *e = ids + off[gc];
+  const int cnt = off[gc + 1] - off[gc];
+  for (int k = 1; k < cnt; ++k) {
+    const int32_t x = e[k];
+    int m = k - 1;
+    while (m >= 0 && e[m] > x) {
+      e[m + 1] = e[m];
+      --m;
+    }
+    e[m + 1] = x;
+  }
 }
 
 // A thread per cell of every grid: its list in (tlo, index) order (insertion sort).
@@ -1657,6 +1769,7 @@ struct rt_ctx {
   size_t sg_entries = 0;
   double sg_build_ms = 0.0;
   double bvh_build_ms = 0.0, lg_build_ms = 0.0;  // rt_upload_scene's host builds (rt_info)
+  int nsph_up = 0;  // spheres of the scene being uploaded (the device grid builders)
   // behind grid (rt_bvh.h build_ugrid): the backward half of the ordered
   // walks' closest-hit lines (rt_device.h behind_cells), built at upload
   int ug_mode = -1;  // RT_HIP_BEHIND_GRID: -1 auto (scenes above kBvhAlwaysAbove spheres), 0 off, 1 on
@@ -1717,7 +1830,17 @@ struct rt_ctx {
   int merge_q = 64;           // kStackMerge: the launch's LDS queue entries per wave (launch_render4 picks it)
   int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (8, 16, 32 or 64)
   int defer_level = kDeferLevel;  // RT_HIP_DEFER_LEVEL (>= 1)
-  QRay *dq_buf = nullptr;     // its queue, grow-only
+  int defer_div = RT_DEFER_CAP_DIV;  // RT_HIP_DEFER_DIV (tuning build): queue room = launch pixels / defer_div
+  QRay *dq_buf = nullptr;     // its queue (and its slots' stacks), grow-only
+  // kStackMerge: the merged waves' stack homes (merge_tiles, home_acquire),
+  // twice as many as the render kernel can have resident, and their bitmap
+  StackEnt *d_homes = nullptr;
+  size_t homes_bytes = 0;
+  unsigned long long *d_home_bits = nullptr;
+  int home_words = 0;
+  const void *occ_kernel = nullptr;  // the occupancy of the last kernel asked (blocks per CU at occ_lds)
+  size_t occ_lds = 0;
+  int occ_blocks = 0;
   size_t dq_bytes = 0;
   // frames of the launch being enqueued (rt_render_frames_async; 1 otherwise) and their cameras
   int nframes = 1;
@@ -1754,9 +1877,11 @@ struct rt_ctx {
   // share their reflection rays' passes (class >= 1 there: 0.2285 -> 0.2364 ms
   // per frame, profiles/r3c/ab_single.log)
   int single_class = -1;
-  // RT_HIP_TAIL: multi-frame launches give their last tiles (the lightest, about
-  // one per wave slot of the chip) a wave each (merge_end); 0: four per wave to the end
+  // RT_HIP_TAIL: launches give their last tiles (the lightest, about one per
+  // wave slot of the chip: tail_waves per CU over the frames) a wave each
+  // (merge_end); 0: four per wave to the end.  RT_HIP_TAIL_WAVES (tuning build)
   int tail = 1;
+  int tail_waves = 12;
   // RT_HIP_XCD_FRAMES: multi-frame launches put every frame of a tile group on
   // one XCD (render_kernel).  -1 (default): for scenes with the uniform grid
   // (large scenes, whose lists and nodes outgrow an XCD's L2: synth10k 2.58 ->
@@ -2149,11 +2274,6 @@ constexpr int kSgMaxSpheres = 2048;     // RT_HIP_SPHERE_GRID=-1: larger scenes 
 constexpr int kSgMaxGlobal = 32;        // spheres overlapping an origin ball (on every list of its grid)
 constexpr size_t kSgMaxEntries = size_t(256) << 20;  // 2 GiB of lists (built on the device)
 
-// Sphere grids for the reflective spheres of the scene being uploaded (the
-// origins of reflection rays, main.cpp:46, lie within |r| + 0.001 of their
-// sphere's centre up to the rounding of the hit point; the ball is grown by a
-// relative 1e-6 and the device checks every ray against it).  No grids (and
-// RT_OK) when disabled, too large, or refused.
 // device scratch of one upload-time build, freed on every exit path
 struct DevScratch {
   std::vector<void *> p;
@@ -2189,44 +2309,24 @@ int device_scan(rt_ctx *c, const int *x, long long n, int *y, long long &total) 
   return RT_OK;
 }
 
-// Sphere grids for the reflective spheres of the scene being uploaded (the
-// origins of reflection rays, main.cpp:46, lie within |r| + 0.001 of their
-// sphere's centre up to the rounding of the hit point; the ball is grown by a
-// relative 1e-6 and the device checks every ray against it), built on the
-// device (sg_*_kernel; the geometry is on the device already).  No grids (and
-// RT_OK) when disabled, too large, or refused.
-int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
-  const int n = s->num_spheres;
-  if (c->sg_mode == 0 || (c->sg_mode < 0 && n > kSgMaxSpheres) || n == 0 || !std::isfinite(diam)) return RT_OK;
-  const auto t0 = std::chrono::steady_clock::now();
-  std::vector<double> rho((size_t)n, -1.0);
-  std::vector<int> gsph, gidx((size_t)n, -1);
-  for (int i = 0; i < n; i++) {
-    const rt_sphere &sp = s->spheres[i];
-    const double r = std::fabs(sp.radius);
-    const double mag = std::fabs(sp.center[0]) + std::fabs(sp.center[1]) + std::fabs(sp.center[2]);
-    if (sp.reflectivity > 0.0 && std::isfinite(r) && std::isfinite(mag))  // main.cpp:43
-      rho[(size_t)i] = (r + kEps) * (1.0 + 1e-6) + 1e-12 * mag + 1e-9 * diam;
-    if (rho[(size_t)i] >= 0.0 && std::isfinite(rho[(size_t)i])) {  // (build_sphere_grids: a finite ball)
-      gidx[(size_t)i] = (int)gsph.size();
-      gsph.push_back(i);
-    }
-  }
-  const int N = c->sg_n_opt ? c->sg_n_opt : (n <= kSgFineSpheres ? kSgNFine : kSgN);
-  // the device indexes grid key's starts at key * (6 N^2 + 1) in 32 bits, and
-  // every sphere has its row of starts: refuse grids that would overflow it
-  // or hold more than 1 GiB of starts
-  const long long cells = 6LL * N * N;
-  const size_t nstart = (size_t)n * (size_t)(cells + 1);
-  if (nstart > (size_t)INT32_MAX || nstart * sizeof(int32_t) > ((size_t)1 << 30)) return RT_OK;
-  const int ng = (int)gsph.size();
-  c->sg_grids = 0;
-  c->sg_entries = 0;
-  if (ng == 0) {
-    c->sg_build_ms = ms_since(t0);
-    return RT_OK;
-  }
-  if ((long long)ng * cells >= INT32_MAX) return RT_OK;  // 32-bit CSR offsets
+// Point grids on the device (pg_*_kernel passes) for the grids `pts`, each
+// with N cells per cube-map face edge: per grid ok (sphere grids: refused past
+// max_global global spheres or dropped pairs; light grids: never), the CSR
+// offsets of the ng x row lists (device, ng * row + 1 ints, held by `keep`)
+// and the entries (`out`: int2 (sphere, tlo) or, for light grids, int ids;
+// the caller owns it; nullptr when the lists would exceed max_entries).
+struct PgMode {
+  int sides, globlist, max_global;
+  size_t max_entries;
+};
+int point_grids(rt_ctx *c, const std::vector<GridPt> &pts, const std::vector<unsigned char> &allglob, double diam,
+                int N, const PgMode &md, DevScratch &keep, int *&d_off, std::vector<unsigned char> &ok,
+                long long &total, void *&out) {
+  const int n = c->nsph_up, ng = (int)pts.size();
+  const long long cells = 6LL * N * N, row = cells + (md.globlist ? 1 : 0);
+  out = nullptr;
+  total = 0;
+  ok.assign((size_t)ng, 0);
   rt_ctx::CgTables tab;
   int rc = upload_tables(c, N, tab);
   struct TabGuard {
@@ -2235,39 +2335,38 @@ int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
   } tab_guard{tab};
   if (rc != RT_OK) return rc;
   const long long nblocks = 6LL * tab.NB * tab.NB;
-  // pairs kept per grid (a grid with more is refused, as one past the host
-  // builder's entry cap); grids in batches whose disks and pairs fit kSgScratch
-  constexpr size_t kSgScratch = size_t(128) << 20;
-  const long long maxp = std::min<long long>(2LL * n * nblocks, 1 << 22);
+  // pairs kept per grid (past it a sphere grid is refused, as one past the
+  // host builder's entry cap; a light grid keeps every pair); grids in batches
+  // whose disks and pairs fit kPgScratch
+  constexpr size_t kPgScratch = size_t(128) << 20;
+  const long long worst = (long long)md.sides * n * nblocks;
+  const long long maxp = std::max(1LL, md.globlist ? worst : std::min<long long>(worst, 1 << 22));
   const size_t per_grid = 2 * (size_t)n * sizeof(CgDisk) + (size_t)maxp * sizeof(int2);
   const int batch = (int)std::max<long long>(
-      1, std::min<long long>({(long long)ng, (long long)(kSgScratch / per_grid),
+      1, std::min<long long>({(long long)ng, (long long)(kPgScratch / per_grid),
                               (long long)(((1ull << 32) - 1) / (4ull * (unsigned long long)maxp))}));
+  if (4ull * (unsigned long long)maxp >= (1ull << 32)) return RT_OK;  // a grid's work items past 32 bits: none
   DevScratch sc;
-  double *d_rho = nullptr;
-  int *d_gsph = nullptr, *d_gidx = nullptr, *d_cnt = nullptr, *d_off = nullptr;
-  unsigned char *d_ok = nullptr;
+  GridPt *d_pts = nullptr;
+  unsigned char *d_ag = nullptr;
+  int *d_cnt = nullptr;
   CgDisk *d_disks = nullptr;
   int2 *d_pairs = nullptr;
   unsigned *d_np = nullptr, *d_woff = nullptr;
-  RT_TRY(c, sc.alloc(d_rho, sizeof(double) * (size_t)n));
-  RT_TRY(c, sc.alloc(d_gsph, sizeof(int) * (size_t)ng));
-  RT_TRY(c, sc.alloc(d_gidx, sizeof(int) * (size_t)n));
-  RT_TRY(c, sc.alloc(d_ok, (size_t)ng));
-  RT_TRY(c, sc.alloc(d_cnt, sizeof(int) * (size_t)(ng * cells)));
-  RT_TRY(c, sc.alloc(d_off, sizeof(int) * (size_t)(ng * cells + 1)));
-  RT_TRY(c, sc.alloc(d_disks, 2 * (size_t)n * batch * sizeof(CgDisk)));
+  RT_TRY(c, sc.alloc(d_pts, sizeof(GridPt) * (size_t)ng));
+  RT_TRY(c, sc.alloc(d_ag, (size_t)ng));
+  RT_TRY(c, sc.alloc(d_cnt, sizeof(int) * (size_t)(ng * row)));
+  RT_TRY(c, keep.alloc(d_off, sizeof(int) * (size_t)(ng * row + 1)));
+  RT_TRY(c, sc.alloc(d_disks, 2 * (size_t)std::max(n, 1) * batch * sizeof(CgDisk)));
   RT_TRY(c, sc.alloc(d_pairs, (size_t)maxp * batch * sizeof(int2)));
   RT_TRY(c, sc.alloc(d_np, 2 * sizeof(unsigned) * kSgCntStride * (size_t)batch));
   RT_TRY(c, sc.alloc(d_woff, sizeof(unsigned) * (size_t)(batch + 1)));
-  RT_TRY(c, hipMemcpy(d_rho, rho.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
-  RT_TRY(c, hipMemcpy(d_gsph, gsph.data(), sizeof(int) * (size_t)ng, hipMemcpyHostToDevice));
-  RT_TRY(c, hipMemcpy(d_gidx, gidx.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice));
-  RT_TRY(c, hipMemsetAsync(d_cnt, 0, sizeof(int) * (size_t)(ng * cells), c->stream));
+  RT_TRY(c, hipMemcpy(d_pts, pts.data(), sizeof(GridPt) * (size_t)ng, hipMemcpyHostToDevice));
+  RT_TRY(c, hipMemcpy(d_ag, allglob.data(), (size_t)ng, hipMemcpyHostToDevice));
+  RT_TRY(c, hipMemsetAsync(d_cnt, 0, sizeof(int) * (size_t)(ng * row), c->stream));
   SgBuild b{};
   b.geo = c->d_geo;
   b.rad = c->d_rad;
-  b.rho = d_rho;
   b.faces = tab.faces;
   b.blocks = tab.blocks;
   b.tiles = tab.tiles;
@@ -2283,20 +2382,24 @@ int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
   b.NT = tab.NT;
   b.NB = tab.NB;
   b.maxp = (int)maxp;
+  b.row = (int)row;
+  b.sides = md.sides;
+  b.globlist = md.globlist;
   b.diam = diam;
-  std::vector<unsigned char> ok((size_t)ng, 0);
   std::vector<std::vector<unsigned>> woffs;
-  // one batch of grids: disks and pairs (pass 1), and on the count pass the
-  // grids' refusals and work offsets; then the bin pass (count or fill)
+  // one batch of grids: disks and pairs (pass 1) -- and, counting, the
+  // grids' refusals and work offsets -- then the bin pass
   auto run_batch = [&](int g0, bool fill) -> int {
     const int nbg = std::min(batch, ng - g0);
-    b.gsph = d_gsph + g0;
+    b.pts = d_pts + g0;
+    b.allglob = d_ag + g0;
     b.ng = nbg;
     b.g0 = g0;
-    b.cnt = d_cnt + (size_t)g0 * cells;
+    b.cnt = d_cnt + (size_t)g0 * row;
+    b.fill = fill ? 1 : 0;
     RT_TRY(c, hipMemsetAsync(d_np, 0, 2 * sizeof(unsigned) * kSgCntStride * (size_t)batch, c->stream));
     const long long waves = (long long)n * nbg;
-    hipLaunchKernelGGL(sg_disk_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, c->stream, b);
+    if (waves > 0) hipLaunchKernelGGL(pg_disk_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, c->stream, b);
     RT_TRY(c, hipGetLastError());
     if (!fill) {
       std::vector<unsigned> hn(2 * kSgCntStride * (size_t)batch);
@@ -2305,7 +2408,7 @@ int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
       std::vector<unsigned> wo((size_t)nbg + 1, 0);
       for (int j = 0; j < nbg; j++) {
         const unsigned np = hn[(size_t)j * kSgCntStride], nglob = hn[((size_t)batch + j) * kSgCntStride];
-        const bool g_ok = nglob <= (unsigned)kSgMaxGlobal && np <= (unsigned)maxp;
+        const bool g_ok = nglob <= (unsigned)md.max_global && np <= (unsigned)maxp;
         ok[(size_t)(g0 + j)] = g_ok ? 1 : 0;
         wo[(size_t)j + 1] = wo[(size_t)j] + (g_ok ? 4u * np : 0u);
       }
@@ -2315,11 +2418,7 @@ int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
     RT_TRY(c, hipMemcpyAsync(d_woff, wo.data(), sizeof(unsigned) * wo.size(), hipMemcpyHostToDevice, c->stream));
     const unsigned items = wo.back();
     if (items) {
-      const dim3 grid((unsigned)std::min<unsigned>(items, 16384u));
-      if (fill)
-        hipLaunchKernelGGL(sg_bin_kernel<true>, grid, dim3(64), 0, c->stream, b);
-      else
-        hipLaunchKernelGGL(sg_bin_kernel<false>, grid, dim3(64), 0, c->stream, b);
+      hipLaunchKernelGGL(pg_bin_kernel, dim3((unsigned)std::min<unsigned>(items, 16384u)), dim3(64), 0, c->stream, b);
       RT_TRY(c, hipGetLastError());
     }
     // the host copy of the work offsets is read by the stream: wait before the next batch rewrites them
@@ -2328,40 +2427,102 @@ int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
   };
   for (int g0 = 0; g0 < ng; g0 += batch)
     if ((rc = run_batch(g0, false)) != RT_OK) return rc;
-  long long total = 0;
-  if ((rc = device_scan(c, d_cnt, (long long)ng * cells, d_off, total)) != RT_OK) return rc;
-  int grids = 0;
-  for (int j = 0; j < ng; j++) grids += ok[(size_t)j];
-  if ((size_t)total > kSgMaxEntries || grids == 0) {  // as build_sphere_grids past max_entries: no grids
+  if (md.globlist)  // a refused light grid's global list holds spheres too: keep it out of the counts
+    for (int j = 0; j < ng; j++)
+      if (!ok[(size_t)j]) return RT_OK;
+  if ((rc = device_scan(c, d_cnt, (long long)ng * row, d_off, total)) != RT_OK) return rc;
+  if ((size_t)total > md.max_entries || total > INT32_MAX) return RT_OK;
+  const size_t esz = md.globlist ? sizeof(int32_t) : sizeof(int2);
+  RT_TRY(c, hipMalloc(&out, esz * ((size_t)total + 1)));
+  b.ent = md.globlist ? nullptr : static_cast<int2 *>(out);
+  b.ids = md.globlist ? static_cast<int32_t *>(out) : nullptr;
+  b.nent = total;
+  RT_TRY(c, hipMemsetAsync(d_cnt, 0, sizeof(int) * (size_t)(ng * row), c->stream));
+  for (int g0 = 0; g0 < ng; g0 += batch)
+    if ((rc = run_batch(g0, true)) != RT_OK) return rc;
+  const long long nlists = (long long)ng * row;
+  if (md.globlist)
+    hipLaunchKernelGGL(ids_sort_kernel, dim3((unsigned)((nlists + 255) / 256)), dim3(256), 0, c->stream, d_off, nlists,
+                       b.ids);
+  else
+    hipLaunchKernelGGL(sg_sort_kernel, dim3((unsigned)((nlists + 255) / 256)), dim3(256), 0, c->stream, d_off, nlists,
+                       b.ent);
+  RT_TRY(c, hipGetLastError());
+  RT_TRY(c, hipStreamSynchronize(c->stream));  // the scratch is freed on return
+  return RT_OK;
+}
+
+// Sphere grids for the reflective spheres of the scene being uploaded (the
+// origins of reflection rays, main.cpp:46, lie within |r| + 0.001 of their
+// sphere's centre up to the rounding of the hit point; the ball is grown by a
+// relative 1e-6 and the device checks every ray against it), built on the
+// device (point_grids; the geometry is on the device already).  No grids (and
+// RT_OK) when disabled, too large, or refused.
+int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
+  const int n = s->num_spheres;
+  if (c->sg_mode == 0 || (c->sg_mode < 0 && n > kSgMaxSpheres) || n == 0 || !std::isfinite(diam)) return RT_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<double> rho((size_t)n, -1.0);
+  std::vector<int> gidx((size_t)n, -1);
+  std::vector<GridPt> pts;
+  for (int i = 0; i < n; i++) {
+    const rt_sphere &sp = s->spheres[i];
+    const double r = std::fabs(sp.radius);
+    const double mag = std::fabs(sp.center[0]) + std::fabs(sp.center[1]) + std::fabs(sp.center[2]);
+    if (sp.reflectivity > 0.0 && std::isfinite(r) && std::isfinite(mag))  // main.cpp:43
+      rho[(size_t)i] = (r + kEps) * (1.0 + 1e-6) + 1e-12 * mag + 1e-9 * diam;
+    if (rho[(size_t)i] >= 0.0 && std::isfinite(rho[(size_t)i])) {  // (build_sphere_grids: a finite ball)
+      gidx[(size_t)i] = (int)pts.size();
+      pts.push_back(GridPt{sp.center[0], sp.center[1], sp.center[2], rho[(size_t)i]});
+    }
+  }
+  const int N = c->sg_n_opt ? c->sg_n_opt : (n <= kSgFineSpheres ? kSgNFine : kSgN);
+  // the device indexes grid key's starts at key * (6 N^2 + 1) in 32 bits, and
+  // every sphere has its row of starts: refuse grids that would overflow it
+  // or hold more than 1 GiB of starts
+  const long long cells = 6LL * N * N;
+  const size_t nstart = (size_t)n * (size_t)(cells + 1);
+  if (nstart > (size_t)INT32_MAX || nstart * sizeof(int32_t) > ((size_t)1 << 30)) return RT_OK;
+  const int ng = (int)pts.size();
+  c->sg_grids = 0;
+  c->sg_entries = 0;
+  if (ng == 0 || (long long)ng * cells >= INT32_MAX) {  // (32-bit CSR offsets)
     c->sg_build_ms = ms_since(t0);
     return RT_OK;
   }
-  int2 *d_ent = nullptr;
-  int32_t *d_start = nullptr;
-  double *d_rho2 = nullptr;
-  RT_TRY(c, hipMalloc(&d_ent, sizeof(int2) * ((size_t)total + 1)));
-  c->d_sg_ent = d_ent;  // owned by the context from here (free_scene)
-  RT_TRY(c, hipMalloc(&d_start, sizeof(int32_t) * nstart));
-  c->d_sg_start = d_start;
-  RT_TRY(c, hipMalloc(&d_rho2, sizeof(double) * (size_t)n));
-  c->d_sg_rho2 = d_rho2;
-  b.ent = d_ent;
-  b.nent = total;
-  RT_TRY(c, hipMemsetAsync(d_cnt, 0, sizeof(int) * (size_t)(ng * cells), c->stream));
-  for (int g0 = 0; g0 < ng; g0 += batch)
-    if ((rc = run_batch(g0, true)) != RT_OK) return rc;
-  hipLaunchKernelGGL(sg_sort_kernel, dim3((unsigned)((ng * cells + 255) / 256)), dim3(256), 0, c->stream, d_off,
-                     (long long)(ng * cells), d_ent);
+  DevScratch keep;
+  int *d_off = nullptr;
+  std::vector<unsigned char> ok;
+  long long total = 0;
+  void *ent = nullptr;
+  int rc = point_grids(c, pts, std::vector<unsigned char>((size_t)ng, 0), diam, N,
+                       PgMode{2, 0, kSgMaxGlobal, kSgMaxEntries}, keep, d_off, ok, total, ent);
+  c->d_sg_ent = static_cast<int2 *>(ent);  // owned by the context from here (free_scene)
+  if (rc != RT_OK) return rc;
+  int grids = 0;
+  for (int j = 0; j < ng; j++) grids += ok[(size_t)j];
+  if (!ent || grids == 0) {  // as build_sphere_grids past max_entries: no grids
+    c->sg_build_ms = ms_since(t0);
+    return RT_OK;
+  }
+  DevScratch sc;
+  int *d_gidx = nullptr;
+  unsigned char *d_ok = nullptr;
+  RT_TRY(c, sc.alloc(d_gidx, sizeof(int) * (size_t)n));
+  RT_TRY(c, sc.alloc(d_ok, (size_t)ng));
+  RT_TRY(c, hipMemcpy(d_gidx, gidx.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice));
   RT_TRY(c, hipMemcpy(d_ok, ok.data(), (size_t)ng, hipMemcpyHostToDevice));
+  RT_TRY(c, hipMalloc(&c->d_sg_start, sizeof(int32_t) * nstart));
+  RT_TRY(c, hipMalloc(&c->d_sg_rho2, sizeof(double) * (size_t)n));
   hipLaunchKernelGGL(sg_start_kernel, dim3((unsigned)((nstart + 255) / 256)), dim3(256), 0, c->stream, d_gidx, d_ok,
-                     d_off, n, cells, d_start);
+                     d_off, n, cells, c->d_sg_start);
   RT_TRY(c, hipGetLastError());
   std::vector<double> rho2((size_t)n);
   for (int i = 0; i < n; i++) {
     const int j = gidx[(size_t)i];
     rho2[(size_t)i] = (j >= 0 && ok[(size_t)j]) ? rho[(size_t)i] * rho[(size_t)i] : -1.0;
   }
-  RT_TRY(c, hipMemcpy(d_rho2, rho2.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
+  RT_TRY(c, hipMemcpy(c->d_sg_rho2, rho2.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
   RT_TRY(c, hipStreamSynchronize(c->stream));  // the scratch is freed on return
   c->sg_n = N;
   c->sg_nstart = (long long)nstart;
@@ -2370,6 +2531,74 @@ int sphere_grids(rt_ctx *c, const rt_scene *s, double diam) {
   c->sg_grids = grids;
   c->sg_entries = (size_t)total;
   c->sg_build_ms = ms_since(t0);
+  return RT_OK;
+}
+
+// The per-light direction grids for shadow rays (rt_lightgrid.h
+// build_light_grid's lists and layout), built on the device (point_grids,
+// one side, global lists); the host builder when the device lists would not
+// fit 32-bit offsets.
+int light_grids(rt_ctx *c, const rt_scene *s, double diam) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int n = s->num_spheres, nl = s->num_lights, N = c->lg_n;
+  const long long cells = 6LL * N * N;
+  c->lg_max_off = std::isfinite(diam) ? 1e-7 * diam : 0.0;
+  const double dm = std::isfinite(diam) ? diam : 0.0;
+  std::vector<GridPt> pts((size_t)nl);
+  std::vector<unsigned char> allglob((size_t)nl);
+  for (int l = 0; l < nl; l++) {
+    const rt_light &L = s->lights[l];
+    pts[(size_t)l] = GridPt{L.position[0], L.position[1], L.position[2], 0.0};
+    allglob[(size_t)l] = !(std::isfinite(L.position[0]) && std::isfinite(L.position[1]) && std::isfinite(L.position[2]));
+  }
+  int32_t *ids = nullptr;
+  long long total = 0;
+  bool dev = nl > 0 && (long long)nl * (cells + 2) < INT32_MAX;
+  if (dev) {
+    DevScratch keep;
+    int *d_off = nullptr;
+    std::vector<unsigned char> ok;
+    void *out = nullptr;
+    int rc = point_grids(c, pts, allglob, dm, N, PgMode{1, 1, INT32_MAX, (size_t)INT32_MAX}, keep, d_off, ok, total,
+                         out);
+    ids = static_cast<int32_t *>(out);
+    c->d_lg_ids = ids;  // owned by the context from here (free_scene)
+    if (rc != RT_OK) return rc;
+    if (ids) {
+      const long long nstart = (long long)nl * (cells + 2);
+      RT_TRY(c, hipMalloc(&c->d_lg_start, sizeof(int32_t) * (size_t)(nstart + 1)));
+      hipLaunchKernelGGL(lg_start_kernel, dim3((unsigned)((nstart + 255) / 256)), dim3(256), 0, c->stream, d_off, nl,
+                         cells, c->d_lg_start);
+      RT_TRY(c, hipGetLastError());
+      RT_TRY(c, hipStreamSynchronize(c->stream));  // d_off is freed on return
+      c->lg_nstart = nstart;
+      c->lg_nids = total;
+    } else {
+      dev = false;
+    }
+  }
+  if (!dev) {  // no lights, or lists past 32 bits: the host builder
+    std::vector<double> lx((size_t)nl), ly((size_t)nl), lz((size_t)nl);
+    for (int l = 0; l < nl; l++) {
+      lx[(size_t)l] = s->lights[l].position[0];
+      ly[(size_t)l] = s->lights[l].position[1];
+      lz[(size_t)l] = s->lights[l].position[2];
+    }
+    std::vector<int32_t> lg_start, lg_ids;
+    build_light_grid(c->h_sx.data(), c->h_sy.data(), c->h_sz.data(), c->h_sr.data(), n, lx.data(), ly.data(),
+                     lz.data(), nl, diam, N, lg_start, lg_ids);
+    c->lg_nstart = (long long)lg_start.size();
+    c->lg_nids = (long long)lg_ids.size();
+    if (c->d_lg_ids) (void)hipFree(c->d_lg_ids);
+    c->d_lg_ids = nullptr;
+    RT_TRY(c, hipMalloc(&c->d_lg_start, sizeof(int32_t) * (lg_start.size() + 1)));
+    RT_TRY(c, hipMalloc(&c->d_lg_ids, sizeof(int32_t) * (lg_ids.size() + 1)));
+    if (!lg_start.empty())
+      RT_TRY(c, hipMemcpy(c->d_lg_start, lg_start.data(), sizeof(int32_t) * lg_start.size(), hipMemcpyHostToDevice));
+    if (!lg_ids.empty())
+      RT_TRY(c, hipMemcpy(c->d_lg_ids, lg_ids.data(), sizeof(int32_t) * lg_ids.size(), hipMemcpyHostToDevice));
+  }
+  c->lg_build_ms = ms_since(t0);
   return RT_OK;
 }
 
@@ -2491,7 +2720,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   if (kStack == kStackMerge)  // the wave's ray queue and finished pixels (merge_tiles)
     lds += (size_t)c->merge_q * sizeof(QRay) + kPixbufBytes;
   StackEnt *gstack = nullptr;
-  if (depth > 1) {
+  if (depth > 1 && kStack == kStackGlobal) {
     // the kernel indexes the stack with 32 bits: entry + level * npx < 2^32
     if ((unsigned long long)(depth - 1) * rows.count * od.xw * nf >= (1ull << 32)) return RT_ERR_INVALID_ARG;
     // grow-only: sized for this launch's frames; a later launch of as many
@@ -2520,14 +2749,18 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     int rc = tile_perm(c, cam, W, H, rows, od, 8 * kWx, 8 * kWy, ntiles, perm);
     if (rc != RT_OK) return rc;
     if (kStack == kStackMerge) {  // the heaviest classes lead the order: one wave per tile for them
-      const int sc = c->single_class >= 0 ? c->single_class : (nf == 1 ? 0 : kSchedClasses);
+      // one-frame launches: the tiles under reflective spheres (class >= 1) a
+      // wave each, the rest four per wave, the last ones (tail) single again
+      // (synth200 0.314 -> 0.298 ms, complex 0.293 -> 0.286 against every tile
+      // single, profiles/r5g/); multi-frame launches merge every class
+      const int sc = c->single_class >= 0 ? c->single_class : (nf == 1 ? 1 : kSchedClasses);
       long long heavy = 0;
       for (int k = sc; k < kSchedClasses; k++) heavy += c->perm_cls[k];
       nsingle = (int)std::min<long long>(heavy, ntiles);
       // multi-frame launches end on their lightest tiles one per wave: about
       // as many as the chip holds waves (12 per CU), over the launch's frames
-      if (c->tail && nf > 1)
-        tail = std::min<long long>(ntiles - nsingle, ((long long)c->n_cu * 12 + nf - 1) / nf);
+      if (c->tail)
+        tail = std::min<long long>(ntiles - nsingle, ((long long)c->n_cu * c->tail_waves + nf - 1) / nf);
       nslots = nsingle + (ntiles - nsingle - tail + kMergeTiles - 1) / kMergeTiles + tail;
     }
   }
@@ -2576,10 +2809,11 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.xcd_frames = xcd_frames ? 1 : 0;
   if (kStack == kStackMerge && (c->defer > 0 || (c->defer < 0 && nf > 1)) && depth > c->defer_level) {
     // room for 1/8 of the launch's pixels (deferred rays are ~2 % on synth200); a ray
-    // that finds its shard segment full simply continues in its merge_tiles lane
+    // that finds its shard segment full simply continues in its merge_tiles lane.
+    // Each queue slot has its chain's stack after the queue: [depth-1][kShards * cap]
     const size_t npx = (size_t)rows.count * od.xw * nf;
-    const size_t cap = std::max<size_t>(64, ((npx / kShards / RT_DEFER_CAP_DIV) + 63) & ~(size_t)63);
-    const size_t need = cap * kShards * sizeof(QRay);
+    const size_t cap = std::max<size_t>(64, ((npx / kShards / (size_t)c->defer_div) + 63) & ~(size_t)63);
+    const size_t need = cap * kShards * (sizeof(QRay) + (size_t)(depth - 1) * sizeof(StackEnt));
     if (c->dq_bytes < need) {
       RT_TRY(c, hipStreamSynchronize(c->stream));
       if (c->dq_buf) (void)hipFree(c->dq_buf);
@@ -2588,15 +2822,50 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       RT_TRY(c, hipMalloc(&c->dq_buf, need));
       c->dq_bytes = need;
     }
-    if (cap < (size_t)1 << 30) {
+    if (cap < (size_t)1 << 30 && (unsigned long long)cap * kShards * (unsigned)(depth - 1) < (1ull << 32)) {
       ra.dq = c->dq_buf;
       ra.dq_cap = (int)cap;
+      ra.dstack = reinterpret_cast<StackEnt *>(c->dq_buf + cap * kShards);
     }
   }
   if constexpr (kStack == kStackMerge && !kLds && kSamples == 1) {
     // the default configuration (ordered 4-wide BVH walk, light grids) has kernels
     // compiled with only those paths (kFast): no registers held for the others
     const bool fast = bv.ordered && bv.wide && lg.on;
+    if (depth > 1) {  // the stack homes: 2 x the render kernel's resident waves
+      const void *kf = fast ? reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack, true>)
+                            : reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack>);
+      if (kf != c->occ_kernel || lds != c->occ_lds) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kf, 64 * kWg, lds) != hipSuccess || nb < 1) {
+          (void)hipGetLastError();
+          nb = 32;  // the most waves a CU holds
+        }
+        c->occ_kernel = kf;
+        c->occ_lds = lds;
+        c->occ_blocks = nb;
+      }
+      const int words = (int)(((long long)2 * c->occ_blocks * kWg * c->n_cu + 63) / 64);
+      const size_t hb = (size_t)words * 64 * (size_t)(depth - 1) * kHomePx * sizeof(StackEnt);
+      if (c->homes_bytes < hb || c->home_words < words) {
+        RT_TRY(c, hipStreamSynchronize(c->stream));  // launches in flight hold homes
+        if (c->d_homes) (void)hipFree(c->d_homes);
+        if (c->d_home_bits) (void)hipFree(c->d_home_bits);
+        c->d_homes = nullptr;
+        c->d_home_bits = nullptr;
+        c->homes_bytes = 0;
+        c->home_words = 0;
+        RT_TRY(c, hipMalloc(&c->d_homes, hb));
+        RT_TRY(c, hipMalloc(&c->d_home_bits, (size_t)words * sizeof(unsigned long long)));
+        // zero once: every wave returns the home it took, so a drained launch leaves the bitmap zero
+        RT_TRY(c, hipMemset(c->d_home_bits, 0, (size_t)words * sizeof(unsigned long long)));
+        c->homes_bytes = hb;
+        c->home_words = words;
+      }
+      ra.homes = c->d_homes;
+      ra.home_bits = c->d_home_bits;
+      ra.home_words = c->home_words;
+    }
     // the camera grids' host part (policy, tables, buffers) first; the
     // launch's timing starts after it: the grids' device passes ahead of the
     // render kernel are part of the launch
@@ -2775,6 +3044,8 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_GRID_CLOSEST")) c->ug_closest = std::atoi(e) != 0 ? 1 : 0;  // (see ug_closest)
   if (const char *e = std::getenv("RT_HIP_XCD_FRAMES")) c->xcd_frames = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_TAIL")) c->tail = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_TAIL_WAVES")) c->tail_waves = std::max(1, std::min(64, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_DEFER_DIV")) c->defer_div = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_GRID_CELLS")) c->ug_cells = std::max(0.05, std::min(64.0, std::atof(e)));
   if (const char *e = std::getenv("RT_HIP_SINGLE_CLASS"))
     c->single_class = std::max(0, std::min(kSchedClasses, std::atoi(e)));
@@ -2821,6 +3092,8 @@ void rt_destroy(rt_ctx *c) {
   if (c->d_tmp) (void)hipFree(c->d_tmp);
   if (c->cstack_buf) (void)hipFree(c->cstack_buf);
   if (c->dq_buf) (void)hipFree(c->dq_buf);
+  if (c->d_homes) (void)hipFree(c->d_homes);
+  if (c->d_home_bits) (void)hipFree(c->d_home_bits);
   if (c->d_perm) (void)hipFree(c->d_perm);
   if (c->h_perm) (void)hipHostFree(c->h_perm);
   if (c->d_bperm) (void)hipFree(c->d_bperm);
@@ -3013,43 +3286,16 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
     double d2 = 0.0;
     for (int k = 0; k < 3; k++) d2 += (hi[k] - lo[k]) * (hi[k] - lo[k]);
     const double diam = n + nl > 0 ? std::sqrt(d2) : 0.0;
-    std::vector<double> sx(n), sy(n), sz(n), lx(nl), ly(nl), lz(nl);
+    std::vector<double> sx(n), sy(n), sz(n);
     for (int i = 0; i < n; i++) {
       sx[i] = s->spheres[i].center[0];
       sy[i] = s->spheres[i].center[1];
       sz[i] = s->spheres[i].center[2];
     }
-    for (int i = 0; i < nl; i++) {
-      lx[i] = s->lights[i].position[0];
-      ly[i] = s->lights[i].position[1];
-      lz[i] = s->lights[i].position[2];
-    }
-    const auto t_lg = std::chrono::steady_clock::now();
-    std::vector<int32_t> lg_start, lg_ids;
-    build_light_grid(sx.data(), sy.data(), sz.data(), br.data(), n, lx.data(), ly.data(), lz.data(), nl, diam,
-                     c->lg_n, lg_start, lg_ids);
-    c->lg_max_off = std::isfinite(diam) ? 1e-7 * diam : 0.0;
-    c->lg_nstart = (long long)lg_start.size();
-    c->lg_nids = (long long)lg_ids.size();
     c->h_sx = sx;
     c->h_sy = sy;
     c->h_sz = sz;
     c->h_sr = br;
-    if ((e = hipMalloc(&c->d_lg_start, sizeof(int32_t) * (lg_start.size() + 1))) != hipSuccess ||
-        (e = hipMalloc(&c->d_lg_ids, sizeof(int32_t) * (lg_ids.size() + 1))) != hipSuccess ||
-        (!lg_start.empty() && (e = hipMemcpy(c->d_lg_start, lg_start.data(), sizeof(int32_t) * lg_start.size(),
-                                             hipMemcpyHostToDevice)) != hipSuccess) ||
-        (!lg_ids.empty() && (e = hipMemcpy(c->d_lg_ids, lg_ids.data(), sizeof(int32_t) * lg_ids.size(),
-                                           hipMemcpyHostToDevice)) != hipSuccess)) {
-      rc = fail(c, e, "rt_upload_scene(light grid)");
-      free_scene(c);
-      delete[] hg;
-      delete[] hr;
-      delete[] hm;
-      delete[] hl;
-      return rc;
-    }
-    c->lg_build_ms = ms_since(t_lg);
     scene_diam = diam;
   }
   for (int k = 0; k < 3; k++) {
@@ -3068,7 +3314,8 @@ int rt_upload_scene(rt_ctx *c, const rt_scene *s) {
       (e = hipMemcpy(c->d_lights, hl, sizeof(LightD) * nl, hipMemcpyHostToDevice)) != hipSuccess) {
     rc = fail(c, e, "rt_upload_scene");
     free_scene(c);
-  } else if ((rc = sphere_grids(c, s, scene_diam)) != RT_OK) {  // built on the device from d_geo / d_rad
+  } else if ((c->nsph_up = n, rc = light_grids(c, s, scene_diam)) != RT_OK ||  // built on the device from d_geo /
+             (rc = sphere_grids(c, s, scene_diam)) != RT_OK) {                // d_rad
     free_scene(c);
   } else {
     c->nsph = n;
@@ -3301,6 +3548,9 @@ int rt_get_info(rt_ctx *c, rt_info *out) {
   out->behind_grid_build_ms = c->ug_build_ms;
   out->bvh_build_ms = c->bvh_build_ms;
   out->light_grid_build_ms = c->lg_build_ms;
+  out->scratch_bytes = (uint64_t)(c->cstack_bytes + c->dq_bytes + c->homes_bytes +
+                                  (size_t)c->home_words * sizeof(unsigned long long) + c->cg_count_cap + c->cg_ent_cap +
+                                  c->cg_disks_cap + c->cg_pairs_cap + c->cg_npairs_cap + c->perm_cap);
   return RT_OK;
 }
 

@@ -68,7 +68,7 @@ class rt_info(C.Structure):
                 ("sphere_grid_build_ms", C.c_double), ("behind_grid", C.c_int32), ("behind_grid_last", C.c_int32),
                 ("behind_grid_cells", C.c_uint64), ("behind_grid_entries", C.c_uint64),
                 ("behind_grid_build_ms", C.c_double), ("bvh_build_ms", C.c_double),
-                ("light_grid_build_ms", C.c_double)]
+                ("light_grid_build_ms", C.c_double), ("scratch_bytes", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -55,7 +55,7 @@ extern "C" {
 #define RT_HIP_ABI_VERSION 11 /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
                                    6: rt_render_tiles; 7: rt_get_info; 8: rt_info sphere-grid fields;
                                    9: rt_info behind-grid fields; 10: RT_ERR_CHECK;
-                                   11: rt_info BVH / light-grid build times */
+                                   11: rt_info BVH / light-grid build times, scratch bytes */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -282,6 +282,8 @@ typedef struct rt_info {
     double behind_grid_build_ms; /* host wall time of its build, part of upload_ms */
     double bvh_build_ms;         /* host wall time of the BVH build and upload, part of upload_ms */
     double light_grid_build_ms;  /* host wall time of the light grids' build and upload, part of upload_ms */
+    uint64_t scratch_bytes;      /* device scratch the context holds for its launches: reflection stacks (stack
+                                    homes / per-pixel stack), the deferred queue, the camera grids, the tile order */
 } rt_info;
 int rt_get_info(rt_ctx *ctx, rt_info *out);
 

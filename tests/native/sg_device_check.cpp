@@ -1,5 +1,6 @@
-// Check of the sphere grids' device builder (rt_kernel.hip sg_disk_kernel /
-// sg_bin_kernel / the scan / sg_sort_kernel / sg_start_kernel) on the CPU:
+// Check of the device point-grid builder (rt_kernel.hip pg_disk_kernel /
+// pg_bin_kernel / the scan / sg_sort_kernel, ids_sort_kernel / sg_start_kernel,
+// lg_start_kernel) on the CPU, for the sphere grids and the light grids:
 // the kernels' per-lane functions (csrc/rt_cgbuild.h: cg_view with the origin
 // ball's rho, cg_side, cg_block, cg_tile, cg_cell, cg_before) run lane by
 // lane in the kernels' pass structure -- pass 1 a wave per (grid, sphere)
@@ -8,8 +9,11 @@
 // counting then filling CSR lists, the (tlo, index) sort -- against the host
 // builder (rt_lightgrid.cpp build_sphere_grids, the one rt_upload_scene used
 // before) on random scenes: which spheres get a grid, and for every grid and
-// cell the exact list (sphere, tlo bits) in order.
-// Prints "scenes <n> grids <n> refused <n> cells <n> entries <n> differ <n>".
+// cell the exact list (sphere, tlo bits) in order.  The light grids (one side,
+// global spheres on a separate list, ids ascending) against build_light_grid:
+// every light's start row and ids, lights with non-finite positions included.
+// Prints "scenes <n> grids <n> refused <n> cells <n> entries <n> differ <n>
+// lights <n> light_entries <n> light_differ <n>".
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -95,11 +99,62 @@ void build_device(const std::vector<double> &cx, const std::vector<double> &cy, 
     }
   }
 }
+// the device build of the light grids: per light, lists for the 6N^2 cells
+// and the global list (index 6N^2), ids ascending
+std::vector<std::vector<int>> build_device_lights(const std::vector<double> &cx, const std::vector<double> &cy,
+                                                  const std::vector<double> &cz, const std::vector<double> &r,
+                                                  const std::vector<double> &lx, const std::vector<double> &ly,
+                                                  const std::vector<double> &lz, double diam, int N) {
+  const int n = (int)cx.size(), nl = (int)lx.size();
+  std::vector<rtk::CubePatch> faces, blocks, tiles;
+  std::vector<double> cell;
+  int NT = 0, NB = 0;
+  rtk::cube_tables(N, faces, blocks, tiles, cell, NT, NB);
+  const int nb = 6 * NB * NB;
+  const long long cells = 6LL * N * N, row = cells + 1;
+  const double dm = std::isfinite(diam) ? diam : 0.0;
+  std::vector<std::vector<int>> lists((size_t)(nl * row));
+  for (int l = 0; l < nl; l++) {
+    const bool allglob = !(std::isfinite(lx[l]) && std::isfinite(ly[l]) && std::isfinite(lz[l]));
+    for (int i = 0; i < n; i++) {
+      rtk::CgView v = rtk::cg_view(cx[i], cy[i], cz[i], std::fabs(r[i]), lx[l], ly[l], lz[l], dm, 0.0);
+      if (allglob) v = rtk::cg_view(0.0, 0.0, 0.0, INFINITY, 0.0, 0.0, 0.0, 0.0);
+      if (v.global) {
+        lists[(size_t)(l * row + cells)].push_back(i);
+        continue;
+      }
+      const rtk::CgDisk k = rtk::cg_side(v, 0, i);
+      for (int b = 0; b < nb; b++) {
+        if (!rtk::cg_block(k, faces.data(), blocks.data(), NB, b)) continue;
+        const bool wide = rtk::cg_wide(k);
+        const int f = b / (NB * NB), bj = (b / NB) % NB, bi = b % NB;
+        unsigned long long tmask = 0, imask = 0;
+        for (int lane = 0; lane < 64; lane++) {
+          bool tm, inside;
+          rtk::cg_tile(k, tiles.data(), NT, f, bi, bj, lane, tm, inside);
+          if (tm) tmask |= 1ull << lane;
+          if (inside) imask |= 1ull << lane;
+        }
+        while (tmask) {
+          const int tl = __builtin_ctzll(tmask);
+          tmask &= tmask - 1;
+          for (int lane = 0; lane < 64; lane++) {
+            const int gc = rtk::cg_cell(k, wide, cell.data(), N, f, bi, bj, tl, lane, (imask >> tl) & 1ull);
+            if (gc >= 0) lists[(size_t)(l * row + gc)].push_back(i);
+          }
+        }
+      }
+    }
+  }
+  for (auto &e : lists) std::sort(e.begin(), e.end());  // ids_sort_kernel
+  return lists;
+}
 }  // namespace
 
 int main(int argc, char **argv) {
   const int seeds = argc > 1 ? std::atoi(argv[1]) : 20;
-  long scenes = 0, grids = 0, refused = 0, ncells = 0, entries = 0, differ = 0;
+  long scenes = 0, grids = 0, refused = 0, ncells = 0, entries = 0, differ = 0, lights = 0, lentries = 0,
+       ldiffer = 0;
   for (int seed = 0; seed < seeds; seed++) {
     std::mt19937_64 rng(9100 + seed);
     std::uniform_real_distribution<double> U(-1.0, 1.0);
@@ -176,8 +231,40 @@ int main(int argc, char **argv) {
         differ += same ? 0 : 1;
       }
     }
+    // light grids: 1-6 lights (one maybe non-finite, one inside a sphere), N as drawn (or 128 / 768-like sizes)
+    const int nl = 1 + (int)(rng() % 6);
+    std::vector<double> lx(nl), ly(nl), lz(nl);
+    for (int l = 0; l < nl; l++) {
+      lx[l] = shift + scale * 15 * U(rng);
+      ly[l] = shift + scale * 15 * U(rng);
+      lz[l] = shift + scale * 15 * U(rng);
+    }
+    if (nl > 1 && rng() % 3 == 0) lx[1] = NAN;
+    if (nl > 2) lx[2] = cx[0], ly[2] = cy[0], lz[2] = cz[0];  // a light at a sphere's centre
+    const int NL = (int[]){1, 3, 16, 64, 128}[rng() % 5];
+    std::vector<int32_t> lstart, lids;
+    rtk::build_light_grid(cx.data(), cy.data(), cz.data(), r.data(), n, lx.data(), ly.data(), lz.data(), nl, diam, NL,
+                          lstart, lids);
+    const std::vector<std::vector<int>> dl = build_device_lights(cx, cy, cz, r, lx, ly, lz, diam, NL);
+    const long long lcells = 6LL * NL * NL;
+    // the device's start row is the exclusive prefix of its list lengths (lg_start_kernel)
+    long long off = 0;
+    for (int l = 0; l < nl; l++) {
+      lights++;
+      bool same = true;
+      for (long long c = 0; c <= lcells; c++) {
+        const std::vector<int> &e = dl[(size_t)(l * (lcells + 1) + c)];
+        same = same && lstart[(size_t)(l * (lcells + 2) + c)] == off &&
+               lstart[(size_t)(l * (lcells + 2) + c + 1)] == off + (long long)e.size();
+        for (size_t k = 0; same && k < e.size(); k++) same = lids[(size_t)off + k] == e[k];
+        off += (long long)e.size();
+        lentries += (long)e.size();
+      }
+      ldiffer += same ? 0 : 1;
+    }
   }
-  std::printf("scenes %ld grids %ld refused %ld cells %ld entries %ld differ %ld\n", scenes, grids, refused, ncells,
-              entries, differ);
-  return differ ? 1 : 0;
+  std::printf("scenes %ld grids %ld refused %ld cells %ld entries %ld differ %ld lights %ld light_entries %ld "
+              "light_differ %ld\n",
+              scenes, grids, refused, ncells, entries, differ, lights, lentries, ldiffer);
+  return differ || ldiffer ? 1 : 0;
 }

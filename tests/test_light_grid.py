@@ -172,15 +172,18 @@ def test_camera_grid_device_builder(tmp_path):
 
 
 def test_sphere_grid_device_builder_matches_host(tmp_path):
-    """The device sphere-grid builder (rt_kernel.hip sg_disk / sg_bin / scan /
-    sg_sort / sg_start kernels, per-lane functions shared through
+    """The device point-grid builder (rt_kernel.hip pg_disk / pg_bin / scan /
+    sort / start kernels, per-lane functions shared through
     csrc/rt_cgbuild.h) run lane by lane in its pass structure on the CPU
     (tests/native/sg_device_check.cpp) gives, on 120 random scenes (scales
     0.1-1000, far from the origin, negative and tiny radii, a ground-sized
     sphere, dense clusters whose grids exceed the global-sphere cap), the same
     grid spheres, the same refusals and, for every cell of every grid, exactly
     build_sphere_grids' list (sphere, tlo bits) in the same order -- so the
-    host builder's proofs (tests/native/sg_check.cpp) carry over."""
+    host builder's proofs (tests/native/sg_check.cpp) carry over; and for the
+    light grids (1-6 lights per scene, one at a sphere's centre, some
+    non-finite) exactly build_light_grid's start rows and ids
+    (tests/native/lg_check.cpp's proofs carry over)."""
     exe = tmp_path / "sg_device_check"
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-o", str(exe),
                     os.path.join(REPO, "tests", "native", "sg_device_check.cpp"),
@@ -190,6 +193,8 @@ def test_sphere_grid_device_builder_matches_host(tmp_path):
     w = out.stdout.split()
     assert w[0] == "scenes" and int(w[3]) > 3000 and int(w[5]) > 500 and int(w[9]) > 10000000, out.stdout
     assert w[11] == "0", out.stdout
+    # the light grids (one side, a separate global list, ids ascending) against build_light_grid
+    assert w[12] == "lights" and int(w[13]) > 300 and int(w[15]) > 5000000 and w[17] == "0", out.stdout
 
 
 CAM_SCENES = dict(GRID_SCENES)
