@@ -1080,6 +1080,140 @@ __host__ __device__ __forceinline__ void grid_line(const BvhArgs &bv, D3 o, D3 d
   }
 }
 
+// grid_line<true> (the whole line) as a resumable walk, one cell per call of
+// gw_step: render_deferred_grid advances each lane's walk on its own, so the
+// lanes whose walks ended shade and take new rays while others still walk.
+// The same cells in the same order, the same candidates and the same stop
+// test as grid_closest_line -- so the same (t, index) for every ray
+// (tests/native/ug_check.cpp compares the two on the CPU).
+// The line of a walk, derived from (o, d) whenever the walk resumes (not
+// kept across the shading: fewer registers held).
+struct GridLine {
+  float ox, oy, oz, dx, dy, dz;  // the prefilter's line (fp32, relative to c0)
+  float i0, i1, i2;              // 1 / d per axis
+};
+__host__ __device__ __forceinline__ GridLine gw_line(const BvhArgs &bv, D3 o, D3 d) {
+  const UgArgs &ug = bv.ug;
+  GridLine l;
+  l.ox = (float)(o.x - bv.c0x), l.oy = (float)(o.y - bv.c0y), l.oz = (float)(o.z - bv.c0z);
+  l.dx = (float)d.x, l.dy = (float)d.y, l.dz = (float)d.z;
+  l.i0 = 1.0f / l.dx, l.i1 = 1.0f / l.dy, l.i2 = 1.0f / l.dz;
+  (void)ug;
+  return l;
+}
+// Where the walk is: the current cell, its exit per axis, the line's end in
+// the grid, the step directions (bit k: +1 along axis k), steps left, the
+// sphere tested last.
+struct GridWalk {
+  float e0, e1, e2, s1;
+  int c0, c1, c2, sgn, guard, last;
+};
+__host__ __device__ __forceinline__ float gw_exit(float cs, int c, float p, float iv, bool pos) {
+  return (iv == __builtin_inff() || iv == -__builtin_inff()) ? __builtin_inff()
+                                                            : ((float)(c + (pos ? 1 : 0)) * cs - p) * iv;
+}
+// Starts the walk of (o, d): the global spheres are tested here (test_fn);
+// false when the line misses the grid (nothing more to walk).
+template <typename F>
+__host__ __device__ __forceinline__ bool gw_begin(const BvhArgs &bv, D3 o, D3 d, Work &work, F &&test_fn,
+                                                  GridWalk &w) {
+  const UgArgs &ug = bv.ug;
+  for (int k = 0; k < ug.nglob; ++k) {
+    work.exact += 1;
+    test_fn((int)ug.glob[k]);
+  }
+  const GridLine l = gw_line(bv, o, d);
+  const float cs = ug.cs;
+  const float p0 = l.ox - ug.gx, p1 = l.oy - ug.gy, p2 = l.oz - ug.gz;  // the origin in grid coordinates
+  float s0 = -__builtin_inff(), s1 = __builtin_inff();
+  auto clip = [&](float p, float iv, int n) {
+    const float ta = (0.0f - p) * iv, tb = ((float)n * cs - p) * iv;
+    if (iv == __builtin_inff() || iv == -__builtin_inff()) {
+      if (!(p >= 0.0f && p <= (float)n * cs)) s1 = -__builtin_inff();
+    } else {
+      s0 = fmaxf(s0, fminf(ta, tb));
+      s1 = fminf(s1, fmaxf(ta, tb));
+    }
+  };
+  clip(p0, l.i0, ug.nx);
+  clip(p1, l.i1, ug.ny);
+  clip(p2, l.i2, ug.nz);
+  if (!(s0 <= s1)) return false;
+  w.s1 = s1;
+  const float ics = 1.0f / cs;
+  auto cell_of = [&](float p, float v, int n) {
+    const int c = (int)floorf((p + v * s0) * ics);
+    return c < 0 ? 0 : (c >= n ? n - 1 : c);
+  };
+  w.c0 = cell_of(p0, l.dx, ug.nx), w.c1 = cell_of(p1, l.dy, ug.ny), w.c2 = cell_of(p2, l.dz, ug.nz);
+  w.sgn = (l.dx > 0.0f ? 1 : 0) | (l.dy > 0.0f ? 2 : 0) | (l.dz > 0.0f ? 4 : 0);
+  w.e0 = gw_exit(cs, w.c0, p0, l.i0, w.sgn & 1);
+  w.e1 = gw_exit(cs, w.c1, p1, l.i1, w.sgn & 2);
+  w.e2 = gw_exit(cs, w.c2, p2, l.i2, w.sgn & 4);
+  w.guard = ug.nx + ug.ny + ug.nz + 2;
+  w.last = -1;
+  return true;
+}
+// Tests the current cell's spheres, then moves to the next cell; false when
+// the walk is over (the line left the grid, or the cell's exit is past the
+// best t + tol: grid_line's stop).  l = gw_line of the walk's (o, d).
+template <typename F, typename B>
+__host__ __device__ __forceinline__ bool gw_step(const BvhArgs &bv, const GridLine &l, GridWalk &w, Work &work,
+                                                 F &&test_fn, B &&best_fn) {
+  const UgArgs &ug = bv.ug;
+  const float cs = ug.cs;
+  const int cur = RT_CK(kCkUgCell, (w.c2 * ug.ny + w.c1) * ug.nx + w.c0, ug.nx * ug.ny * ug.nz);
+  const float4 r0 = ug.rec[4 * cur], r1 = ug.rec[4 * cur + 1], r2 = ug.rec[4 * cur + 2], r3 = ug.rec[4 * cur + 3];
+  const float ex = fminf(w.e0, fminf(w.e1, w.e2));  // this cell's exit
+  bool more = false;
+  if (--w.guard > 0) {
+    if (w.e0 <= w.e1 && w.e0 <= w.e2) {
+      w.c0 += (w.sgn & 1) ? 1 : -1;
+      more = w.e0 <= w.s1 && w.c0 >= 0 && w.c0 < ug.nx;
+      w.e0 = gw_exit(cs, w.c0, l.ox - ug.gx, l.i0, w.sgn & 1);
+    } else if (w.e1 <= w.e2) {
+      w.c1 += (w.sgn & 2) ? 1 : -1;
+      more = w.e1 <= w.s1 && w.c1 >= 0 && w.c1 < ug.ny;
+      w.e1 = gw_exit(cs, w.c1, l.oy - ug.gy, l.i1, w.sgn & 2);
+    } else {
+      w.c2 += (w.sgn & 4) ? 1 : -1;
+      more = w.e2 <= w.s1 && w.c2 >= 0 && w.c2 < ug.nz;
+      w.e2 = gw_exit(cs, w.c2, l.oz - ug.gz, l.i2, w.sgn & 4);
+    }
+  }
+  work.cull += 1;
+  const bool behind = ex < 0.0f;  // a cell wholly behind the origin: the deep-inside skip applies
+  const float pm = bv.pmargin;
+  const float d2 = l.dx * l.dx + l.dy * l.dy + l.dz * l.dz;
+  const float dd_hi = d2 * (1.0f + 1e-5f), dd_lo = d2 * (1.0f - 1e-5f);
+  auto one = [&](const float4 &q, int id_at, const int32_t *ids) {
+    const float wx = q.x - l.ox, wy = q.y - l.oy, wz = q.z - l.oz;
+    const float cx = wy * l.dz - wz * l.dy, cy = wz * l.dx - wx * l.dz, cz = wx * l.dy - wy * l.dx;
+    const float x2 = cx * cx + cy * cy + cz * cz;
+    const float ro = q.w + pm, ri = q.w * (1.0f - 0x1p-22f) - pm;
+    if (x2 > ro * ro * dd_hi) return;
+    if (behind && ri > 0.0f && x2 < ri * ri * dd_lo) return;
+    const int id = (int)ids[id_at];
+    if (id == w.last) return;
+    w.last = id;
+    work.exact += 1;
+    test_fn(id);
+  };
+  auto slot = [&](const float4 &q, int j) {
+    if (q.w >= 0.0f) {
+      one(q, 4 * cur + j, ug.rid);
+      return true;
+    }
+    if (q.w == -2.0f)
+      for (int k = __builtin_bit_cast(int, q.x), ke = __builtin_bit_cast(int, q.y); k < ke; ++k)
+        one(ug.q[RT_CK(kCkUgOver, k, ug.nq)], RT_CK(kCkUgOver, k, ug.nq), ug.ids);
+    return false;
+  };
+  if (slot(r0, 0) && slot(r1, 1) && slot(r2, 2)) slot(r3, 3);
+  if (!more) return false;
+  return !((double)ex > best_fn() + (double)ug.tol);
+}
+
 // Host-callable too (tests/native/ug_check.cpp runs this same code on the CPU).
 template <typename F>
 __host__ __device__ __forceinline__ void behind_cells(const BvhArgs &bv, D3 o, D3 d, Work &work, F &&test_fn) {

@@ -8,9 +8,6 @@
 // last ambient/camera wins; malformed records are skipped with a warning;
 // trailing tokens are ignored.  Numbers go through std::istream >> double, the
 // same extractor the reference uses, so parsed doubles are identical.
-#include <fcntl.h>
-#include <unistd.h>
-#include <cerrno>
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -21,6 +18,7 @@
 #include <sstream>
 #include <string>
 #include <vector>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 
@@ -195,79 +193,79 @@ int rt_camera_from_scene(const rt_scene *s, rt_camera *c) {
 // instead of ostream double formatting (1.85 s at 1080p upstream).
 int rt_write_ppm(const char *path, const uint8_t *rgb, int width, int height, int binary) {
   if (!path || !rgb || width < 0 || height < 0) return RT_ERR_INVALID_ARG;
-  const size_t n = (size_t)width * (size_t)height;
-  char head[64];
-  const int hn = std::snprintf(head, sizeof head, "%s\n%d %d\n255\n", binary ? "P6" : "P3", width, height);
-  // "0".."255" and their lengths, built once (a function-local static: safe
-  // when several threads write images at the same time)
-  struct Tab {
-    char s[256][4];
-    unsigned char n[256];
-    Tab() {
-      for (int v = 0; v < 256; v++) n[v] = (unsigned char)std::snprintf(s[v], 4, "%d", v);
-    }
-  };
-  static const Tab T;
-  // P3: pixel ranges formatted in parallel (each into its own buffer, at most
-  // 12 bytes per pixel) -- the serial writer's bytes, main.cpp:69-91: rows as
-  // given, "r g b\n" per pixel -- then each range written at its offset (the
-  // header's length plus the ranges before it) by its own thread; P6: the
-  // bytes as given, in ranges the same way
-  const unsigned hw = std::thread::hardware_concurrency();
-  const size_t nthr = n < ((size_t)1 << 16) ? 1 : std::max<size_t>(1, std::min<size_t>(hw ? hw : 1, 16));
-  std::vector<std::vector<char>> bufs(nthr);
-  auto format = [&](size_t k) {
-    const size_t p0 = n * k / nthr, p1 = n * (k + 1) / nthr;
-    std::vector<char> &out = bufs[k];
-    if (binary) return;
-    out.resize((p1 - p0) * 12);
-    char *o = out.data();
-    for (size_t p = p0; p < p1; p++) {
-      for (int c = 0; c < 3; c++) {
-        const unsigned v = rgb[3 * p + c];
-        std::memcpy(o, T.s[v], 4);
-        o += T.n[v];
-        *o++ = c == 2 ? '\n' : ' ';
+  FILE *f = std::fopen(path, "wb");
+  if (!f) return RT_ERR_IO;
+  size_t n = (size_t)width * (size_t)height;
+  std::fprintf(f, "%s\n%d %d\n255\n", binary ? "P6" : "P3", width, height);
+  int rc = RT_OK;
+  if (binary) {
+    if (std::fwrite(rgb, 1, n * 3, f) != n * 3) rc = RT_ERR_IO;
+  } else {
+    // "0".."255" and their lengths, built once (a function-local static: safe
+    // when several threads write images at the same time)
+    struct Tab {
+      char s[256][4];
+      unsigned char n[256];
+      Tab() {
+        for (int v = 0; v < 256; v++) n[v] = (unsigned char)std::snprintf(s[v], 4, "%d", v);
       }
+    };
+    static const Tab T;
+    // pixel ranges formatted in parallel (each into its own buffer, at most
+    // 12 bytes per pixel), then written in order: the bytes are the serial
+    // writer's (main.cpp:69-91: rows as given, "r g b\n" per pixel)
+    auto format = [&](size_t p0, size_t p1, std::vector<char> &out) {
+      out.resize((p1 - p0) * 12);
+      char *o = out.data();
+      for (size_t p = p0; p < p1; p++) {
+        for (int c = 0; c < 3; c++) {
+          const unsigned v = rgb[3 * p + c];
+          std::memcpy(o, T.s[v], 4);
+          o += T.n[v];
+          *o++ = c == 2 ? '\n' : ' ';
+        }
+      }
+      out.resize((size_t)(o - out.data()));
+    };
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t nthr = n < ((size_t)1 << 16) ? 1 : std::max<size_t>(1, std::min<size_t>(hw ? hw : 1, 16));
+    const size_t nchunk = nthr * 4;  // a few per thread: the first write starts while the rest are formatted
+    std::vector<std::vector<char>> bufs(nchunk);
+    std::vector<unsigned char> done(nchunk, 0);
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t next = 0;
+    auto worker = [&]() {
+      for (;;) {
+        size_t k;
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          if (next >= nchunk) return;
+          k = next++;
+        }
+        format(n * k / nchunk, n * (k + 1) / nchunk, bufs[k]);
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          done[k] = 1;
+        }
+        cv.notify_all();
+      }
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nthr; t++) th.emplace_back(worker);
+    if (nthr == 1) worker();
+    for (size_t k = 0; k < nchunk; k++) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done[k] != 0; });
+      }
+      if (rc == RT_OK && std::fwrite(bufs[k].data(), 1, bufs[k].size(), f) != bufs[k].size()) rc = RT_ERR_IO;
+      std::vector<char>().swap(bufs[k]);
     }
-    out.resize((size_t)(o - out.data()));
-  };
-  auto bytes_of = [&](size_t k) -> std::pair<const char *, size_t> {
-    if (binary) {
-      const size_t p0 = n * k / nthr, p1 = n * (k + 1) / nthr;
-      return {reinterpret_cast<const char *>(rgb) + 3 * p0, 3 * (p1 - p0)};
-    }
-    return {bufs[k].data(), bufs[k].size()};
-  };
-  const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-  if (fd < 0) return RT_ERR_IO;
-  auto put = [fd](const char *p, size_t len, off_t at) {
-    while (len > 0) {
-      const ssize_t w = ::pwrite(fd, p, len, at);
-      if (w < 0 && errno == EINTR) continue;
-      if (w <= 0) return false;
-      p += w;
-      len -= (size_t)w;
-      at += (off_t)w;
-    }
-    return true;
-  };
-  std::vector<std::thread> th;
-  for (size_t k = 1; k < nthr; k++) th.emplace_back(format, k);
-  format(0);
-  for (auto &t : th) t.join();
-  th.clear();
-  std::vector<off_t> at(nthr + 1, (off_t)hn);
-  for (size_t k = 0; k < nthr; k++) at[k + 1] = at[k] + (off_t)bytes_of(k).second;
-  bool ok = put(head, (size_t)hn, 0);
-  std::vector<unsigned char> okk(nthr, 1);
-  for (size_t k = 1; k < nthr; k++)
-    th.emplace_back([&, k] { okk[k] = put(bytes_of(k).first, bytes_of(k).second, at[k]) ? 1 : 0; });
-  okk[0] = put(bytes_of(0).first, bytes_of(0).second, at[0]) ? 1 : 0;
-  for (auto &t : th) t.join();
-  for (size_t k = 0; k < nthr; k++) ok = ok && okk[k];
-  if (::close(fd) != 0) ok = false;
-  return ok ? RT_OK : RT_ERR_IO;
+    for (auto &t : th) t.join();
+  }
+  if (std::fclose(f) != 0) rc = RT_ERR_IO;
+  return rc;
 }
 
 }  // extern "C"

@@ -1276,6 +1276,128 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
   flush_counts(kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters), sums, work);
 }
 
+// render_deferred for scenes with the uniform grid's whole-line closest hits
+// (bv.ug.closest: scenes above 1,024 spheres), with the walks decoupled from
+// the shading as in render_deferred_walk: a lane's grid walk advances one cell
+// per step (gw_step, the same cells, candidates and stop as
+// grid_closest_line), a lane whose walk ended waits, and the ready lanes
+// shade once kShadeAt of them are (or no lane walks); a spawned reflection ray
+// starts its walk at once, an ended chain stores its pixel and the lane takes
+// the next queued ray.  The level >= 2 rays' walks are long and uneven
+// (cfg 5: lane utilisation 0.46 in render_deferred's lockstep walks).
+__global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_grid(const RenderArgs a) {
+  const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards;
+  const int cap = a.dq_cap;
+  const unsigned long long cnt = a.counters[(size_t)shard * kShardStride + kDeferSlot];
+  const unsigned n_dq = (unsigned)(cnt < (unsigned long long)cap ? cnt : (unsigned long long)cap);
+  if (first * 64u >= n_dq) return;
+  const int lane = (int)(threadIdx.x & 63);
+  const unsigned npx_frame = (unsigned)((size_t)a.rows.count * a.od.xw);
+  const unsigned sstride = (unsigned)kShards * (unsigned)cap;  // the chain's stack: dstack[level][queue slot]
+  Work work;
+  unsigned c_shadow = 0, c_reflect = 0, c_neg = 0;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  bool act = false, walking = false, more = true;
+  unsigned long long *fetch = kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters) +
+                              (size_t)shard * kShardStride + kFetchSlot;  // as render_deferred
+  D3 o = mk(0.0, 0.0, 0.0), d = o;
+  int key = -1, dleft = 0, lev = 0;
+  unsigned pixg = 0, qslot = 0;  // the ray's output pixel (launch index) and queue slot
+  // the grid walk of this lane's ray and the best hit so far (t, numerator, sphere)
+  GridWalk gw;
+  int bi = -1;
+  double bt = kInf, bn = __builtin_inf();
+  auto begin = [&](const BvhArgs &bv) {  // a new ray: an empty best, the global spheres, the first cell
+    bt = kInf;
+    bn = __builtin_inf();
+    bi = -1;
+    const double a4 = 4.0 * dot(d, d), a2 = 0.5 * a4;
+    const bool fast = a2_ok(a2);
+    const SphGeo *__restrict__ g = a.geo;
+    walking = gw_begin(bv, o, d, work, [&](int i) { closest_test(g[RT_CK(kCkSphere, i, a.n)], i, o, d, a4, a2, fast, bt, bn, bi); }, gw);
+  };
+  while (true) {
+    {
+      const unsigned long long idle = ~__ballot(act);
+      if (idle && more) {
+        const int fi = __builtin_ctzll(idle);
+        unsigned long long base = 0;
+        if (lane == fi) base = atomicAdd(fetch, (unsigned long long)__popcll(idle));
+        base = __shfl(base, fi, 64);
+        const unsigned long long i = base + (unsigned long long)__popcll(idle & lt);
+        more = base + (unsigned long long)__popcll(idle) < n_dq;
+        if (!act && i < n_dq) {
+          const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[RT_CK(kCkDeferQ, (size_t)shard * (size_t)cap + i, (long long)kShards * cap)];
+          o = mk(e.ox, e.oy, e.oz);
+          d = mk(e.dx, e.dy, e.dz);
+          lev = e.orig;
+          dleft = e.dleft;
+          key = e.key;
+          pixg = (unsigned)e.pix;
+          qslot = shard * (unsigned)cap + (unsigned)i;
+          act = true;
+          begin(kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv));
+        }
+      }
+    }
+    if (__ballot(act) == 0) break;
+    // walk until enough lanes are ready to shade (or no lane walks)
+    if (__ballot(walking)) {
+      const BvhArgs &bv = kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv);
+      const double a4 = 4.0 * dot(d, d), a2 = 0.5 * a4;
+      const bool fast = a2_ok(a2);
+      const SphGeo *__restrict__ g = a.geo;
+      const GridLine gl = gw_line(bv, o, d);
+      while (true) {
+        const unsigned long long wm = __ballot(walking);
+        if (wm == 0 || __popcll(__ballot(act) & ~wm) >= kShadeAt) break;
+        if (walking)
+          walking = gw_step(bv, gl, gw, work,
+                            [&](int i) { closest_test(g[RT_CK(kCkSphere, i, a.n)], i, o, d, a4, a2, fast, bt, bn, bi); },
+                            [&] { return bt; });
+      }
+    }
+    const bool ready = act && !walking;
+    if (__ballot(ready)) {
+      int outcome = 0, nkey = 0;
+      D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
+      double refl = 0.0;
+      shade_hit<true, true, true>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, ready, o, d, key,
+                                   dleft, bi, bt, work, c_shadow, outcome, color, refl, no, nd, nkey);
+      bool spawned = false;
+      if (ready) {
+        StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, dstack)>(a.dstack);
+        if (outcome == kSpawned) {
+          gs[RT_CK(kCkStack, qslot + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)] =
+              StackEnt{color.x, color.y, color.z, refl};
+          ++lev;
+          o = no;
+          d = nd;
+          key = nkey;
+          --dleft;
+          ++c_reflect;
+          spawned = true;
+        } else {
+          D3 res = color;
+          while (lev > 0) {  // main.cpp:54, innermost first
+            --lev;
+            const StackEnt e = gs[RT_CK(kCkStack, qslot + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)];
+            res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
+          }
+          const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
+          const unsigned f = pixg / npx_frame;
+          or_px(static_cast<uint8_t *>(od.ptr) + (size_t)RT_CK(kCkOut, f, a.frames) * (size_t)od.fstride, pixg - f * npx_frame,
+                pack_px(res, c_neg));
+          act = false;
+        }
+      }
+      if (spawned) begin(kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv));
+    }
+  }
+  unsigned long long sums[4] = {0ull, wave_sum(c_shadow), wave_sum(c_reflect), wave_sum(c_neg)};
+  flush_counts(kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters), sums, work);
+}
+
 // Reassemble rank-major shards into PPM row order (one workgroup per row).
 __global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                            int W, int H, int band, int G, int R) {
@@ -1826,7 +1948,10 @@ struct rt_ctx {
   // without it, profiles/r3n/ab_knobs.log; 32-frame launches are 13 % slower
   // per frame without it)
   int defer = -1;
-  bool defer_walk = true;     // RT_HIP_DEFER_WALK: deferred rays of a scene whose closest hits always walk the BVH use render_deferred_walk
+  bool defer_walk = true;
+  // RT_HIP_DEFER_GRID (tuning build): deferred rays of a scene whose closest hits walk the uniform grid use
+  // render_deferred_grid (decoupled walks) instead of render_deferred
+  bool defer_grid = false;     // RT_HIP_DEFER_WALK: deferred rays of a scene whose closest hits always walk the BVH use render_deferred_walk
   int merge_q = 64;           // kStackMerge: the launch's LDS queue entries per wave (launch_render4 picks it)
   int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (8, 16, 32 or 64)
   int defer_level = kDeferLevel;  // RT_HIP_DEFER_LEVEL (>= 1)
@@ -2893,6 +3018,8 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       // the cull sweeps (synth200 1 % slower on the walk kernel)
       if (kCull && fast && c->defer_walk && bv.nnodes > 0 && bv.always && !(bv.ug.on && bv.ug.closest))
         hipLaunchKernelGGL(render_deferred_walk, dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
+      else if (kCull && fast && c->defer_grid && bv.ug.on && bv.ug.closest)  // the same with grid walks
+        hipLaunchKernelGGL(render_deferred_grid, dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
       else if (fast)
         hipLaunchKernelGGL((render_deferred<kCull, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
       else
@@ -3032,6 +3159,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0 ? 1 : 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_WALK")) c->defer_walk = std::atoi(e) != 0;
+  if (const char *e = std::getenv("RT_HIP_DEFER_GRID")) c->defer_grid = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_LEVEL")) c->defer_level = std::max(1, std::min(RT_MAX_DEPTH, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(8, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(1024, std::atoi(e)));

@@ -59,7 +59,8 @@ def scene(rng):
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 300.0
     rng = random.Random(int(sys.argv[2]) if len(sys.argv) > 2 else 20261016)
-    r = rt_hip.Renderer(0)
+    # FUZZ_VARIANT=tuning: the tuning build, so its RT_HIP_* knobs apply
+    r = rt_hip.Renderer(0, variant=os.environ.get("FUZZ_VARIANT") or None)
     t0, k, px, frames, moving = time.time(), 0, 0, 0, 0
     try:
         while time.time() - t0 < budget:
