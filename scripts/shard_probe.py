@@ -25,7 +25,8 @@ fpl = int(os.environ.get("FPL", "1"))  # frames per launch (rt_render_frames_asy
 name, W, H, D = WORK[wl]
 scene = rt_hip.Scene.load(os.path.join(ROOT, "cs420-ray-tracer_amd", "scenes", name + ".txt"))
 cam = scene.camera()
-r = rt_hip.Renderer(0)
+# PROBE_VARIANT=tuning: the tuning build, so its RT_HIP_* knobs apply
+r = rt_hip.Renderer(0, variant=os.environ.get("PROBE_VARIANT") or None)
 r.upload(scene)
 out = torch.empty((fpl, H, W, 3), dtype=torch.uint8, device="cuda:0")
 res = {"workload": wl, "band": band, "frames_per_launch": fpl}
