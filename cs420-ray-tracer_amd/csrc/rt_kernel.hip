@@ -99,7 +99,8 @@ struct RenderArgs {
   int dq_cap;                     // entries per shard segment; 0 = no deferral
   int merge_q;                    // kStackMerge: LDS ray-queue entries per wave (16..64)
   int nsingle;                    // kStackMerge: the first nsingle tile slots (heaviest class) get a wave each
-  int merge_end;                  // kStackMerge: slots [nsingle, merge_end) go kMergeTiles per wave, the rest
+  int npair;                      // kStackMerge: the next npair slots go two per wave
+  int merge_end;                  // kStackMerge: slots [nsingle + npair, merge_end) go kMergeTiles per wave, the rest
                                   // (the launch's tail: its lightest tiles) one per wave again
   int pix_off;                    // kStackMerge: LDS offset of the wave's finished pixels (flush_tile)
   int rows_dword;                 // kStackMerge: every 8-pixel tile row starts dword aligned (flush_tile)
@@ -638,7 +639,9 @@ __device__ __forceinline__ int home_acquire(unsigned long long *bits, int nwords
   int h = -1;
   if ((threadIdx.x & 63) == 0) {
     int w = (int)(blockIdx.x % (unsigned)nwords);
-    unsigned long long cur = 0ull;  // a guess: the first try learns the word
+    // the first try: a bit picked by the workgroup id as well (a half-full word
+    // then takes one atomic, not two); it learns the word
+    unsigned long long cur = ~(1ull << ((blockIdx.x / (unsigned)nwords) & 63u));
     while (h < 0) {
       while (~cur) {
         const int bit = __builtin_ctzll(~cur);
@@ -714,11 +717,22 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     // merge_end, then one slot per group again (the launch's last, lightest
     // tiles: the waves that end a launch are short, so fewer slots idle while
     // the last ones finish)
+    // (and, between the singles and the merged groups, npair slots two per group)
     const int ns = kernarg_late<true, offsetof(RenderArgs, nsingle)>(a.nsingle);
+    const int pr = kernarg_late<true, offsetof(RenderArgs, npair)>(a.npair);
     const int me = kernarg_late<true, offsetof(RenderArgs, merge_end)>(a.merge_end);
-    const int nm = (me - ns + kMergeTiles - 1) / kMergeTiles;
-    const int base = group < ns ? group : (group < ns + nm ? ns + (group - ns) * kMergeTiles : me + (group - ns - nm));
-    const int nt = group < ns || group >= ns + nm ? 1 : (me - base < kMergeTiles ? me - base : kMergeTiles);
+    const int np = (pr + 1) >> 1, m0 = ns + pr;  // pair groups; the first slot of the merged groups
+    const int nm = (me - m0 + kMergeTiles - 1) / kMergeTiles;
+    int base, nt;
+    if (group < ns) {
+      base = group, nt = 1;
+    } else if (group < ns + np) {
+      base = ns + 2 * (group - ns), nt = m0 - base < 2 ? m0 - base : 2;
+    } else if (group < ns + np + nm) {
+      base = m0 + (group - ns - np) * kMergeTiles, nt = me - base < kMergeTiles ? me - base : kMergeTiles;
+    } else {
+      base = me + (group - ns - np - nm), nt = 1;
+    }
     bool tile_pass = false;
     if (__ballot(act) == 0) {
       if (next < nt) {  // camera rays of the next tile: camera.h:17-25, main.cpp:151-154 (as trace_tile)
@@ -2007,6 +2021,7 @@ struct rt_ctx {
   // (merge_end); 0: four per wave to the end.  RT_HIP_TAIL_WAVES (tuning build)
   int tail = 1;
   int tail_waves = 12;
+  int pair_class = -1;  // RT_HIP_PAIR_CLASS (tuning build): tiles of classes [pair_class, single class) two per wave
   // RT_HIP_XCD_FRAMES: multi-frame launches put every frame of a tile group on
   // one XCD (render_kernel).  -1 (default): for scenes with the uniform grid
   // (large scenes, whose lists and nodes outgrow an XCD's L2: synth10k 2.58 ->
@@ -2862,7 +2877,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     gstack = reinterpret_cast<StackEnt *>(c->cstack_buf);
   }
   const int *perm = nullptr;
-  int nsingle = 0;
+  int nsingle = 0, npair = 0;
   long long tail = 0;
   // The heavy-first order pays off when a launch has many more tiles than the
   // chip has wave slots; a small launch (a hybrid driver's 64x64 tile) keeps
@@ -2882,11 +2897,16 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       long long heavy = 0;
       for (int k = sc; k < kSchedClasses; k++) heavy += c->perm_cls[k];
       nsingle = (int)std::min<long long>(heavy, ntiles);
+      // RT_HIP_PAIR_CLASS (tuning build): classes [pair_class, sc) two tiles per wave
+      long long pairs = 0;
+      for (int k = std::max(0, c->pair_class); k < sc; k++) pairs += c->perm_cls[k];
+      if (c->pair_class < 0) pairs = 0;
+      npair = (int)std::min<long long>(pairs, ntiles - nsingle);
       // multi-frame launches end on their lightest tiles one per wave: about
       // as many as the chip holds waves (12 per CU), over the launch's frames
       if (c->tail)
-        tail = std::min<long long>(ntiles - nsingle, ((long long)c->n_cu * c->tail_waves + nf - 1) / nf);
-      nslots = nsingle + (ntiles - nsingle - tail + kMergeTiles - 1) / kMergeTiles + tail;
+        tail = std::min<long long>(ntiles - nsingle - npair, ((long long)c->n_cu * c->tail_waves + nf - 1) / nf);
+      nslots = nsingle + (npair + 1) / 2 + (ntiles - nsingle - npair - tail + kMergeTiles - 1) / kMergeTiles + tail;
     }
   }
   const bool xcd_frames = nf > 1 && (c->xcd_frames > 0 || (c->xcd_frames < 0 && bv.ug.on));
@@ -2924,6 +2944,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.dq_cap = 0;
   ra.merge_q = c->merge_q;
   ra.nsingle = nsingle;
+  ra.npair = npair;
   ra.merge_end = (int)(ntiles - tail);
   // merge_tiles' pixel bytes: after the scene and the walk stacks, where render_kernel's park/queue region starts
   ra.pix_off = (int)(((lds_layout(kLds, c->nsph, c->nlight, bv.nnodes).end + 31) & ~(size_t)31) +
@@ -3173,6 +3194,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_XCD_FRAMES")) c->xcd_frames = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_TAIL")) c->tail = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_TAIL_WAVES")) c->tail_waves = std::max(1, std::min(64, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_PAIR_CLASS")) c->pair_class = std::max(-1, std::min(kSchedClasses, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER_DIV")) c->defer_div = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_GRID_CELLS")) c->ug_cells = std::max(0.05, std::min(64.0, std::atof(e)));
   if (const char *e = std::getenv("RT_HIP_SINGLE_CLASS"))

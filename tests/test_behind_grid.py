@@ -106,7 +106,7 @@ def test_tangent_scenes_need_the_negative_root():
 _FORCED = {"RT_HIP_BEHIND_GRID": "1", "RT_HIP_BVH_ALWAYS": "1", "RT_HIP_SPHERE_GRID": "0", "RT_HIP_CAM_GRID": "0"}
 
 
-@pytest.fixture(params=["on", "off", "on-defer1", "closest"])  # on*: BVH walk ahead + behind_cells
+@pytest.fixture(params=["on", "off", "on-defer1", "closest", "closest-defer-grid"])  # on*: BVH walk ahead + behind_cells
 def behind_renderer(request, monkeypatch):
     import rt_hip
 
@@ -116,9 +116,11 @@ def behind_renderer(request, monkeypatch):
         env["RT_HIP_BEHIND_GRID"] = "0"
     if request.param == "on-defer1":
         env["RT_HIP_DEFER_LEVEL"] = "1"  # level >= 1 rays of multi-frame launches in the deferred walk kernel
-    if request.param == "closest":
+    if request.param.startswith("closest"):
         env["RT_HIP_GRID_CLOSEST"] = "1"  # closest hits along the whole line through the grid, no BVH walk
         env["RT_HIP_DEFER_LEVEL"] = "1"
+    if request.param == "closest-defer-grid":
+        env["RT_HIP_DEFER_GRID"] = "1"  # the deferred rays' walks decoupled (render_deferred_grid)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     r = rt_hip.Renderer(0, variant=knob_variant())
