@@ -156,7 +156,32 @@ enum { kEnded = 1, kSpawned = 2 };
 // shading with the shadow queries, and the reflection decision.  Lanes with
 // alive = false take no part; it has no wave-wide operation that needs every
 // lane active (render_deferred_walk calls it for the lanes whose walk ended).
-template <bool kCull, bool kArgMem = false, bool kFast = false>
+// Position of the k-th (from 0) set bit of m (k < popcount(m)).
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    const unsigned long long low = m & ((1ull << s) - 1ull);
+    const int c = __popcll(low);
+    if (k >= c) {
+      k -= c;
+      m >>= s;
+      pos += s;
+    } else {
+      m = low;
+    }
+  }
+  return pos;
+}
+
+// kWide (one-frame launches): a wave whose hit lanes are at most half of it
+// spreads the light loop over the lanes -- in passes of lpp = 64 / hits lights,
+// lane j handles light l0 + j % lpp of the (j / lpp)-th hit lane: its shadow
+// query and Phong terms, computed with the same operands and operations as the
+// loop below (the hit lane's normal and view direction passed over) -- and each
+// hit lane then adds its lights' terms in file order (scene.h:117): the same
+// bits, in ceil(lights / lpp) passes instead of one per light.
+template <bool kCull, bool kArgMem = false, bool kFast = false, bool kWide = false>
 __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                           const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                           int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o,
@@ -179,7 +204,72 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
     // scene.h:94-120: per light in file order, the shadow query then (if lit)
     // the Phong terms with the same ldir -- skipped by a wave (or the active
     // lanes of one) whose rays all left the scene
-    if (__ballot(hit)) {
+    bool wide_done = false;
+    if constexpr (kWide && kFast) {
+      const unsigned long long hm = __ballot(hit);
+      const int nh = __popcll(hm);
+      const LgArgs &lgw = kernarg_late<kArgMem, offsetof(RenderArgs, lg)>(lg_arg);
+      const int lpp = nh ? (64 / nh < nl ? 64 / nh : nl) : 0;  // lights per pass
+      if (nl >= 2 && lpp >= 2 && lgw.on) {                   // wave-uniform
+        const int lane = (int)(threadIdx.x & 63);
+        const int rank = (int)__popcll(hm & ((1ull << lane) - 1ull));
+        D3 nrm = mk(0.0, 0.0, 0.0), view = nrm;
+        if (hit) {
+          const SphGeo sg = g[hi];
+          nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
+          view = normalized(sub(o, hp));                       // main.cpp:38
+        }
+        for (int l0 = 0; l0 < nl; l0 += lpp) {  // lights l0 .. l0 + cnt - 1 in this pass
+          const int cnt = nl - l0 < lpp ? nl - l0 : lpp;
+          const bool helper = lane < nh * cnt;
+          const int r = helper ? lane / cnt : 0, lh = l0 + (helper ? lane - r * cnt : 0);
+          const int src = nth_set_bit(hm, r);
+          // the owner's hit point, sphere, normal and view direction
+          const D3 hq = mk(__shfl(hp.x, src, 64), __shfl(hp.y, src, 64), __shfl(hp.z, src, 64));
+          const D3 nq = mk(__shfl(nrm.x, src, 64), __shfl(nrm.y, src, 64), __shfl(nrm.z, src, 64));
+          const D3 vq = mk(__shfl(view.x, src, 64), __shfl(view.y, src, 64), __shfl(view.z, src, 64));
+          const int hq_i = RT_CK(kCkSphere, __shfl(hi, src, 64), n > 0 ? n : 1);
+          D3 t = mk(0.0, 0.0, 0.0);
+          bool lit = false;
+          {
+            const SphMat m = mat[hq_i];
+            const D3 mc = mk(m.cr, m.cg, m.cb);
+            const LightD L = slight[lh];
+            const D3 lp = mk(L.px, L.py, L.pz);
+            const LgRange cell = lg_range(lgw, lh, hq, lp, helper);
+            const int id0 = lg_first(lgw, cell);
+            const D3 to_light = sub(lp, hq);
+            const double dist = length(to_light);
+            const D3 ldir = normalized(to_light);
+            const D3 so = add(hq, scale(ldir, kEps)), sd = renormalized(ldir);
+            const bool occ = shadow_cells(g, n, helper, so, sd, lp, dist, lgw, lh, cell, id0, work, hq_i);
+            if (helper && !occ) {  // the terms of the loop below, same operands and order
+              const double ndl = max0(dot(nq, ldir));
+              const D3 diffuse = scale(scale(mc, 1.0 - m.refl), ndl);
+              const D3 nl2 = scale(ldir, -1.0);
+              const D3 rdir = sub(nl2, scale(scale(nq, 2.0), dot(nl2, nq)));
+              const double rdv = max0(dot(rdir, vq));
+              double spec = 0.0;
+              int ipow = 0;
+              if (!(rdv == 0.0 && m.shin > 0.0))
+                spec = int_pow_ok(rdv, m.shin, ipow) ? int_pow(rdv, ipow) : pow_call(rdv, m.shin);
+              const D3 specular = scale(scale(mk(L.cr, L.cg, L.cb), kSpec), spec);
+              t = add(specular, diffuse);
+              lit = true;
+            }
+          }
+          // each hit lane adds this pass's lights' terms in file order (scene.h:117)
+          const unsigned long long litm = __ballot(lit);
+          for (int l = 0; l < cnt; ++l) {
+            const int sl = hit ? rank * cnt + l : 0;
+            const D3 tl = mk(__shfl(t.x, sl, 64), __shfl(t.y, sl, 64), __shfl(t.z, sl, 64));
+            if (hit && ((litm >> sl) & 1ull)) col = add(tl, col);
+          }
+        }
+        wide_done = true;
+      }
+    }
+    if (!wide_done && __ballot(hit)) {
       const SphGeo sg = g[hi];
       const SphMat m = mat[hi];
       const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
@@ -308,7 +398,7 @@ __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const d
   return bi;
 }
 
-template <bool kCull, bool kArgMem = false, bool kFast = false>
+template <bool kCull, bool kArgMem = false, bool kFast = false, bool kWide = false>
 __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                        const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                        int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o, D3 d,
@@ -316,8 +406,8 @@ __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const doubl
                                        double &refl, D3 &no, D3 &nd, int &nkey, bool cam_pass = false) {
   double bt;
   const int bi = closest_hit<kCull, kArgMem, kFast>(g, rad, n, bv, alive, o, d, key, work, bt, cam_pass);
-  shade_hit<kCull, kArgMem, kFast>(g, rad, mat, slight, n, nl, amb, bv, lg_arg, alive, o, d, key, dleft, bi, bt, work,
-                                   c_shadow, outcome, color, refl, no, nd, nkey);
+  shade_hit<kCull, kArgMem, kFast, kWide>(g, rad, mat, slight, n, nl, amb, bv, lg_arg, alive, o, d, key, dleft, bi, bt,
+                                          work, c_shadow, outcome, color, refl, no, nd, nkey);
 }
 
 // trace_ray for one camera ray per lane, the wave walking the levels together
@@ -664,7 +754,7 @@ __device__ __forceinline__ void home_release(unsigned long long *bits, int h) {
   if ((threadIdx.x & 63) == 0) atomicAnd(bits + (h >> 6), ~(1ull << (h & 63)));
 }
 
-template <bool kCull, bool kFast>
+template <bool kCull, bool kFast, bool kWide = false>
 __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                             const SphMat *__restrict__ mat, const LightD *__restrict__ slight,
                                             const RenderArgs &a, int group, int frame, const CompactArgs &ca,
@@ -795,7 +885,7 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     const int bi = closest_hit<kCull, true, kFast>(g, rad, a.n, a.bv, act, o, d, key, work, bt,
                                              kFast && tile_pass && kernarg_late<true, offsetof(RenderArgs, cg)>(a.cg).on,
                                              frame);
-    shade_hit<kCull, true, kFast>(g, rad, mat, slight, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft, bi, bt,
+    shade_hit<kCull, true, kFast, kWide>(g, rad, mat, slight, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft, bi, bt,
                                   work, c_shadow, outcome, color, refl, no, nd, nkey);
     const unsigned sidx = pix + ca.fpx;
     bool defer = false;
@@ -967,7 +1057,7 @@ constexpr int wg_waves() {
   return kLdsGeo ? 4 : 1;
 }
 
-template <bool kLdsGeo, bool kCull, int kSamples, int kStack, bool kFast = false>
+template <bool kLdsGeo, bool kCull, int kSamples, int kStack, bool kFast = false, bool kWide = false>
 __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) void render_kernel(
     const RenderArgs a) {
   // Workgroups are dealt to the 8 XCDs round robin (b % 8), so every image
@@ -1042,7 +1132,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
     // the wave's ray queue sits where trace_wave parks colours, after the
     // finished-pixel bytes (launch_tiles)
     QRay *q = reinterpret_cast<QRay *>(reinterpret_cast<unsigned char *>(ca.park) + kPixbufBytes);
-    merge_tiles<kCull, kFast>(g, rad, sm, slight, a, slot, frame, ca, q, work, sums);
+    merge_tiles<kCull, kFast, kWide>(g, rad, sm, slight, a, slot, frame, ca, q, work, sums);
   } else {
     trace_tile<kCull, kSamples, kStack, !kLdsGeo>(g, rad, sm, slight, a.n, a.nl, a.amb, kernarg_cam(frame), a.W, a.H,
                                                   a.depth, a.rows, bv, a.lg, a.od,
@@ -1066,7 +1156,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
 // queue slot's [level][slot] entries of dstack), unwinds the chain's whole
 // stack -- the levels merge_tiles copied there at the deferral first -- and
 // stores the pixel.
-template <bool kCull, bool kFast = false>
+template <bool kCull, bool kFast = false, bool kWide = false>
 __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const RenderArgs a) {
   const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards;
   const int cap = a.dq_cap;
@@ -1115,8 +1205,8 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const
       int outcome = 0, nkey = 0;
       D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
       double refl = 0.0;
-      bounce<kCull, true, kFast>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key, dleft,
-                          work, c_shadow, outcome, color, refl, no, nd, nkey);
+      bounce<kCull, true, kFast, kWide>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, act, o, d, key,
+                                        dleft, work, c_shadow, outcome, color, refl, no, nd, nkey);
       if (act) {
         StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, dstack)>(a.dstack);
         if (outcome == kSpawned) {
@@ -2021,7 +2111,16 @@ struct rt_ctx {
   // (merge_end); 0: four per wave to the end.  RT_HIP_TAIL_WAVES (tuning build)
   int tail = 1;
   int tail_waves = 12;
-  int pair_class = -1;  // RT_HIP_PAIR_CLASS (tuning build): tiles of classes [pair_class, single class) two per wave
+  // RT_HIP_PAIR_CLASS (tuning build): tiles of classes [pair_class, single
+  // class) two per wave (slower: profiles/r5n)
+  int pair_class = -1;
+  // RT_HIP_WIDE (tuning build): the render kernel whose sparse waves spread
+  // their light loop over the lanes (shade_hit kWide).  3 (default): the
+  // render and the deferred kernels of every fp64 launch; 2: the render kernel
+  // only; 1: one-frame launches only; 0: the lane-per-ray loop (synth200 one
+  // frame 0.297 -> 0.279 ms, 20 frames 0.1965 -> 0.1932 ms per frame; complex
+  // 0.1797 -> 0.1755; profiles/r5o, profiles/r5p/ab_wide.log)
+  int wide_mode = 3;
   // RT_HIP_XCD_FRAMES: multi-frame launches put every frame of a tile group on
   // one XCD (render_kernel).  -1 (default): for scenes with the uniform grid
   // (large scenes, whose lists and nodes outgrow an XCD's L2: synth10k 2.58 ->
@@ -2978,9 +3077,12 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     // the default configuration (ordered 4-wide BVH walk, light grids) has kernels
     // compiled with only those paths (kFast): no registers held for the others
     const bool fast = bv.ordered && bv.wide && lg.on;
+    // the light loop of sparse waves spread over the lanes (shade_hit kWide, the default)
+    const bool wide = fast && (c->wide_mode >= 2 || (nf == 1 && c->wide_mode == 1));
     if (depth > 1) {  // the stack homes: 2 x the render kernel's resident waves
-      const void *kf = fast ? reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack, true>)
-                            : reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack>);
+      const void *kf = wide   ? reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack, true, true>)
+                       : fast ? reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack, true>)
+                              : reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack>);
       if (kf != c->occ_kernel || lds != c->occ_lds) {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kf, 64 * kWg, lds) != hipSuccess || nb < 1) {
@@ -3029,7 +3131,10 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       ra.sg = SgArgs{c->d_sg_start, c->d_sg_ent, c->d_sg_rho2, c->sg_n, 1, c->sg_nstart, c->sg_nent, c->nsph};
     c->cg_last = ra.cg.on != 0;
     c->cg_last_n = ra.cg.on ? ra.cg.N : 0;
-    if (fast)
+    if (wide)
+      hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, true, true>), grid, dim3(64 * kWg), lds, c->stream,
+                         ra);
+    else if (fast)
       hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, true>), grid, dim3(64 * kWg), lds, c->stream, ra);
     else
       hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
@@ -3041,6 +3146,9 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
         hipLaunchKernelGGL(render_deferred_walk, dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
       else if (kCull && fast && c->defer_grid && bv.ug.on && bv.ug.closest)  // the same with grid walks
         hipLaunchKernelGGL(render_deferred_grid, dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
+      else if (fast && c->wide_mode == 3)  // the deferred waves' tails spread their light loops too
+        hipLaunchKernelGGL((render_deferred<kCull, true, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream,
+                           ra);
       else if (fast)
         hipLaunchKernelGGL((render_deferred<kCull, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
       else
@@ -3194,6 +3302,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_XCD_FRAMES")) c->xcd_frames = std::max(-1, std::min(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_TAIL")) c->tail = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_TAIL_WAVES")) c->tail_waves = std::max(1, std::min(64, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_WIDE")) c->wide_mode = std::max(0, std::min(3, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_PAIR_CLASS")) c->pair_class = std::max(-1, std::min(kSchedClasses, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER_DIV")) c->defer_div = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_GRID_CELLS")) c->ug_cells = std::max(0.05, std::min(64.0, std::atof(e)));

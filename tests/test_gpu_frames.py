@@ -310,3 +310,66 @@ def test_camera_grid_fallbacks(monkeypatch, env):
             assert frames[f].tobytes() == want, f"frame {f}: {diff_summary(frames[f].tobytes(), want)}"
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("name", ["synth200_1920x1080_d4", "complex_1920x1080_d4", "complex_1280x720_d10",
+                                  "mirrorfrac_320x240_d6", "complexfrac_960x540_d4", "medium_1920x1080_d2",
+                                  "simple_800x600_d10", "synth10k_384x216_d6", "simple_2x2_d10"])
+def test_wide_light_loop(monkeypatch, name):
+    """The default kernels spread the light loop of sparse waves over their
+    lanes (shade_hit kWide: a lane per (hit, light) for the shadow query and
+    the Phong terms, each hit lane adding its lights' terms in file order,
+    scene.h:94-120).  Against the reference's image and against the
+    lane-per-ray loop (RT_HIP_WIDE=0, tuning build) from moved cameras, one
+    frame and three per launch, ray counts included."""
+    import rt_hip
+
+    m = manifest()[name]
+    W, H, D = m["width"], m["height"], m["depth"]
+    r = rt_hip.Renderer(0)
+    monkeypatch.setenv("RT_HIP_WIDE", "0")
+    narrow = rt_hip.Renderer(0, variant="tuning")
+    try:
+        sc, _ = _load(r, name)
+        narrow.upload(sc)
+        rgb, st = _single(r, sc.camera(), W, H, D)
+        assert rgb == golden_rgb(name), diff_summary(rgb, golden_rgb(name))
+        for k in (1, -2):
+            cam = _moved(sc.camera(), 0.3 * k)
+            rgb, st = _single(r, cam, W, H, D)
+            want, st0 = _single(narrow, cam, W, H, D)
+            assert rgb == want, diff_summary(rgb, want)
+            assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (st0.rays_primary, st0.rays_shadow,
+                                                                          st0.rays_reflect)
+        cams = [_moved(sc.camera(), 0.2 * k) for k in range(3)]
+        frames, _, _ = _frames(r, cams, W, H, D)
+        want, _, _ = _frames(narrow, cams, W, H, D)
+        for f in range(len(cams)):
+            assert frames[f].tobytes() == want[f].tobytes(), f"frame {f}"
+    finally:
+        r.close()
+        narrow.close()
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_wide_mirror_cloud_vs_oracle(seed):
+    """A camera inside a cloud of mirrors (most waves' deeper levels sparse,
+    many rays deferred): the default (wide light loop) kernels against the
+    oracle."""
+    import orc
+    import rt_hip
+    from test_gpu_parity import _mirror_cloud
+
+    text = _mirror_cloud(seed, 180, frac=seed == 4)
+    sc = rt_hip.Scene.parse(text)
+    r = rt_hip.Renderer(0)
+    try:
+        r.upload(sc)
+        W, H, D = 160, 120, 7
+        rgb, st = _single(r, sc.camera(), W, H, D)
+        want, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=16)
+        assert rgb == want, diff_summary(rgb, want)
+        assert (st.rays_primary, st.rays_shadow, st.rays_reflect) == (counts["primary"], counts["shadow"],
+                                                                      counts["reflect"])
+    finally:
+        r.close()
