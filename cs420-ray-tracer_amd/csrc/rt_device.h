@@ -250,7 +250,7 @@ __device__ __forceinline__ double min1(double x) { return (x < 1.0) ? x : 1.0; }
 
 // Sphere::intersect (sphere.h:26-59) for a ray whose a = dot(d,d) is hoisted:
 // a4 = 4*a, a2 = 2*a (both exact scalings).  Returns true and t on a hit.
-__device__ __forceinline__ bool intersect(const SphGeo &s, D3 o, D3 d, double a4, double a2, double &t) {
+__host__ __device__ __forceinline__ bool intersect(const SphGeo &s, D3 o, D3 d, double a4, double a2, double &t) {
   double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
   double b = 2.0 * ((ocx * d.x + ocy * d.y) + ocz * d.z);
   double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.rr;
@@ -277,17 +277,37 @@ __device__ __forceinline__ bool intersect(const SphGeo &s, D3 o, D3 d, double a4
 // zero nor change sign, so the root choice of sphere.h:51-57 (t2 < 0 -> miss;
 // t = t1 < 0 ? t2 : t1) is made on the numerators: t = fl(num / a2).
 // Returns 0 = miss, 1 = hit with numerator `num`, 2 = "decide with the exact
-// intersect()" (a numerator too close to zero, or a2 out of range).
+// intersect()" (a numerator too close to zero, or a2 out of range), 3 = a hit
+// whose t lies below the caller's bound (qocc, see below), num not formed.
+// Two cases of disc > 0 are decided without the square root:
+//  * b > 0 with disc < b^2 (1 - 2^-50) (b^2 normal): sqrt(disc) rounds below
+//    b, so n2 = -b + sq < 0 and both roots are negative: a miss (the same
+//    bound as shadow_cells' own-sphere test).  Spheres behind the origin
+//    that the line runs through (the sorted lists' behind entries, the light
+//    lists' spheres beyond the shaded point) end here;
+//  * c > 0 and b < 0 (the origin outside, the centre ahead): disc =
+//    fl(b^2 - fl(a4 c)) <= fl(b^2), so sq <= fl(sqrt(fl(b^2))) = |b| and
+//    0 <= n1 = fl(|b| - sq) <= |b|: the reference's t is t1 = fl(n1/a2) >= 0
+//    (also through intersect() when n1 is tiny).  With -b below qocc (a
+//    shadow query's q(1-2^-48), where a numerator gives t < T) that is an
+//    occluder.  qocc < 0 (closest hits) never takes it.
 constexpr double kTinyNum = 0x1p-900;
-__device__ __forceinline__ int intersect_num(const SphGeo &s, D3 o, D3 d, double a4, double &num) {
+__host__ __device__ __forceinline__ int intersect_num(const SphGeo &s, D3 o, D3 d, double a4, double &num,
+                                                      double qocc = -1.0) {
   double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
   double b = 2.0 * ((ocx * d.x + ocy * d.y) + ocz * d.z);
   double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.rr;
-  double disc = b * b - a4 * c;
+  double p = b * b;
+  double disc = p - a4 * c;
   if (!(disc >= 0.0)) return 0;
   if (disc == 0.0) {
     num = -b;  // t = -b / a2, negative roots included (sphere.h:43-47)
     return 1;
+  }
+  if (b > 0.0) {
+    if (p > 1e-290 && disc < p * (1.0 - 0x1p-50)) return 0;
+  } else if (c > 0.0 && -b < qocc) {
+    return 3;
   }
   double sq = __builtin_sqrt(disc);
   double n1 = -b - sq, n2 = -b + sq;
@@ -296,7 +316,7 @@ __device__ __forceinline__ int intersect_num(const SphGeo &s, D3 o, D3 d, double
   num = (n1 < 0.0) ? n2 : n1;
   return 1;
 }
-__device__ __forceinline__ bool a2_ok(double a2) { return a2 >= 0x1p-60 && a2 <= 0x1p60; }
+__host__ __device__ __forceinline__ bool a2_ok(double a2) { return a2 >= 0x1p-60 && a2 <= 0x1p60; }
 
 // ---------------------------------------------------------------------------
 // Wave-wide reductions.  Called only where all 64 lanes are active.
@@ -1479,8 +1499,10 @@ __device__ __forceinline__ bool sweep_shadow(const SphGeo *__restrict__ g, const
   bool occ = false;
   auto test = [&](int i) {
     double num;
-    const int r = fast ? intersect_num(g[RT_CK(kCkSphere, i, n)], o, d, a4, num) : 2;
-    if (r == 1) {
+    const int r = fast ? intersect_num(g[RT_CK(kCkSphere, i, n)], o, d, a4, num, qlo) : 2;
+    if (r == 3) {
+      occ = true;
+    } else if (r == 1) {
       if (num < qlo) occ = true;
       else if (!(num > qhi)) {
         const double t = num / a2;
@@ -1641,8 +1663,10 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
   bool occ = false;
   auto test = [&](int i) {
     double num;
-    const int r = fast ? intersect_num(g[RT_CK(kCkSphere, i, n)], o, d, a4, num) : 2;
-    if (r == 1) {
+    const int r = fast ? intersect_num(g[RT_CK(kCkSphere, i, n)], o, d, a4, num, qlo) : 2;
+    if (r == 3) {
+      occ = true;
+    } else if (r == 1) {
       if (num < qlo) occ = true;
       else if (!(num > qhi)) {
         const double t = num / a2;

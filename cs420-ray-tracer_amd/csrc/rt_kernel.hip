@@ -201,6 +201,14 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
     const SphMat m0 = mat[hi];
     col = mul(amb, mk(m0.cr, m0.cg, m0.cb));                   // scene.h:91
   }
+  // the normal (sphere.h:62-64), used by the shading and by the reflection
+  // (main.cpp:44-46: the same expression, formed once), and the view direction
+  D3 nrm = mk(0.0, 0.0, 0.0), view = nrm;
+  if (hit) {
+    const SphGeo sg = g[hi];
+    nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));
+    view = normalized(sub(o, hp));  // main.cpp:38
+  }
     // scene.h:94-120: per light in file order, the shadow query then (if lit)
     // the Phong terms with the same ldir -- skipped by a wave (or the active
     // lanes of one) whose rays all left the scene
@@ -213,12 +221,6 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
       if (nl >= 2 && lpp >= 2 && lgw.on) {                   // wave-uniform
         const int lane = (int)(threadIdx.x & 63);
         const int rank = (int)__popcll(hm & ((1ull << lane) - 1ull));
-        D3 nrm = mk(0.0, 0.0, 0.0), view = nrm;
-        if (hit) {
-          const SphGeo sg = g[hi];
-          nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
-          view = normalized(sub(o, hp));                       // main.cpp:38
-        }
         for (int l0 = 0; l0 < nl; l0 += lpp) {  // lights l0 .. l0 + cnt - 1 in this pass
           const int cnt = nl - l0 < lpp ? nl - l0 : lpp;
           const bool helper = lane < nh * cnt;
@@ -270,10 +272,7 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
       }
     }
     if (!wide_done && __ballot(hit)) {
-      const SphGeo sg = g[hi];
       const SphMat m = mat[hi];
-      const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));  // sphere.h:62-64
-      const D3 view = normalized(sub(o, hp));                       // main.cpp:38
       const D3 mc = mk(m.cr, m.cg, m.cb);
       LgRange next{0, 0};
       {
@@ -335,8 +334,6 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
       color = A;  // with no depth left trace_ray(depth 0) is black: A + (0,0,0)*refl == A
       outcome = kEnded;
       if (dleft - 1 >= 1) {
-        const SphGeo sg = g[hi];
-        const D3 nrm = normalized(sub(hp, mk(sg.cx, sg.cy, sg.cz)));
         const D3 rd = sub(d, scale(scale(nrm, 2.0), dot(d, nrm)));
         no = add(hp, scale(nrm, kEps));
         nd = renormalized(rd);

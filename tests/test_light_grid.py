@@ -131,6 +131,30 @@ def test_own_sphere_pretest_agrees_with_reference(tmp_path):
     assert w[-1] == "0", out.stdout
 
 
+def test_sqrt_free_decisions_agree_with_reference(tmp_path):
+    """intersect_num decides two cases of disc > 0 without the square root
+    (rt_device.h): b > 0 with disc < b^2 (1 - 2^-50) is a miss (both roots
+    negative), and c > 0, b < 0 with -b below a shadow query's bound is an
+    occluder (0 <= n1 <= -b).  On 8M shadow pairs (spheres along the query's
+    line: between the point and the light, beyond either, through the origin,
+    grazing within |r| 10^-15, exactly tangent to axis-aligned lines) and 16M
+    closest-hit pairs, the decisions equal the reference's test (sphere.h:26-59,
+    scene.h:78-82) and every returned numerator gives its t exactly
+    (tests/native/num_check.cpp)."""
+    exe = tmp_path / "num_check"
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-I",
+                    os.path.join(REPO, "cs420-ray-tracer_amd", "csrc"), "-I", os.path.join(REPO, "include"), "-o",
+                    str(exe), os.path.join(REPO, "tests", "native", "num_check.cpp")], check=True)
+    out = subprocess.run([str(exe), "1000000"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    sh, cl = out.stdout.strip().splitlines()[-2:]
+    w = sh.split()
+    assert w[0] == "shadow" and int(w[1]) > 7000000 and int(w[5]) > 500000 and int(w[7]) > 500000, sh
+    assert w[-1] == "0", sh
+    c = cl.split()
+    assert c[0] == "closest" and int(c[3]) > 5000000 and c[-1] == "0", cl
+
+
 def test_camera_grid_lists_and_scan(tmp_path):
     """Camera grid (rt_lightgrid.h build_point_grid, rt_device.h cam_closest):
     every sphere the reference's test reports a hit for on a camera ray, with
