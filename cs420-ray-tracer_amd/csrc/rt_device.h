@@ -1592,6 +1592,7 @@ struct LgArgs {
   int on;          // 0: shadow rays use sweep_shadow
   double max_off;  // largest distance of a ray's line from its light the grid margins cover
   long long nstart, nids;  // CSR starts and list ids (RT_CHECK bounds)
+  int off_free;    // 1: every query's line provably within max_off of its light (the host's bound, below)
 };
 
 // The cell list a shadow query of light l from point hp will test: the cell
@@ -1712,14 +1713,22 @@ __device__ __forceinline__ bool shadow_cells(const SphGeo *__restrict__ g, int n
     const int N = lg.N, cells = 6 * N * N;
     const int32_t *st = lg.start + (size_t)l * (size_t)(cells + 2);
     // The line o + t d passes (up to rounding) through the light; the grid's
-    // margins assume it does within max_off -- checked here, per ray.
-    const D3 w = sub(lp, o);
-    const double off = __builtin_fabs(w.y * d.z - w.z * d.y) + __builtin_fabs(w.z * d.x - w.x * d.z) +
-                       __builtin_fabs(w.x * d.y - w.y * d.x);
+    // margins assume it does within max_off -- checked here, per ray, unless
+    // the host has bounded it for the whole scene (off_free: |hit point|,
+    // |light| <= B, so the line's distance from the light, as computed here,
+    // is below 60 u (4B + 2 EPSILON) + the cross product's rounding, far
+    // under 2^-41 (1.01 B + 0.01) <= max_off; tests/native/num_check.cpp)
+    bool off_ok = true;
+    if (!lg.off_free) {
+      const D3 w = sub(lp, o);
+      const double off = __builtin_fabs(w.y * d.z - w.z * d.y) + __builtin_fabs(w.z * d.x - w.x * d.z) +
+                         __builtin_fabs(w.x * d.y - w.y * d.x);
+      off_ok = off <= lg.max_off;
+    }
     // the cell's list (first id prefetched), then the global list; a lane
     // whose line cannot use the grid tests every sphere (ids 0 .. n-1) in the
     // same loop
-    const bool all = !(off <= lg.max_off) || cell.cb < 0;
+    const bool all = !off_ok || cell.cb < 0;
     const int cl = RT_CK(kCkLgStart, cells, lg.nstart - 1 - (long long)l * (cells + 2));
     const int gb = st[cl], ge = st[cl + 1];
     const int len1 = all ? n : cell.ce - cell.cb, len = all ? n : len1 + (ge - gb);

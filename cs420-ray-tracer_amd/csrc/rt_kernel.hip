@@ -1952,6 +1952,7 @@ struct rt_ctx {
   long long lg_nstart = 0, lg_nids = 0;
   int lg_n_opt = 0;            // RT_HIP_SHADOW_GRID_N; 0 = 128, or 768 above kBvhAlwaysAbove spheres
   double lg_max_off = 0.0;
+  bool lg_off_free = false;  // shadow queries skip the per-ray max_off check (light_grids)
   // camera grids (rt_device.h CgArgs), built on the device per camera
   // position of a launch (cg_bin_kernel / cg_sort_kernel) and kept while the
   // positions and the scene stay the same
@@ -2261,6 +2262,7 @@ LgArgs lg_args(const rt_ctx *c) {
   g.N = c->lg_n;
   g.on = (c->lg_on && c->cull && c->d_lg_start) ? 1 : 0;
   g.max_off = c->lg_max_off;
+  g.off_free = c->lg_off_free ? 1 : 0;
   g.nstart = c->lg_nstart;
   g.nids = c->lg_nids;
   return g;
@@ -2779,6 +2781,15 @@ int light_grids(rt_ctx *c, const rt_scene *s, double diam) {
   const int n = s->num_spheres, nl = s->num_lights, N = c->lg_n;
   const long long cells = 6LL * N * N;
   c->lg_max_off = std::isfinite(diam) ? 1e-7 * diam : 0.0;
+  {
+    // every hit point lies on a finite sphere, inside the scene box up to
+    // rounding, and every light inside it: with B the box's largest |coordinate|
+    // the shadow lines' computed distance from their light stays below
+    // 2^-41 (1.01 B + 0.01) (shadow_cells), so the per-ray check can go
+    double B = 0.0;
+    for (int k = 0; k < 3; k++) B = std::max(B, std::max(std::fabs(c->lo[k]), std::fabs(c->hi[k])));
+    c->lg_off_free = std::isfinite(B) && c->lg_max_off > 0.0 && 0x1p-41 * (1.01 * B + 0.01) <= c->lg_max_off;
+  }
   const double dm = std::isfinite(diam) ? diam : 0.0;
   std::vector<GridPt> pts((size_t)nl);
   std::vector<unsigned char> allglob((size_t)nl);
@@ -3807,6 +3818,8 @@ int rt_get_info(rt_ctx *c, rt_info *out) {
   out->scratch_bytes = (uint64_t)(c->cstack_bytes + c->dq_bytes + c->homes_bytes +
                                   (size_t)c->home_words * sizeof(unsigned long long) + c->cg_count_cap + c->cg_ent_cap +
                                   c->cg_disks_cap + c->cg_pairs_cap + c->cg_npairs_cap + c->perm_cap);
+  out->shadow_line_bounded = c->lg_off_free ? 1 : 0;
+  out->reserved0 = 0;
   return RT_OK;
 }
 

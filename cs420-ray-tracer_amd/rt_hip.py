@@ -28,7 +28,7 @@ VARIANTS = {"tuning": os.path.join(HERE, "variants", "librt_hip_tuning.so"),
             "check": os.path.join(HERE, "variants", "librt_hip_check.so")}
 
 RT_MAX_DEPTH = 64
-ABI_VERSION = 11  # RT_HIP_ABI_VERSION in include/rt_hip.h
+ABI_VERSION = 12  # RT_HIP_ABI_VERSION in include/rt_hip.h
 MAX_FRAMES = 32  # RT_MAX_FRAMES
 
 
@@ -68,7 +68,8 @@ class rt_info(C.Structure):
                 ("sphere_grid_build_ms", C.c_double), ("behind_grid", C.c_int32), ("behind_grid_last", C.c_int32),
                 ("behind_grid_cells", C.c_uint64), ("behind_grid_entries", C.c_uint64),
                 ("behind_grid_build_ms", C.c_double), ("bvh_build_ms", C.c_double),
-                ("light_grid_build_ms", C.c_double), ("scratch_bytes", C.c_uint64)]
+                ("light_grid_build_ms", C.c_double), ("scratch_bytes", C.c_uint64),
+                ("shadow_line_bounded", C.c_int32), ("reserved0", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

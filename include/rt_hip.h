@@ -52,10 +52,11 @@
 extern "C" {
 #endif
 
-#define RT_HIP_ABI_VERSION 11 /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
+#define RT_HIP_ABI_VERSION 12 /* 4: the reference hybrid interface (rt_hip_compat.h); 5: rt_rows_for_shard;
                                    6: rt_render_tiles; 7: rt_get_info; 8: rt_info sphere-grid fields;
                                    9: rt_info behind-grid fields; 10: RT_ERR_CHECK;
-                                   11: rt_info BVH / light-grid build times, scratch bytes */
+                                   11: rt_info BVH / light-grid build times, scratch bytes;
+                                   12: rt_info shadow_line_bounded */
 /* Longest reflection chain the GPU path keeps per pixel (depth <= RT_MAX_DEPTH). */
 #define RT_MAX_DEPTH 64
 
@@ -284,6 +285,9 @@ typedef struct rt_info {
     double light_grid_build_ms;  /* host wall time of the light grids' build and upload, part of upload_ms */
     uint64_t scratch_bytes;      /* device scratch the context holds for its launches: reflection stacks (stack
                                     homes / per-pixel stack), the deferred queue, the camera grids, the tile order */
+    int32_t shadow_line_bounded; /* 1: the scene's bound keeps every shadow line within its light grid's margin, so
+                                    the per-ray check is skipped (rt_device.h shadow_cells off_free); 0: checked */
+    int32_t reserved0;
 } rt_info;
 int rt_get_info(rt_ctx *ctx, rt_info *out);
 

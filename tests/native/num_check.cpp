@@ -12,8 +12,9 @@
 //    "occluded" for every pair;
 //  * closest hits (qocc < 0): a returned numerator gives the reference's t
 //    exactly (fl(num / a2)), a miss is a miss.
-// Prints "shadow <pairs> occluded <k> early <e> skipped <s> wrong <w>" and
-// "closest <pairs> hits <h> skipped <s> wrong <w>".
+// Also the bound behind shadow_cells' off_free (below).  Prints "shadow
+// <pairs> occluded <k> early <e> skipped <s> wrong <w>", "closest <pairs> hits
+// <h> skipped <s> wrong <w>" and "off <queries> max_ratio <r> wrong <w>".
 //   hipcc -O2 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I csrc num_check.cpp
 #include <cmath>
 #include <cstdio>
@@ -183,7 +184,47 @@ int main(int argc, char **argv) {
       }
     }
   }
+  // shadow_cells' off_free bound: for scenes at scales 1e-3 .. 1e5, centred
+  // up to 1e6 scene sizes from the origin, hit points on spheres (a ray's
+  // hit, o + d t) and lights in the box, the line's distance from its light as
+  // shadow_cells computes it stays below 2^-41 (1.01 B + 0.01), B the box's
+  // largest |coordinate| (the host then skips the per-ray check when that is
+  // <= max_off)
+  long off_n = 0, off_wrong = 0;
+  double off_ratio = 0.0;
+  for (long it = 0; it < N / 4; ++it) {
+    const double scale = std::pow(10.0, -3.0 + 8.0 * U01(rng));
+    const V ctr = scl(rdir(), scale * std::pow(10.0, 6.0 * U01(rng)) * (U01(rng) < 0.3 ? 0.0 : 1.0));
+    const V c = add(ctr, scl({U(rng), U(rng), U(rng)}, scale));
+    const double r = scale * std::pow(10.0, -3.0 * U01(rng));
+    const V L = add(ctr, scl({U(rng), U(rng), U(rng)}, scale * 2.0));
+    // the box of the sphere and the light
+    double B = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      const double ck = k == 0 ? c.x : k == 1 ? c.y : c.z, lk = k == 0 ? L.x : k == 1 ? L.y : L.z;
+      B = std::max(B, std::max(std::fabs(ck) + r, std::fabs(lk)));
+    }
+    const V o0 = add(c, scl(rdir(), r * (1.0 + 10.0 * U01(rng))));
+    const V d0 = unit(sub(add(c, scl(rdir(), r * U01(rng))), o0));
+    double t0;
+    if (!ref_hit(c, r * r, o0, d0, t0) || !(t0 > 0)) continue;
+    const V hp = add(o0, scl(d0, t0));
+    const V to_light = sub(L, hp);
+    const double len = std::sqrt((to_light.x * to_light.x + to_light.y * to_light.y) + to_light.z * to_light.z);
+    if (!(len > 0)) continue;
+    const V ldir = {to_light.x / len, to_light.y / len, to_light.z / len};
+    const V o = add(hp, scl(ldir, 0.001)), d = unit(ldir);  // Ray(): direction normalised again
+    const V w = sub(L, o);
+    const double off = std::fabs(w.y * d.z - w.z * d.y) + std::fabs(w.z * d.x - w.x * d.z) +
+                       std::fabs(w.x * d.y - w.y * d.x);
+    const double bound = 0x1p-41 * (1.01 * B + 0.01);
+    ++off_n;
+    off_ratio = std::max(off_ratio, off / bound);
+    if (!(off <= bound) && ++off_wrong <= 5)
+      std::printf("off wrong: B %.17g off %.17g bound %.17g\n", B, off, bound);
+  }
   std::printf("shadow %ld occluded %ld early %ld skipped %ld wrong %ld\n", sh, sh_occ, sh_early, sh_skip, sh_wrong);
   std::printf("closest %ld hits %ld skipped %ld wrong %ld\n", cl, cl_hit, cl_skip, cl_wrong);
-  return (sh_wrong || cl_wrong) ? 1 : 0;
+  std::printf("off %ld max_ratio %.3g wrong %ld\n", off_n, off_ratio, off_wrong);
+  return (sh_wrong || cl_wrong || off_wrong) ? 1 : 0;
 }

@@ -414,6 +414,41 @@ def test_bvh_far_from_origin(bvh_renderer):
     assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
 
 
+@pytest.mark.parametrize("offset,bounded", [(0, 1), (100000, 1), (100000000, 0)])
+def test_shadow_line_check_paths(offset, bounded):
+    """shadow_cells skips its per-ray check that a shadow line passes within
+    the light grid's margin of its light when the host bounds it for the whole
+    scene (rt_info.shadow_line_bounded: 2^-41 (1.01 B + 0.01) <= 1e-7 x the
+    scene diameter, B the box's largest |coordinate|).  A scene at the origin
+    and 1e5 away takes the bounded path, 1e8 away (B / diameter ~ 3e6) the
+    checked one; both against the oracle (scene.h:65-86), image and shadow
+    ray count."""
+    import orc
+    import rt_hip
+
+    lines = []
+    for i in range(40):
+        lines.append("sphere %d %d %d 0.7 0.5 0.5 0.9 0.3 0.5 20" % (offset + (i % 7) * 2, offset + (i // 7),
+                                                                     -offset - 20 - (i % 5) * 3))
+    lines += ["light %d %d %d 1 1 1 1" % (offset + 10, offset + 20, -offset),
+              "light %d %d %d 0.5 0.6 0.7 1" % (offset - 10, offset + 10, -offset - 5),
+              "camera %d %d %d %d %d %d 50" % (offset + 4, offset + 3, -offset + 10, offset + 4, offset + 3,
+                                              -offset - 20)]
+    text = "\n".join(lines) + "\n"
+    sc = rt_hip.Scene.parse(text)
+    r = rt_hip.Renderer(0)
+    try:
+        r.upload(sc)
+        assert r.info().shadow_line_bounded == bounded
+        W, H, D = 96, 64, 6
+        ref, counts, _ = orc.OracleScene(text=text).render(W, H, D, threads=4)
+        rgb, st = r.render(sc.camera(), W, H, D)
+        assert bytes(rgb) == ref, diff_summary(bytes(rgb), ref)
+        assert st.rays_shadow == counts["shadow"]
+    finally:
+        r.close()
+
+
 # the layouts the product reaches without a knob (the global stack: tiles,
 # antialias; scanline order: launches under 1,024 tiles; an 8-entry merge
 # queue: scenes whose walk stacks fill the LDS; deferral on / off: multi- /

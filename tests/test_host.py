@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     lib = rt_hip.lib()
     for n in names:
         getattr(lib, n)
-    assert lib.rt_abi_version() == rt_hip.ABI_VERSION == 11
+    assert lib.rt_abi_version() == rt_hip.ABI_VERSION == 12
 
 
 def test_error_strings():

@@ -139,7 +139,8 @@ def test_sqrt_free_decisions_agree_with_reference(tmp_path):
     line: between the point and the light, beyond either, through the origin,
     grazing within |r| 10^-15, exactly tangent to axis-aligned lines) and 16M
     closest-hit pairs, the decisions equal the reference's test (sphere.h:26-59,
-    scene.h:78-82) and every returned numerator gives its t exactly
+    scene.h:78-82) and every returned numerator gives its t exactly; and the
+    bound that lets shadow_cells skip its per-ray line check (off_free) holds
     (tests/native/num_check.cpp)."""
     exe = tmp_path / "num_check"
     subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-I",
@@ -147,12 +148,15 @@ def test_sqrt_free_decisions_agree_with_reference(tmp_path):
                     str(exe), os.path.join(REPO, "tests", "native", "num_check.cpp")], check=True)
     out = subprocess.run([str(exe), "1000000"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
-    sh, cl = out.stdout.strip().splitlines()[-2:]
+    sh, cl, off = out.stdout.strip().splitlines()[-3:]
     w = sh.split()
     assert w[0] == "shadow" and int(w[1]) > 7000000 and int(w[5]) > 500000 and int(w[7]) > 500000, sh
     assert w[-1] == "0", sh
     c = cl.split()
     assert c[0] == "closest" and int(c[3]) > 5000000 and c[-1] == "0", cl
+    # shadow_cells' off_free: the computed line-to-light distance under 2^-41 (1.01 B + 0.01)
+    f = off.split()
+    assert f[0] == "off" and int(f[1]) > 100000 and float(f[3]) < 0.01 and f[-1] == "0", off
 
 
 def test_camera_grid_lists_and_scan(tmp_path):
