@@ -1686,7 +1686,7 @@ __global__ __launch_bounds__(256) void cg_sort_kernel(const CgBuild a) {
 //                    1 per listed cell, <fill> takes a slot there and writes
 //                    the entry at the cell's CSR offset
 //   scan_*           the exclusive prefix of the counts (CSR offsets)
-//   sg_sort_kernel / ids_sort_kernel   a thread per list: (tlo, index) / index order
+//   sg_sort_kernel / ids_sort_kernel   a thread per list: (tlo, index) / (nearest distance, index) order
 //   sg_start_kernel / lg_start_kernel  the host builders' start arrays
 struct GridPt {  // a grid's point and origin-ball radius
   double x, y, z, rho;
@@ -1885,16 +1885,30 @@ __global__ __launch_bounds__(256) void lg_start_kernel(const int *off, int nl, l
   start[k] = off[l * (cells + 1) + c];  // c = cells + 1: the next light's first offset (or the total)
 }
 
-// A thread per list: ascending ids (insertion sort).
-__global__ __launch_bounds__(256) void ids_sort_kernel(const int *off, long long nlists, int32_t *ids) {
+// A thread per list: ascending ids (insertion sort); with `near` (light
+// grids) ascending by the sphere's nearest distance from the grid's point
+// (|C - P| - |r|, then the id), so a shadow query meets the spheres between
+// its point and the light before those beyond it -- the lists' order is free:
+// a shadow query is an any-hit test (scene.h:78-82).
+__device__ __forceinline__ double near_key(const SphGeo *geo, const GridPt &p, int i) {
+  const SphGeo s = geo[i];
+  const double dx = s.cx - p.x, dy = s.cy - p.y, dz = s.cz - p.z;
+  return __builtin_sqrt(dx * dx + dy * dy + dz * dz) - __builtin_sqrt(s.rr);
+}
+__global__ __launch_bounds__(256) void ids_sort_kernel(const int *off, long long nlists, int32_t *ids,
+                                                       const SphGeo *geo, const GridPt *pts, long long row, int near) {
   const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gc >= nlists) return;
   int32_t *e = ids + off[gc];
   const int cnt = off[gc + 1] - off[gc];
+  const GridPt p = near ? pts[gc / row] : GridPt{};
   for (int k = 1; k < cnt; ++k) {
     const int32_t x = e[k];
+    const double kx = near ? near_key(geo, p, x) : 0.0;
     int m = k - 1;
-    while (m >= 0 && e[m] > x) {
+    while (m >= 0) {
+      const double km = near ? near_key(geo, p, e[m]) : 0.0;
+      if (!(kx < km || (!(km < kx) && x < e[m]))) break;
       e[m + 1] = e[m];
       --m;
     }
@@ -1953,6 +1967,10 @@ struct rt_ctx {
   int lg_n_opt = 0;            // RT_HIP_SHADOW_GRID_N; 0 = 128, or 768 above kBvhAlwaysAbove spheres
   double lg_max_off = 0.0;
   bool lg_off_free = false;  // shadow queries skip the per-ray max_off check (light_grids)
+  // RT_HIP_LG_ORDER (tuning build): 1 (default) = light lists nearest first
+  // (ids_sort_kernel; synth10k 2.439 -> 2.386 ms per frame, synth200 and
+  // complex within +-0.3 %, profiles/r5x/ab_lg_order.log), 0 = by sphere index
+  int lg_order = 1;
   // camera grids (rt_device.h CgArgs), built on the device per camera
   // position of a launch (cg_bin_kernel / cg_sort_kernel) and kept while the
   // positions and the scene stay the same
@@ -2556,6 +2574,7 @@ int device_scan(rt_ctx *c, const int *x, long long n, int *y, long long &total) 
 struct PgMode {
   int sides, globlist, max_global;
   size_t max_entries;
+  int near = 0;  // light grids: lists by distance from the point (ids_sort_kernel)
 };
 int point_grids(rt_ctx *c, const std::vector<GridPt> &pts, const std::vector<unsigned char> &allglob, double diam,
                 int N, const PgMode &md, DevScratch &keep, int *&d_off, std::vector<unsigned char> &ok,
@@ -2681,7 +2700,7 @@ int point_grids(rt_ctx *c, const std::vector<GridPt> &pts, const std::vector<uns
   const long long nlists = (long long)ng * row;
   if (md.globlist)
     hipLaunchKernelGGL(ids_sort_kernel, dim3((unsigned)((nlists + 255) / 256)), dim3(256), 0, c->stream, d_off, nlists,
-                       b.ids);
+                       b.ids, c->d_geo, d_pts, row, md.near);
   else
     hipLaunchKernelGGL(sg_sort_kernel, dim3((unsigned)((nlists + 255) / 256)), dim3(256), 0, c->stream, d_off, nlists,
                        b.ent);
@@ -2806,8 +2825,8 @@ int light_grids(rt_ctx *c, const rt_scene *s, double diam) {
     int *d_off = nullptr;
     std::vector<unsigned char> ok;
     void *out = nullptr;
-    int rc = point_grids(c, pts, allglob, dm, N, PgMode{1, 1, INT32_MAX, (size_t)INT32_MAX}, keep, d_off, ok, total,
-                         out);
+    int rc = point_grids(c, pts, allglob, dm, N, PgMode{1, 1, INT32_MAX, (size_t)INT32_MAX, c->lg_order}, keep, d_off,
+                         ok, total, out);
     ids = static_cast<int32_t *>(out);
     c->d_lg_ids = ids;  // owned by the context from here (free_scene)
     if (rc != RT_OK) return rc;
@@ -3311,6 +3330,7 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_TAIL")) c->tail = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_TAIL_WAVES")) c->tail_waves = std::max(1, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_WIDE")) c->wide_mode = std::max(0, std::min(3, std::atoi(e)));
+  if (const char *e = std::getenv("RT_HIP_LG_ORDER")) c->lg_order = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_PAIR_CLASS")) c->pair_class = std::max(-1, std::min(kSchedClasses, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER_DIV")) c->defer_div = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_GRID_CELLS")) c->ug_cells = std::max(0.05, std::min(64.0, std::atof(e)));

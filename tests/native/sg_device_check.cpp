@@ -10,8 +10,9 @@
 // builder (rt_lightgrid.cpp build_sphere_grids, the one rt_upload_scene used
 // before) on random scenes: which spheres get a grid, and for every grid and
 // cell the exact list (sphere, tlo bits) in order.  The light grids (one side,
-// global spheres on a separate list, ids ascending) against build_light_grid:
-// every light's start row and ids, lights with non-finite positions included.
+// global spheres on a separate list, nearest first) against build_light_grid
+// (ids ascending): every light's start row and the same ids in every list,
+// lights with non-finite positions included.
 // Prints "scenes <n> grids <n> refused <n> cells <n> entries <n> differ <n>
 // lights <n> light_entries <n> light_differ <n>".
 #include <algorithm>
@@ -100,7 +101,7 @@ void build_device(const std::vector<double> &cx, const std::vector<double> &cy, 
   }
 }
 // the device build of the light grids: per light, lists for the 6N^2 cells
-// and the global list (index 6N^2), ids ascending
+// and the global list (index 6N^2), nearest first
 std::vector<std::vector<int>> build_device_lights(const std::vector<double> &cx, const std::vector<double> &cy,
                                                   const std::vector<double> &cz, const std::vector<double> &r,
                                                   const std::vector<double> &lx, const std::vector<double> &ly,
@@ -146,7 +147,29 @@ std::vector<std::vector<int>> build_device_lights(const std::vector<double> &cx,
       }
     }
   }
-  for (auto &e : lists) std::sort(e.begin(), e.end());  // ids_sort_kernel
+  // ids_sort_kernel with `near`: each list by (|C - L| - |r|, id), the
+  // kernel's insertion sort and comparison (NaN keys fall back to the id)
+  for (int l = 0; l < nl; l++)
+    for (long long c = 0; c < row; c++) {
+      std::vector<int> &e = lists[(size_t)(l * row + c)];
+      auto key = [&](int i) {
+        const double dx = cx[i] - lx[l], dy = cy[i] - ly[l], dz = cz[i] - lz[l];
+        return std::sqrt(dx * dx + dy * dy + dz * dz) - std::sqrt(r[i] * r[i]);
+      };
+      std::sort(e.begin(), e.end());  // the fill order is arbitrary on the device: start from a fixed one
+      for (size_t k = 1; k < e.size(); ++k) {
+        const int x = e[k];
+        const double kx = key(x);
+        long m = (long)k - 1;
+        while (m >= 0) {
+          const double km = key(e[(size_t)m]);
+          if (!(kx < km || (!(km < kx) && x < e[(size_t)m]))) break;
+          e[(size_t)m + 1] = e[(size_t)m];
+          --m;
+        }
+        e[(size_t)m + 1] = x;
+      }
+    }
   return lists;
 }
 }  // namespace
@@ -256,7 +279,10 @@ int main(int argc, char **argv) {
         const std::vector<int> &e = dl[(size_t)(l * (lcells + 1) + c)];
         same = same && lstart[(size_t)(l * (lcells + 2) + c)] == off &&
                lstart[(size_t)(l * (lcells + 2) + c + 1)] == off + (long long)e.size();
-        for (size_t k = 0; same && k < e.size(); k++) same = lids[(size_t)off + k] == e[k];
+        // the same ids (the host builder's ascending, the device's nearest-first)
+        std::vector<int> asc(e);
+        std::sort(asc.begin(), asc.end());
+        for (size_t k = 0; same && k < asc.size(); k++) same = lids[(size_t)off + k] == asc[k];
         off += (long long)e.size();
         lentries += (long)e.size();
       }

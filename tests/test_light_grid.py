@@ -210,7 +210,9 @@ def test_sphere_grid_device_builder_matches_host(tmp_path):
     build_sphere_grids' list (sphere, tlo bits) in the same order -- so the
     host builder's proofs (tests/native/sg_check.cpp) carry over; and for the
     light grids (1-6 lights per scene, one at a sphere's centre, some
-    non-finite) exactly build_light_grid's start rows and ids
+    non-finite) exactly build_light_grid's start rows and, list by list, the
+    same ids -- the device orders them nearest first (ids_sort_kernel), the
+    host by id; a shadow query is an any-hit test, so the order is free
     (tests/native/lg_check.cpp's proofs carry over)."""
     exe = tmp_path / "sg_device_check"
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-o", str(exe),
@@ -221,7 +223,7 @@ def test_sphere_grid_device_builder_matches_host(tmp_path):
     w = out.stdout.split()
     assert w[0] == "scenes" and int(w[3]) > 3000 and int(w[5]) > 500 and int(w[9]) > 10000000, out.stdout
     assert w[11] == "0", out.stdout
-    # the light grids (one side, a separate global list, ids ascending) against build_light_grid
+    # the light grids (one side, a separate global list, nearest first) against build_light_grid
     assert w[12] == "lights" and int(w[13]) > 300 and int(w[15]) > 5000000 and w[17] == "0", out.stdout
 
 
