@@ -79,7 +79,7 @@ BAND = 8
 WARM_BUSY_S = float(os.environ.get("BENCH_WARM_BUSY_S", "0.05"))
 # the sources the PMC record in profiles/pmc_traffic.json must have been measured with
 KERNEL_SOURCES = ("rt_kernel.hip", "rt_device.h", "rt_cgbuild.h", "rt_bvh.cpp", "rt_bvh.h", "rt_lightgrid.cpp",
-                  "rt_lightgrid.h", "rt_sched.cpp", "rt_sched.h")
+                  "rt_lightgrid.h", "rt_sched.cpp", "rt_sched.h", "Makefile")  # Makefile: the compile flags
 
 
 def kernel_source_sha() -> str:

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Register budget of the render kernels from the code object's own metadata
-(hipcc -S of rt_kernel.hip for gfx950): arch VGPRs (.vgpr_count), AGPRs
+(hipcc -S of rt_kernel.hip for gfx950, the Makefile's flags): arch VGPRs (.vgpr_count), AGPRs
 (.agpr_count; accum_offset = where they would start), SGPRs, spills, and the
 allocation the hardware makes -- VGPRs in granules of 8 on gfx950, 512 per
 SIMD lane, so waves per SIMD = floor(512 / roundup8(vgprs)).  rocprofv3's
@@ -18,7 +18,8 @@ SRC = os.path.join(ROOT, "cs420-ray-tracer_amd", "csrc", "rt_kernel.hip")
 with tempfile.TemporaryDirectory() as tmp:
     out = os.path.join(tmp, "k.s")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                    "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S", "-o", out, SRC] + sys.argv[1:],
+                    "-I" + os.path.join(ROOT, "include"), "-mllvm", "--amdgpu-sched-strategy=max-memory-clause",
+                    "--cuda-device-only", "-S", "-o", out, SRC] + sys.argv[1:],
                    check=True, stderr=subprocess.DEVNULL)
     txt = open(out).read()
 meta = txt[txt.rfind("amdhsa.kernels"):]
