@@ -52,12 +52,13 @@ struct CgView {
   bool global;
 };
 RT_HD inline CgView cg_view(double cx, double cy, double cz, double r, double px, double py, double pz, double diam,
-                            double rho = 0.0) {
+                            double rho = 0.0, double gextra = 0.0) {
   CgView v;
   v.vx = cx - px, v.vy = cy - py, v.vz = cz - pz;
   v.D = __builtin_sqrt(v.vx * v.vx + v.vy * v.vy + v.vz * v.vz);
   v.R = r * (1.0 + 1e-6) + 1e-6 * (v.D + diam) + rho;
-  v.global = !__builtin_isfinite(v.D) || !__builtin_isfinite(v.R) || !(v.D > v.R);
+  // gextra (light grids: kLgOvershoot): spheres within it of the point go global too
+  v.global = !__builtin_isfinite(v.D) || !__builtin_isfinite(v.R) || !(v.D > v.R + gextra);
   v.alpha = v.global ? 4.0 : asin(v.R / v.D) + kLgSlack;
   v.ca = cos(v.alpha);
   v.sa = sin(v.alpha);

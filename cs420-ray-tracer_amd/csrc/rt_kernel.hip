@@ -1733,7 +1733,8 @@ __global__ __launch_bounds__(256) void pg_disk_kernel(const SgBuild a) {
   const int j = t / a.n, i = t - j * a.n;
   const GridPt P = a.pts[j];
   const SphGeo sp = a.geo[i];
-  CgView v = cg_view(sp.cx, sp.cy, sp.cz, a.rad[i], P.x, P.y, P.z, a.diam, P.rho);
+  // light grids (one side): spheres within a shadow ray's overshoot of the light are global (kLgOvershoot)
+  CgView v = cg_view(sp.cx, sp.cy, sp.cz, a.rad[i], P.x, P.y, P.z, a.diam, P.rho, a.sides == 1 ? kLgOvershoot : 0.0);
   if (a.allglob && a.allglob[j]) v = cg_view(0.0, 0.0, 0.0, __builtin_inf(), 0.0, 0.0, 0.0, 0.0);  // global
   if (v.global && lane == 0) {
     atomicAdd(&a.nglob[j * kSgCntStride], 1u);

@@ -173,8 +173,8 @@ void build_light_grid(const double *cx, const double *cy, const double *cz, cons
       const double vx = cx[s] - lx[l], vy = cy[s] - ly[l], vz = cz[s] - lz[l];
       const double D = std::sqrt(vx * vx + vy * vy + vz * vz);
       const double R = std::fabs(r[s]) * (1.0 + 1e-6) + 1e-6 * (D + dm);  // >= r + max_off + rounding
-      if (!light_ok || !std::isfinite(D) || !std::isfinite(R) || !(D > R) || !std::isfinite(dm)) {
-        global.push_back(s);  // contains (or nearly) the light, or non-finite: every direction
+      if (!light_ok || !std::isfinite(D) || !std::isfinite(R) || !(D > R + kLgOvershoot) || !std::isfinite(dm)) {
+        global.push_back(s);  // contains the light or comes within the overshoot of it, or non-finite: every direction
         continue;
       }
       const Dir v{vx / D, vy / D, vz / D};

@@ -27,6 +27,12 @@
 namespace rtk {
 
 constexpr double kLgSlack = 4e-6;
+// A shadow ray starts EPSILON (0.001, ray_math_constants.h:22) past its point
+// and its t is compared with the point's distance to the light (scene.h:72-82),
+// so it runs up to EPSILON PAST the light: a sphere whose surface comes within
+// that of the light can occlude a ray from any direction (the overshoot enters
+// it behind the light) -- such spheres go on the light's global list.
+constexpr double kLgOvershoot = 0.001 * (1.0 + 1e-6);
 
 // Cell of direction (ux, uy, uz) on an N x N cube map: face 0..5 = +X -X +Y -Y
 // +Z -Z, (a, b) = the two minor coordinates divided by the major one, in

@@ -1,7 +1,9 @@
 // Conservativeness check of the per-light direction grids (rt_lightgrid.h):
 // for random scenes and random shaded points, every sphere the exact fp64
 // shadow test of the reference reports as occluding must be on the global list
-// or on the list of the cell the device would look up.  Prints
+// or on the list of the cell the device would look up -- half the lights just
+// outside a sphere, where the shadow ray's EPSILON overshoot past the light
+// (scene.h:72-82) reaches into it from any direction.  Prints
 // "checked <queries> <occluding pairs> missed <count>".
 #include <cmath>
 #include <cstdio>
@@ -60,6 +62,12 @@ int main(int argc, char **argv) {
       lx[l] = shift + scale * 10 * U(rng);
       ly[l] = shift + scale * 10 * U(rng);
       lz[l] = shift + scale * 10 * U(rng);
+      if (rng() % 2 == 0) {  // just outside a sphere, within the shadow rays' EPSILON overshoot (or a bit beyond)
+        const int s = (int)(rng() % n);
+        const V u = nrm({U(rng), U(rng), U(rng)});
+        const double gap = 0.0015 * std::fabs(U(rng));
+        lx[l] = cx[s] + u.x * (r[s] + gap), ly[l] = cy[s] + u.y * (r[s] + gap), lz[l] = cz[s] + u.z * (r[s] + gap);
+      }
     }
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
     auto grow = [&](double x, double y, double z, double rr) {
@@ -89,7 +97,7 @@ int main(int argc, char **argv) {
       V tl = sub(L, hp);
       const double dist = std::sqrt(dot(tl, tl));
       V ld = nrm(tl);
-      V so = add(hp, scl(ld, 0.001 * scale)), sd = nrm(ld);
+      V so = add(hp, scl(ld, 0.001)), sd = nrm(ld);  // EPSILON, absolute (ray_math_constants.h:22)
       V w = sub(L, so);
       const double off = std::fabs(w.y * sd.z - w.z * sd.y) + std::fabs(w.z * sd.x - w.x * sd.z) +
                          std::fabs(w.x * sd.y - w.y * sd.x);

@@ -118,7 +118,7 @@ std::vector<std::vector<int>> build_device_lights(const std::vector<double> &cx,
   for (int l = 0; l < nl; l++) {
     const bool allglob = !(std::isfinite(lx[l]) && std::isfinite(ly[l]) && std::isfinite(lz[l]));
     for (int i = 0; i < n; i++) {
-      rtk::CgView v = rtk::cg_view(cx[i], cy[i], cz[i], std::fabs(r[i]), lx[l], ly[l], lz[l], dm, 0.0);
+      rtk::CgView v = rtk::cg_view(cx[i], cy[i], cz[i], std::fabs(r[i]), lx[l], ly[l], lz[l], dm, 0.0, rtk::kLgOvershoot);
       if (allglob) v = rtk::cg_view(0.0, 0.0, 0.0, INFINITY, 0.0, 0.0, 0.0, 0.0);
       if (v.global) {
         lists[(size_t)(l * row + cells)].push_back(i);

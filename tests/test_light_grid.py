@@ -43,6 +43,18 @@ GRID_SCENES = {
                                for i in range(-20, 20))
                        + "sphere 0 -101 -5 100 0.5 0.5 0.5 0.5 1 5\nsphere 0 0 -5 1 0.9 0.9 0.9 0.9 1 50\n"
                          "light 0 3.004 -4 1 1 1 1\ncamera 0 1 3 0 0 -5 70\n",
+    # spheres just beyond lights (their surfaces 0.0002-0.0009 past them): a shadow ray starts EPSILON
+    # past its point and runs EPSILON past the light (scene.h:72-82), into these spheres from any
+    # direction -- the floor under the lights is in shadow (the light grids' global lists, kLgOvershoot);
+    # one sphere 0.0015 away (beyond the overshoot: lit), and the fuzz scene's geometry (light 3 of
+    # seed 7101 scene 4787: 0.00093 outside a sphere of radius 0.239)
+    "sphere_beyond_light": "sphere 0 0.5005 -5 0.5 0.9 0.9 0.9 0 1 10\nlight 0 0 -5 1 1 1 1\n"
+                           "sphere 2 0.3002 -5 0.3 0.2 0.9 0.2 0.5 1 20\nlight 2 0 -5 0.8 0.8 0.8 1\n"
+                           "sphere -2 0.3015 -5 0.3 0.9 0.2 0.2 0 1 20\nlight -2 0 -5 0.7 0.7 0.7 1\n"
+                           "sphere -0.23628557 0.493439321 -0.673393603 0.239067465 0.5 0.5 0.9 0 1 10\n"
+                           "light -0.129703 0.285743 -0.729077 0.9 0.9 0.9 1\n"
+                           "sphere 0 -101 -5 100 0.6 0.6 0.6 0.2 1 5\nambient 0.1 0.1 0.1\n"
+                           "camera 0 1.5 3 0 -1 -5 75\n",
     # axis-aligned geometry: shadow lines along x = 0 graze spheres of radius 1 at x = +-1
     "axis_tangent": "sphere 1 2 -5 1 1 0 0 0 1 10\nsphere -1 4 -5 1 0 1 0 0.5 1 10\nsphere 0 -100 -5 100 1 1 1 0 1 1\n"
                     "sphere 1 -1 -5 1 0 0 1 0.2 1 10\nlight 0 10 -5 1 1 1 1\nlight 0 10 5 1 1 1 1\n"
