@@ -2,7 +2,8 @@
 scenes -- whole or fractional shininess (40 % of scenes: int_pow and dd_pow),
 1 to 1,500 spheres (so both the cull sweeps and the always-BVH
 paths, render_deferred and render_deferred_walk), tiny to huge radii, mirror
-clouds, 0 to 6 lights, cameras inside spheres -- rendered on cuda:0 through
+clouds, 0 to 6 lights (FUZZ_NEAR_LIGHTS=1: half of them just outside a
+sphere), cameras inside spheres -- rendered on cuda:0 through
 the C-ABI at small sizes and random depths, against the oracle byte for byte
 and ray count for ray count; every third scene is also rendered as three
 frames of one launch (rt_render_frames_async: the deferred kernel and, for
@@ -45,10 +46,19 @@ def scene(rng):
         lines.append("sphere %.9g %.9g %.9g %.9g %.3f %.3f %.3f %.2f 0.5 %s" % (
             rng.uniform(-spread, spread), rng.uniform(-spread, spread), rng.uniform(-3 * spread, spread), r,
             rng.random(), rng.random(), rng.random(), refl, shin()))
+    near = os.environ.get("FUZZ_NEAR_LIGHTS") == "1"
     for _ in range(rng.randint(0, 6)):
-        lines.append("light %.6g %.6g %.6g %.3f %.3f %.3f 1" % (
-            rng.uniform(-2 * spread, 2 * spread), rng.uniform(-spread, 3 * spread), rng.uniform(-3 * spread, spread),
-            rng.random(), rng.random(), rng.random()))
+        pos = (rng.uniform(-2 * spread, 2 * spread), rng.uniform(-spread, 3 * spread), rng.uniform(-3 * spread, spread))
+        if near and n > 0 and rng.random() < 0.5:
+            # FUZZ_NEAR_LIGHTS=1: a light just outside a sphere, within or near a shadow ray's
+            # EPSILON overshoot past it (scene.h:72-82)
+            f = lines[rng.randrange(n)].split()
+            c, rad = [float(v) for v in f[1:4]], abs(float(f[4]))
+            u = [rng.gauss(0, 1) for _ in range(3)]
+            norm = sum(v * v for v in u) ** 0.5 or 1.0
+            gap = rng.choice([0.0002, 0.0008, 0.00099, 0.0012, 0.003]) * rng.uniform(0.9, 1.1)
+            pos = tuple(c[k] + u[k] / norm * (rad + gap) for k in range(3))
+        lines.append("light %.9g %.9g %.9g %.3f %.3f %.3f 1" % (*pos, rng.random(), rng.random(), rng.random()))
     lines.append("ambient %.3f %.3f %.3f" % (rng.random() * 0.3, rng.random() * 0.3, rng.random() * 0.3))
     cam = [rng.uniform(-spread, spread) * 0.3 for _ in range(3)]
     look = [rng.uniform(-spread, spread) * 0.5, rng.uniform(-spread, spread) * 0.5, -2 * spread]
