@@ -20,7 +20,7 @@ def replay(seed, index):
     rng = random.Random(seed)
     for k in range(index + 1):
         text = gpu_fuzz.scene(rng)
-        W, H, D = rng.choice([(1, 1), (7, 5), (64, 48), (96, 64), (160, 90)]) + (rng.choice([0, 1, 2, 4, 8]),)
+        W, H, D = rng.choice(gpu_fuzz.SIZES) + (rng.choice([0, 1, 2, 4, 8]),)
         cams = None
         if k % 3 == 2:
             sc = rt_hip.Scene.parse(text)

@@ -28,6 +28,12 @@ import orc  # noqa: E402  (the checker)
 import rt_hip  # noqa: E402
 
 
+# FUZZ_LARGE=1: images of 1,024 tiles and more, so launches take the host's
+# heavy-first tile order with single, merged and tail tile groups
+SIZES = [(1, 1), (7, 5), (64, 48), (96, 64), (160, 90)] if os.environ.get("FUZZ_LARGE") != "1" else \
+    [(256, 256), (320, 240), (400, 300), (96, 64)]
+
+
 def scene(rng):
     n = rng.choice([1, 2, 5, 30, 200, 700, 1100, 1500])
     spread = rng.choice([0.5, 5.0, 20.0, 1000.0])
@@ -75,7 +81,7 @@ def main():
     try:
         while time.time() - t0 < budget:
             text = scene(rng)
-            W, H, D = rng.choice([(1, 1), (7, 5), (64, 48), (96, 64), (160, 90)]) + (rng.choice([0, 1, 2, 4, 8]),)
+            W, H, D = rng.choice(SIZES) + (rng.choice([0, 1, 2, 4, 8]),)
             sc = rt_hip.Scene.parse(text)
             r.upload(sc)
             rgb, st = r.render(sc.camera(), W, H, D)
