@@ -343,11 +343,11 @@ __device__ __forceinline__ double wmin(double v) {
 }
 // x rounded up to fp32 (the walks' prune bound: an entry t above it is above
 // x too).  NaN stays NaN (every comparison with it keeps the box).
-__device__ __forceinline__ float float_up(double x) {
+__host__ __device__ __forceinline__ float float_up(double x) {
   float f = (float)x;
   if ((double)f < x) {  // one float up: f is finite here (x > f)
-    const int b = __float_as_int(f);
-    f = f == 0.0f ? 0x1p-149f : __int_as_float(f > 0.0f ? b + 1 : b - 1);
+    const int b = __builtin_bit_cast(int, f);
+    f = f == 0.0f ? 0x1p-149f : __builtin_bit_cast(float, f > 0.0f ? b + 1 : b - 1);
   }
   return f;
 }
@@ -714,6 +714,56 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
   }
 }
 
+// The fp32 form of a closest-hit line for the ordered 4-wide walks
+// (bvh_walk_ordered4, walk4_step): origin and direction relative to the BVH
+// centre c0, the slab reciprocals, |d|^2 grown for the prefilter, the slab
+// planes' origins moved by the box margin once per ray ((lo - m - o) regrouped
+// as lo - (o + m): one subtraction per plane; the two roundings stay ~2^-24 of
+// the diameter, far inside the margin m = 1e-6 of it, so the grown slab still
+// contains the exact one), and the walk's lower bound on a box's exit t.
+// Host-callable, so tests/native/margin_check.cpp runs the walk's own box and
+// prefilter arithmetic on the CPU.
+struct Walk4Ray {
+  float ox, oy, oz, dx, dy, dz, ix, iy, iz, dd, lx, ly, lz, hx, hy, hz, tfm;
+};
+__host__ __device__ __forceinline__ Walk4Ray walk4_ray(const BvhArgs &bv, D3 o, D3 d) {
+  Walk4Ray r;
+  r.ox = (float)(o.x - bv.c0x), r.oy = (float)(o.y - bv.c0y), r.oz = (float)(o.z - bv.c0z);
+  r.dx = (float)d.x, r.dy = (float)d.y, r.dz = (float)d.z;
+  r.ix = 1.0f / r.dx, r.iy = 1.0f / r.dy, r.iz = 1.0f / r.dz;
+  r.dd = (r.dx * r.dx + r.dy * r.dy + r.dz * r.dz) * (1.0f + 1e-5f);
+  const float m = bv.margin;
+  r.lx = r.ox + m, r.ly = r.oy + m, r.lz = r.oz + m, r.hx = r.ox - m, r.hy = r.oy - m, r.hz = r.oz - m;
+  r.tfm = bv.tf_min;
+  return r;
+}
+// The grown fp32 slab test of one box, both directions of the line (so the
+// disc == 0 negative tangent roots behind the origin are never pruned): true
+// when the line meets it and its entry tn is not above the prune bound tmf (an
+// upper bound of the best t, float_up); tf is its exit (the walks also require
+// tf >= r.tfm below the root).  NaN boxes (unused 4-wide slots) give false.
+__host__ __device__ __forceinline__ bool box4_hit(const Walk4Ray &r, float lox, float loy, float loz, float hix,
+                                                  float hiy, float hiz, float tmf, float &tn, float &tf) {
+  const float ax = (lox - r.lx) * r.ix, bx = (hix - r.hx) * r.ix;
+  const float ay = (loy - r.ly) * r.iy, by = (hiy - r.hy) * r.iy;
+  const float az = (loz - r.lz) * r.iz, bz = (hiz - r.hz) * r.iz;
+  tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+  tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+  return tn <= tf && !(tn > tmf);
+}
+// The leaves' fp32 sphere prefilter: false when the line provably misses the
+// sphere grown by pmargin (|w x d|^2 > R^2 |d|^2 with |d|^2 grown by 1e-5; the
+// fp32 rounding of the distance is < 6e-7 * diameter, the fp64 test can only
+// hit within 2e-8 * diameter of the surface; NaN passes).  q: centre - c0 and
+// |radius| rounded up.
+__host__ __device__ __forceinline__ bool pf_keep(const Walk4Ray &r, float qx, float qy, float qz, float qw,
+                                                 float pmargin) {
+  const float wx = qx - r.ox, wy = qy - r.oy, wz = qz - r.oz;
+  const float cx = wy * r.dz - wz * r.dy, cy = wz * r.dx - wx * r.dz, cz = wx * r.dy - wy * r.dx;
+  const float R = qw + pmargin;
+  return !(cx * cx + cy * cy + cz * cz > R * R * r.dd);
+}
+
 // Ordered closest-hit walk over the 4-wide nodes (rt_bvh.h BvhNode4): the
 // same grown fp32 slab test as bvh_walk_ordered on up to four child boxes,
 // the nearest entered, the other hits pushed farthest first (so the nearest
@@ -725,30 +775,17 @@ __device__ __forceinline__ void bvh_walk_ordered(const BvhArgs &bv, D3 o, D3 d, 
 template <bool kLdsStack = false, typename T, typename F>
 __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d, T &&tmax_fn, Work &work,
                                                   F &&leaf_fn) {
-  const float ox = (float)(o.x - bv.c0x), oy = (float)(o.y - bv.c0y), oz = (float)(o.z - bv.c0z);
-  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
-  const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
-  const float dd = (dx * dx + dy * dy + dz * dz) * (1.0f + 1e-5f);
-  const float m = bv.margin;
-  // (lo - m - ox) regrouped as lo - (ox + m): one subtraction per plane; the
-  // two roundings stay ~2^-24 of the diameter, far inside the margin m (1e-6
-  // of it), so the grown slab still contains the exact one
-  const float lx = ox + m, ly = oy + m, lz = oz + m, hx = ox - m, hy = oy - m, hz = oz - m;
+  const Walk4Ray r = walk4_ray(bv, o, d);
   // The prune bound in fp32, rounded up (re-read after every leaf, where the
   // best t can shrink): an entry t > tmf is > tmax_fn() too, so every box the
   // fp64 comparison keeps is kept (a box at tmax < t <= tmf is kept as well,
   // which costs a visit, never a result); NaNs keep boxes either way.
   auto tmax_f = [&] { return float_up(tmax_fn()); };
   float tmf = tmax_f();
-  const float tfm = bv.tf_min;
   {
     const BvhNode &r0 = bv.nodes[0];
-    const float ax = (r0.lo[0] - lx) * ix, bx = (r0.hi[0] - hx) * ix;
-    const float ay = (r0.lo[1] - ly) * iy, by = (r0.hi[1] - hy) * iy;
-    const float az = (r0.lo[2] - lz) * iz, bz = (r0.hi[2] - hz) * iz;
-    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-    if (!(tn <= tf && !(tn > tmf))) return;
+    float tn, tf;
+    if (!box4_hit(r, r0.lo[0], r0.lo[1], r0.lo[2], r0.hi[0], r0.hi[1], r0.hi[2], tmf, tn, tf)) return;
   }
   auto st = [&] {
     if constexpr (kLdsStack) return ordered_stack_lds(bv);
@@ -761,26 +798,23 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
     if (ref >= 0) {
       const BvhNode4 *nd = bv.n4 + RT_CK(kCkBvhNode, ref, bv.nn4);
       float t[4];
-      int r[4];
+      int c[4];
       int hits = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float ax = (nd->lox[k] - lx) * ix, bx = (nd->hix[k] - hx) * ix;
-        const float ay = (nd->loy[k] - ly) * iy, by = (nd->hiy[k] - hy) * iy;
-        const float az = (nd->loz[k] - lz) * iz, bz = (nd->hiz[k] - hz) * iz;
-        const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-        const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-        const bool h = tn <= tf && !(tn > tmf) && tf >= tfm;  // NaN (unused slot) -> false
+        float tn, tf;
+        const bool h = box4_hit(r, nd->lox[k], nd->loy[k], nd->loz[k], nd->hix[k], nd->hiy[k], nd->hiz[k], tmf, tn,
+                                tf) && tf >= r.tfm;
         hits += h ? 1 : 0;
         // sort key: a hit sorts below every miss (fminf keeps it finite-or-below-inf)
         t[k] = h ? fminf(tn, 3.0e38f) : __builtin_inff();
-        r[k] = nd->c[k];
+        c[k] = nd->c[k];
       }
       auto ce = [&](int a, int b) {  // compare-exchange, ascending
         const bool sw = t[b] < t[a];
         const float ta = sw ? t[b] : t[a], tb = sw ? t[a] : t[b];
-        const int ra = sw ? r[b] : r[a], rb = sw ? r[a] : r[b];
-        t[a] = ta, t[b] = tb, r[a] = ra, r[b] = rb;
+        const int ca = sw ? c[b] : c[a], cb = sw ? c[a] : c[b];
+        t[a] = ta, t[b] = tb, c[a] = ca, c[b] = cb;
       };
       ce(0, 1);
       ce(2, 3);
@@ -788,20 +822,17 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
       ce(1, 3);
       ce(1, 2);
       if (hits > 0) {
-        if (hits > 3) st[(sp++) * 64] = stk_entry(r[3], t[3]);
-        if (hits > 2) st[(sp++) * 64] = stk_entry(r[2], t[2]);
-        if (hits > 1) st[(sp++) * 64] = stk_entry(r[1], t[1]);
-        ref = r[0];
+        if (hits > 3) st[(sp++) * 64] = stk_entry(c[3], t[3]);
+        if (hits > 2) st[(sp++) * 64] = stk_entry(c[2], t[2]);
+        if (hits > 1) st[(sp++) * 64] = stk_entry(c[1], t[1]);
+        ref = c[0];
         continue;
       }
     } else {
       const int leaf = -(ref + 1), first = leaf >> 4, cnt = leaf & 15;
       for (int k = 0; k < cnt; ++k) {
         const float4 q = bv.pf[RT_CK(kCkBvhLeaf, first + k, bv.nprims)];  // fp32 prefilter, as bvh_walk
-        const float wx = q.x - ox, wy = q.y - oy, wz = q.z - oz;
-        const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
-        const float R = q.w + bv.pmargin;
-        if (cx * cx + cy * cy + cz * cz > R * R * dd) continue;
+        if (!pf_keep(r, q.x, q.y, q.z, q.w, bv.pmargin)) continue;
         if (!leaf_fn((int)bv.prims[RT_CK(kCkBvhLeaf, first + k, bv.nprims)])) return;
       }
       tmf = tmax_f();
@@ -827,30 +858,12 @@ __device__ __forceinline__ void bvh_walk_ordered4(const BvhArgs &bv, D3 o, D3 d,
 // visits, their order and the pruning are bvh_walk_ordered4's, so the closest
 // hit is the same.  The fp32 form of the ray (walk4_ray) is recomputed
 // wherever a kernel resumes walks, so it is not live across other work.
-struct Walk4Ray {
-  float ox, oy, oz, dx, dy, dz, ix, iy, iz, dd, lx, ly, lz, hx, hy, hz, tfm;
-};
-__device__ __forceinline__ Walk4Ray walk4_ray(const BvhArgs &bv, D3 o, D3 d) {
-  Walk4Ray r;
-  r.ox = (float)(o.x - bv.c0x), r.oy = (float)(o.y - bv.c0y), r.oz = (float)(o.z - bv.c0z);
-  r.dx = (float)d.x, r.dy = (float)d.y, r.dz = (float)d.z;
-  r.ix = 1.0f / r.dx, r.iy = 1.0f / r.dy, r.iz = 1.0f / r.dz;
-  r.dd = (r.dx * r.dx + r.dy * r.dy + r.dz * r.dz) * (1.0f + 1e-5f);
-  const float m = bv.margin;
-  r.lx = r.ox + m, r.ly = r.oy + m, r.lz = r.oz + m, r.hx = r.ox - m, r.hy = r.oy - m, r.hz = r.oz - m;
-  r.tfm = bv.tf_min;
-  return r;
-}
 __device__ __forceinline__ bool walk4_begin(const BvhArgs &bv, const Walk4Ray &r, float tmf, int &ref, int &sp) {
   const BvhNode &r0 = bv.nodes[0];
-  const float ax = (r0.lo[0] - r.lx) * r.ix, bx = (r0.hi[0] - r.hx) * r.ix;
-  const float ay = (r0.lo[1] - r.ly) * r.iy, by = (r0.hi[1] - r.hy) * r.iy;
-  const float az = (r0.lo[2] - r.lz) * r.iz, bz = (r0.hi[2] - r.hz) * r.iz;
-  const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-  const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+  float tn, tf;
   ref = bv.root4;
   sp = 0;
-  return tn <= tf && !(tn > tmf);
+  return box4_hit(r, r0.lo[0], r0.lo[1], r0.lo[2], r0.hi[0], r0.hi[1], r0.hi[2], tmf, tn, tf);
 }
 // leaf_fn(sphere index) tests one sphere; tmf_fn() is the current prune bound
 // (float_up of the closest-hit margin), re-read after a leaf.
@@ -866,12 +879,9 @@ __device__ __forceinline__ bool walk4_step(const BvhArgs &bv, const Walk4Ray &r,
     int hits = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float ax = (nd->lox[k] - r.lx) * r.ix, bx = (nd->hix[k] - r.hx) * r.ix;
-      const float ay = (nd->loy[k] - r.ly) * r.iy, by = (nd->hiy[k] - r.hy) * r.iy;
-      const float az = (nd->loz[k] - r.lz) * r.iz, bz = (nd->hiz[k] - r.hz) * r.iz;
-      const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-      const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-      const bool h = tn <= tf && !(tn > tmf) && tf >= r.tfm;
+      float tn, tf;
+      const bool h = box4_hit(r, nd->lox[k], nd->loy[k], nd->loz[k], nd->hix[k], nd->hiy[k], nd->hiz[k], tmf, tn, tf) &&
+                     tf >= r.tfm;
       hits += h ? 1 : 0;
       t[k] = h ? fminf(tn, 3.0e38f) : __builtin_inff();
       c[k] = nd->c[k];
@@ -898,10 +908,7 @@ __device__ __forceinline__ bool walk4_step(const BvhArgs &bv, const Walk4Ray &r,
     const int leaf = -(ref + 1), first = leaf >> 4, cnt = leaf & 15;
     for (int k = 0; k < cnt; ++k) {
       const float4 q = bv.pf[RT_CK(kCkBvhLeaf, first + k, bv.nprims)];  // fp32 prefilter, as bvh_walk
-      const float wx = q.x - r.ox, wy = q.y - r.oy, wz = q.z - r.oz;
-      const float cx = wy * r.dz - wz * r.dy, cy = wz * r.dx - wx * r.dz, cz = wx * r.dy - wy * r.dx;
-      const float R = q.w + bv.pmargin;
-      if (cx * cx + cy * cy + cz * cz > R * R * r.dd) continue;
+      if (!pf_keep(r, q.x, q.y, q.z, q.w, bv.pmargin)) continue;
       leaf_fn((int)bv.prims[RT_CK(kCkBvhLeaf, first + k, bv.nprims)]);
     }
     tmf = tmf_fn();
@@ -1098,140 +1105,6 @@ __host__ __device__ __forceinline__ void grid_line(const BvhArgs &bv, D3 o, D3 d
     r2 = n2;
     r3 = n3;
   }
-}
-
-// grid_line<true> (the whole line) as a resumable walk, one cell per call of
-// gw_step: render_deferred_grid advances each lane's walk on its own, so the
-// lanes whose walks ended shade and take new rays while others still walk.
-// The same cells in the same order, the same candidates and the same stop
-// test as grid_closest_line -- so the same (t, index) for every ray
-// (tests/native/ug_check.cpp compares the two on the CPU).
-// The line of a walk, derived from (o, d) whenever the walk resumes (not
-// kept across the shading: fewer registers held).
-struct GridLine {
-  float ox, oy, oz, dx, dy, dz;  // the prefilter's line (fp32, relative to c0)
-  float i0, i1, i2;              // 1 / d per axis
-};
-__host__ __device__ __forceinline__ GridLine gw_line(const BvhArgs &bv, D3 o, D3 d) {
-  const UgArgs &ug = bv.ug;
-  GridLine l;
-  l.ox = (float)(o.x - bv.c0x), l.oy = (float)(o.y - bv.c0y), l.oz = (float)(o.z - bv.c0z);
-  l.dx = (float)d.x, l.dy = (float)d.y, l.dz = (float)d.z;
-  l.i0 = 1.0f / l.dx, l.i1 = 1.0f / l.dy, l.i2 = 1.0f / l.dz;
-  (void)ug;
-  return l;
-}
-// Where the walk is: the current cell, its exit per axis, the line's end in
-// the grid, the step directions (bit k: +1 along axis k), steps left, the
-// sphere tested last.
-struct GridWalk {
-  float e0, e1, e2, s1;
-  int c0, c1, c2, sgn, guard, last;
-};
-__host__ __device__ __forceinline__ float gw_exit(float cs, int c, float p, float iv, bool pos) {
-  return (iv == __builtin_inff() || iv == -__builtin_inff()) ? __builtin_inff()
-                                                            : ((float)(c + (pos ? 1 : 0)) * cs - p) * iv;
-}
-// Starts the walk of (o, d): the global spheres are tested here (test_fn);
-// false when the line misses the grid (nothing more to walk).
-template <typename F>
-__host__ __device__ __forceinline__ bool gw_begin(const BvhArgs &bv, D3 o, D3 d, Work &work, F &&test_fn,
-                                                  GridWalk &w) {
-  const UgArgs &ug = bv.ug;
-  for (int k = 0; k < ug.nglob; ++k) {
-    work.exact += 1;
-    test_fn((int)ug.glob[k]);
-  }
-  const GridLine l = gw_line(bv, o, d);
-  const float cs = ug.cs;
-  const float p0 = l.ox - ug.gx, p1 = l.oy - ug.gy, p2 = l.oz - ug.gz;  // the origin in grid coordinates
-  float s0 = -__builtin_inff(), s1 = __builtin_inff();
-  auto clip = [&](float p, float iv, int n) {
-    const float ta = (0.0f - p) * iv, tb = ((float)n * cs - p) * iv;
-    if (iv == __builtin_inff() || iv == -__builtin_inff()) {
-      if (!(p >= 0.0f && p <= (float)n * cs)) s1 = -__builtin_inff();
-    } else {
-      s0 = fmaxf(s0, fminf(ta, tb));
-      s1 = fminf(s1, fmaxf(ta, tb));
-    }
-  };
-  clip(p0, l.i0, ug.nx);
-  clip(p1, l.i1, ug.ny);
-  clip(p2, l.i2, ug.nz);
-  if (!(s0 <= s1)) return false;
-  w.s1 = s1;
-  const float ics = 1.0f / cs;
-  auto cell_of = [&](float p, float v, int n) {
-    const int c = (int)floorf((p + v * s0) * ics);
-    return c < 0 ? 0 : (c >= n ? n - 1 : c);
-  };
-  w.c0 = cell_of(p0, l.dx, ug.nx), w.c1 = cell_of(p1, l.dy, ug.ny), w.c2 = cell_of(p2, l.dz, ug.nz);
-  w.sgn = (l.dx > 0.0f ? 1 : 0) | (l.dy > 0.0f ? 2 : 0) | (l.dz > 0.0f ? 4 : 0);
-  w.e0 = gw_exit(cs, w.c0, p0, l.i0, w.sgn & 1);
-  w.e1 = gw_exit(cs, w.c1, p1, l.i1, w.sgn & 2);
-  w.e2 = gw_exit(cs, w.c2, p2, l.i2, w.sgn & 4);
-  w.guard = ug.nx + ug.ny + ug.nz + 2;
-  w.last = -1;
-  return true;
-}
-// Tests the current cell's spheres, then moves to the next cell; false when
-// the walk is over (the line left the grid, or the cell's exit is past the
-// best t + tol: grid_line's stop).  l = gw_line of the walk's (o, d).
-template <typename F, typename B>
-__host__ __device__ __forceinline__ bool gw_step(const BvhArgs &bv, const GridLine &l, GridWalk &w, Work &work,
-                                                 F &&test_fn, B &&best_fn) {
-  const UgArgs &ug = bv.ug;
-  const float cs = ug.cs;
-  const int cur = RT_CK(kCkUgCell, (w.c2 * ug.ny + w.c1) * ug.nx + w.c0, ug.nx * ug.ny * ug.nz);
-  const float4 r0 = ug.rec[4 * cur], r1 = ug.rec[4 * cur + 1], r2 = ug.rec[4 * cur + 2], r3 = ug.rec[4 * cur + 3];
-  const float ex = fminf(w.e0, fminf(w.e1, w.e2));  // this cell's exit
-  bool more = false;
-  if (--w.guard > 0) {
-    if (w.e0 <= w.e1 && w.e0 <= w.e2) {
-      w.c0 += (w.sgn & 1) ? 1 : -1;
-      more = w.e0 <= w.s1 && w.c0 >= 0 && w.c0 < ug.nx;
-      w.e0 = gw_exit(cs, w.c0, l.ox - ug.gx, l.i0, w.sgn & 1);
-    } else if (w.e1 <= w.e2) {
-      w.c1 += (w.sgn & 2) ? 1 : -1;
-      more = w.e1 <= w.s1 && w.c1 >= 0 && w.c1 < ug.ny;
-      w.e1 = gw_exit(cs, w.c1, l.oy - ug.gy, l.i1, w.sgn & 2);
-    } else {
-      w.c2 += (w.sgn & 4) ? 1 : -1;
-      more = w.e2 <= w.s1 && w.c2 >= 0 && w.c2 < ug.nz;
-      w.e2 = gw_exit(cs, w.c2, l.oz - ug.gz, l.i2, w.sgn & 4);
-    }
-  }
-  work.cull += 1;
-  const bool behind = ex < 0.0f;  // a cell wholly behind the origin: the deep-inside skip applies
-  const float pm = bv.pmargin;
-  const float d2 = l.dx * l.dx + l.dy * l.dy + l.dz * l.dz;
-  const float dd_hi = d2 * (1.0f + 1e-5f), dd_lo = d2 * (1.0f - 1e-5f);
-  auto one = [&](const float4 &q, int id_at, const int32_t *ids) {
-    const float wx = q.x - l.ox, wy = q.y - l.oy, wz = q.z - l.oz;
-    const float cx = wy * l.dz - wz * l.dy, cy = wz * l.dx - wx * l.dz, cz = wx * l.dy - wy * l.dx;
-    const float x2 = cx * cx + cy * cy + cz * cz;
-    const float ro = q.w + pm, ri = q.w * (1.0f - 0x1p-22f) - pm;
-    if (x2 > ro * ro * dd_hi) return;
-    if (behind && ri > 0.0f && x2 < ri * ri * dd_lo) return;
-    const int id = (int)ids[id_at];
-    if (id == w.last) return;
-    w.last = id;
-    work.exact += 1;
-    test_fn(id);
-  };
-  auto slot = [&](const float4 &q, int j) {
-    if (q.w >= 0.0f) {
-      one(q, 4 * cur + j, ug.rid);
-      return true;
-    }
-    if (q.w == -2.0f)
-      for (int k = __builtin_bit_cast(int, q.x), ke = __builtin_bit_cast(int, q.y); k < ke; ++k)
-        one(ug.q[RT_CK(kCkUgOver, k, ug.nq)], RT_CK(kCkUgOver, k, ug.nq), ug.ids);
-    return false;
-  };
-  if (slot(r0, 0) && slot(r1, 1) && slot(r2, 2)) slot(r3, 3);
-  if (!more) return false;
-  return !((double)ex > best_fn() + (double)ug.tol);
 }
 
 // Host-callable too (tests/native/ug_check.cpp runs this same code on the CPU).

@@ -99,8 +99,7 @@ struct RenderArgs {
   int dq_cap;                     // entries per shard segment; 0 = no deferral
   int merge_q;                    // kStackMerge: LDS ray-queue entries per wave (16..64)
   int nsingle;                    // kStackMerge: the first nsingle tile slots (heaviest class) get a wave each
-  int npair;                      // kStackMerge: the next npair slots go two per wave
-  int merge_end;                  // kStackMerge: slots [nsingle + npair, merge_end) go kMergeTiles per wave, the rest
+  int merge_end;                  // kStackMerge: slots [nsingle, merge_end) go kMergeTiles per wave, the rest
                                   // (the launch's tail: its lightest tiles) one per wave again
   int pix_off;                    // kStackMerge: LDS offset of the wave's finished pixels (flush_tile)
   int rows_dword;                 // kStackMerge: every 8-pixel tile row starts dword aligned (flush_tile)
@@ -804,21 +803,16 @@ __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const 
     // merge_end, then one slot per group again (the launch's last, lightest
     // tiles: the waves that end a launch are short, so fewer slots idle while
     // the last ones finish)
-    // (and, between the singles and the merged groups, npair slots two per group)
     const int ns = kernarg_late<true, offsetof(RenderArgs, nsingle)>(a.nsingle);
-    const int pr = kernarg_late<true, offsetof(RenderArgs, npair)>(a.npair);
     const int me = kernarg_late<true, offsetof(RenderArgs, merge_end)>(a.merge_end);
-    const int np = (pr + 1) >> 1, m0 = ns + pr;  // pair groups; the first slot of the merged groups
-    const int nm = (me - m0 + kMergeTiles - 1) / kMergeTiles;
+    const int nm = (me - ns + kMergeTiles - 1) / kMergeTiles;
     int base, nt;
     if (group < ns) {
       base = group, nt = 1;
-    } else if (group < ns + np) {
-      base = ns + 2 * (group - ns), nt = m0 - base < 2 ? m0 - base : 2;
-    } else if (group < ns + np + nm) {
-      base = m0 + (group - ns - np) * kMergeTiles, nt = me - base < kMergeTiles ? me - base : kMergeTiles;
+    } else if (group < ns + nm) {
+      base = ns + (group - ns) * kMergeTiles, nt = me - base < kMergeTiles ? me - base : kMergeTiles;
     } else {
-      base = me + (group - ns - np - nm), nt = 1;
+      base = me + (group - ns - nm), nt = 1;
     }
     bool tile_pass = false;
     if (__ballot(act) == 0) {
@@ -1377,128 +1371,6 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_walk(
   flush_counts(kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters), sums, work);
 }
 
-// render_deferred for scenes with the uniform grid's whole-line closest hits
-// (bv.ug.closest: scenes above 1,024 spheres), with the walks decoupled from
-// the shading as in render_deferred_walk: a lane's grid walk advances one cell
-// per step (gw_step, the same cells, candidates and stop as
-// grid_closest_line), a lane whose walk ended waits, and the ready lanes
-// shade once kShadeAt of them are (or no lane walks); a spawned reflection ray
-// starts its walk at once, an ended chain stores its pixel and the lane takes
-// the next queued ray.  The level >= 2 rays' walks are long and uneven
-// (cfg 5: lane utilisation 0.46 in render_deferred's lockstep walks).
-__global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred_grid(const RenderArgs a) {
-  const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards;
-  const int cap = a.dq_cap;
-  const unsigned long long cnt = a.counters[(size_t)shard * kShardStride + kDeferSlot];
-  const unsigned n_dq = (unsigned)(cnt < (unsigned long long)cap ? cnt : (unsigned long long)cap);
-  if (first * 64u >= n_dq) return;
-  const int lane = (int)(threadIdx.x & 63);
-  const unsigned npx_frame = (unsigned)((size_t)a.rows.count * a.od.xw);
-  const unsigned sstride = (unsigned)kShards * (unsigned)cap;  // the chain's stack: dstack[level][queue slot]
-  Work work;
-  unsigned c_shadow = 0, c_reflect = 0, c_neg = 0;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  bool act = false, walking = false, more = true;
-  unsigned long long *fetch = kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters) +
-                              (size_t)shard * kShardStride + kFetchSlot;  // as render_deferred
-  D3 o = mk(0.0, 0.0, 0.0), d = o;
-  int key = -1, dleft = 0, lev = 0;
-  unsigned pixg = 0, qslot = 0;  // the ray's output pixel (launch index) and queue slot
-  // the grid walk of this lane's ray and the best hit so far (t, numerator, sphere)
-  GridWalk gw;
-  int bi = -1;
-  double bt = kInf, bn = __builtin_inf();
-  auto begin = [&](const BvhArgs &bv) {  // a new ray: an empty best, the global spheres, the first cell
-    bt = kInf;
-    bn = __builtin_inf();
-    bi = -1;
-    const double a4 = 4.0 * dot(d, d), a2 = 0.5 * a4;
-    const bool fast = a2_ok(a2);
-    const SphGeo *__restrict__ g = a.geo;
-    walking = gw_begin(bv, o, d, work, [&](int i) { closest_test(g[RT_CK(kCkSphere, i, a.n)], i, o, d, a4, a2, fast, bt, bn, bi); }, gw);
-  };
-  while (true) {
-    {
-      const unsigned long long idle = ~__ballot(act);
-      if (idle && more) {
-        const int fi = __builtin_ctzll(idle);
-        unsigned long long base = 0;
-        if (lane == fi) base = atomicAdd(fetch, (unsigned long long)__popcll(idle));
-        base = __shfl(base, fi, 64);
-        const unsigned long long i = base + (unsigned long long)__popcll(idle & lt);
-        more = base + (unsigned long long)__popcll(idle) < n_dq;
-        if (!act && i < n_dq) {
-          const QRay &e = kernarg_late<true, offsetof(RenderArgs, dq)>(a.dq)[RT_CK(kCkDeferQ, (size_t)shard * (size_t)cap + i, (long long)kShards * cap)];
-          o = mk(e.ox, e.oy, e.oz);
-          d = mk(e.dx, e.dy, e.dz);
-          lev = e.orig;
-          dleft = e.dleft;
-          key = e.key;
-          pixg = (unsigned)e.pix;
-          qslot = shard * (unsigned)cap + (unsigned)i;
-          act = true;
-          begin(kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv));
-        }
-      }
-    }
-    if (__ballot(act) == 0) break;
-    // walk until enough lanes are ready to shade (or no lane walks)
-    if (__ballot(walking)) {
-      const BvhArgs &bv = kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv);
-      const double a4 = 4.0 * dot(d, d), a2 = 0.5 * a4;
-      const bool fast = a2_ok(a2);
-      const SphGeo *__restrict__ g = a.geo;
-      const GridLine gl = gw_line(bv, o, d);
-      while (true) {
-        const unsigned long long wm = __ballot(walking);
-        if (wm == 0 || __popcll(__ballot(act) & ~wm) >= kShadeAt) break;
-        if (walking)
-          walking = gw_step(bv, gl, gw, work,
-                            [&](int i) { closest_test(g[RT_CK(kCkSphere, i, a.n)], i, o, d, a4, a2, fast, bt, bn, bi); },
-                            [&] { return bt; });
-      }
-    }
-    const bool ready = act && !walking;
-    if (__ballot(ready)) {
-      int outcome = 0, nkey = 0;
-      D3 color = mk(0.0, 0.0, 0.0), no = o, nd = d;
-      double refl = 0.0;
-      shade_hit<true, true, true>(a.geo, a.radius, a.mat, a.lights, a.n, a.nl, a.amb, a.bv, a.lg, ready, o, d, key,
-                                   dleft, bi, bt, work, c_shadow, outcome, color, refl, no, nd, nkey);
-      bool spawned = false;
-      if (ready) {
-        StackEnt *gs = kernarg_late<true, offsetof(RenderArgs, dstack)>(a.dstack);
-        if (outcome == kSpawned) {
-          gs[RT_CK(kCkStack, qslot + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)] =
-              StackEnt{color.x, color.y, color.z, refl};
-          ++lev;
-          o = no;
-          d = nd;
-          key = nkey;
-          --dleft;
-          ++c_reflect;
-          spawned = true;
-        } else {
-          D3 res = color;
-          while (lev > 0) {  // main.cpp:54, innermost first
-            --lev;
-            const StackEnt e = gs[RT_CK(kCkStack, qslot + (unsigned)lev * sstride, (long long)(a.depth - 1) * sstride)];
-            res = mk(e.ax + res.x * e.refl, e.ay + res.y * e.refl, e.az + res.z * e.refl);
-          }
-          const OutDesc &od = kernarg_late<true, offsetof(RenderArgs, od)>(a.od);
-          const unsigned f = pixg / npx_frame;
-          or_px(static_cast<uint8_t *>(od.ptr) + (size_t)RT_CK(kCkOut, f, a.frames) * (size_t)od.fstride, pixg - f * npx_frame,
-                pack_px(res, c_neg));
-          act = false;
-        }
-      }
-      if (spawned) begin(kernarg_late<true, offsetof(RenderArgs, bv)>(a.bv));
-    }
-  }
-  unsigned long long sums[4] = {0ull, wave_sum(c_shadow), wave_sum(c_reflect), wave_sum(c_neg)};
-  flush_counts(kernarg_late<true, offsetof(RenderArgs, counters)>(a.counters), sums, work);
-}
-
 // Reassemble rank-major shards into PPM row order (one workgroup per row).
 __global__ __launch_bounds__(kBlock) void unpermute_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                            int W, int H, int band, int G, int R) {
@@ -1968,10 +1840,6 @@ struct rt_ctx {
   int lg_n_opt = 0;            // RT_HIP_SHADOW_GRID_N; 0 = 128, or 768 above kBvhAlwaysAbove spheres
   double lg_max_off = 0.0;
   bool lg_off_free = false;  // shadow queries skip the per-ray max_off check (light_grids)
-  // RT_HIP_LG_ORDER (tuning build): 1 (default) = light lists nearest first
-  // (ids_sort_kernel; synth10k 2.439 -> 2.386 ms per frame, synth200 and
-  // complex within +-0.3 %, profiles/r5x/ab_lg_order.log), 0 = by sphere index
-  int lg_order = 1;
   // camera grids (rt_device.h CgArgs), built on the device per camera
   // position of a launch (cg_bin_kernel / cg_sort_kernel) and kept while the
   // positions and the scene stay the same
@@ -2069,10 +1937,7 @@ struct rt_ctx {
   // without it, profiles/r3n/ab_knobs.log; 32-frame launches are 13 % slower
   // per frame without it)
   int defer = -1;
-  bool defer_walk = true;
-  // RT_HIP_DEFER_GRID (tuning build): deferred rays of a scene whose closest hits walk the uniform grid use
-  // render_deferred_grid (decoupled walks) instead of render_deferred
-  bool defer_grid = false;     // RT_HIP_DEFER_WALK: deferred rays of a scene whose closest hits always walk the BVH use render_deferred_walk
+  bool defer_walk = true;  // RT_HIP_DEFER_WALK: deferred rays of a scene whose closest hits always walk the BVH use render_deferred_walk
   int merge_q = 64;           // kStackMerge: the launch's LDS queue entries per wave (launch_render4 picks it)
   int merge_q_max = 64;       // RT_HIP_MERGE_Q: longest queue tried (8, 16, 32 or 64)
   int defer_level = kDeferLevel;  // RT_HIP_DEFER_LEVEL (>= 1)
@@ -2128,9 +1993,6 @@ struct rt_ctx {
   // (merge_end); 0: four per wave to the end.  RT_HIP_TAIL_WAVES (tuning build)
   int tail = 1;
   int tail_waves = 12;
-  // RT_HIP_PAIR_CLASS (tuning build): tiles of classes [pair_class, single
-  // class) two per wave (slower: profiles/r5n)
-  int pair_class = -1;
   // RT_HIP_WIDE (tuning build): the render kernel whose sparse waves spread
   // their light loop over the lanes (shade_hit kWide).  3 (default): the
   // render and the deferred kernels of every fp64 launch; 2: the render kernel
@@ -2575,7 +2437,10 @@ int device_scan(rt_ctx *c, const int *x, long long n, int *y, long long &total) 
 struct PgMode {
   int sides, globlist, max_global;
   size_t max_entries;
-  int near = 0;  // light grids: lists by distance from the point (ids_sort_kernel)
+  // light grids: lists by distance from the point (ids_sort_kernel; synth10k
+  // 2.439 -> 2.386 ms per frame against sphere-index order, synth200 and
+  // complex within +-0.3 %, profiles/r5x/ab_lg_order.log)
+  int near = 0;
 };
 int point_grids(rt_ctx *c, const std::vector<GridPt> &pts, const std::vector<unsigned char> &allglob, double diam,
                 int N, const PgMode &md, DevScratch &keep, int *&d_off, std::vector<unsigned char> &ok,
@@ -2826,7 +2691,7 @@ int light_grids(rt_ctx *c, const rt_scene *s, double diam) {
     int *d_off = nullptr;
     std::vector<unsigned char> ok;
     void *out = nullptr;
-    int rc = point_grids(c, pts, allglob, dm, N, PgMode{1, 1, INT32_MAX, (size_t)INT32_MAX, c->lg_order}, keep, d_off,
+    int rc = point_grids(c, pts, allglob, dm, N, PgMode{1, 1, INT32_MAX, (size_t)INT32_MAX, 1}, keep, d_off,
                          ok, total, out);
     ids = static_cast<int32_t *>(out);
     c->d_lg_ids = ids;  // owned by the context from here (free_scene)
@@ -3004,7 +2869,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     gstack = reinterpret_cast<StackEnt *>(c->cstack_buf);
   }
   const int *perm = nullptr;
-  int nsingle = 0, npair = 0;
+  int nsingle = 0;
   long long tail = 0;
   // The heavy-first order pays off when a launch has many more tiles than the
   // chip has wave slots; a small launch (a hybrid driver's 64x64 tile) keeps
@@ -3024,16 +2889,11 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       long long heavy = 0;
       for (int k = sc; k < kSchedClasses; k++) heavy += c->perm_cls[k];
       nsingle = (int)std::min<long long>(heavy, ntiles);
-      // RT_HIP_PAIR_CLASS (tuning build): classes [pair_class, sc) two tiles per wave
-      long long pairs = 0;
-      for (int k = std::max(0, c->pair_class); k < sc; k++) pairs += c->perm_cls[k];
-      if (c->pair_class < 0) pairs = 0;
-      npair = (int)std::min<long long>(pairs, ntiles - nsingle);
       // multi-frame launches end on their lightest tiles one per wave: about
       // as many as the chip holds waves (12 per CU), over the launch's frames
       if (c->tail)
-        tail = std::min<long long>(ntiles - nsingle - npair, ((long long)c->n_cu * c->tail_waves + nf - 1) / nf);
-      nslots = nsingle + (npair + 1) / 2 + (ntiles - nsingle - npair - tail + kMergeTiles - 1) / kMergeTiles + tail;
+        tail = std::min<long long>(ntiles - nsingle, ((long long)c->n_cu * c->tail_waves + nf - 1) / nf);
+      nslots = nsingle + (ntiles - nsingle - tail + kMergeTiles - 1) / kMergeTiles + tail;
     }
   }
   const bool xcd_frames = nf > 1 && (c->xcd_frames > 0 || (c->xcd_frames < 0 && bv.ug.on));
@@ -3071,7 +2931,6 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.dq_cap = 0;
   ra.merge_q = c->merge_q;
   ra.nsingle = nsingle;
-  ra.npair = npair;
   ra.merge_end = (int)(ntiles - tail);
   // merge_tiles' pixel bytes: after the scene and the walk stacks, where render_kernel's park/queue region starts
   ra.pix_off = (int)(((lds_layout(kLds, c->nsph, c->nlight, bv.nnodes).end + 31) & ~(size_t)31) +
@@ -3172,8 +3031,6 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       // the cull sweeps (synth200 1 % slower on the walk kernel)
       if (kCull && fast && c->defer_walk && bv.nnodes > 0 && bv.always && !(bv.ug.on && bv.ug.closest))
         hipLaunchKernelGGL(render_deferred_walk, dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
-      else if (kCull && fast && c->defer_grid && bv.ug.on && bv.ug.closest)  // the same with grid walks
-        hipLaunchKernelGGL(render_deferred_grid, dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
       else if (fast && c->wide_mode == 3)  // the deferred waves' tails spread their light loops too
         hipLaunchKernelGGL((render_deferred<kCull, true, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream,
                            ra);
@@ -3316,7 +3173,6 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_BVH_LEAF")) c->bvh_leaf_opt = std::max(1, std::min(15, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER")) c->defer = std::atoi(e) != 0 ? 1 : 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_WALK")) c->defer_walk = std::atoi(e) != 0;
-  if (const char *e = std::getenv("RT_HIP_DEFER_GRID")) c->defer_grid = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_DEFER_LEVEL")) c->defer_level = std::max(1, std::min(RT_MAX_DEPTH, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_MERGE_Q")) c->merge_q_max = std::max(8, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_SHADOW_GRID_N")) c->lg_n_opt = std::max(1, std::min(1024, std::atoi(e)));
@@ -3331,8 +3187,6 @@ int rt_create(int device, rt_ctx **out) {
   if (const char *e = std::getenv("RT_HIP_TAIL")) c->tail = std::atoi(e) != 0;
   if (const char *e = std::getenv("RT_HIP_TAIL_WAVES")) c->tail_waves = std::max(1, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_WIDE")) c->wide_mode = std::max(0, std::min(3, std::atoi(e)));
-  if (const char *e = std::getenv("RT_HIP_LG_ORDER")) c->lg_order = std::atoi(e) != 0;
-  if (const char *e = std::getenv("RT_HIP_PAIR_CLASS")) c->pair_class = std::max(-1, std::min(kSchedClasses, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_DEFER_DIV")) c->defer_div = std::max(1, std::min(1024, std::atoi(e)));
   if (const char *e = std::getenv("RT_HIP_GRID_CELLS")) c->ug_cells = std::max(0.05, std::min(64.0, std::atof(e)));
   if (const char *e = std::getenv("RT_HIP_SINGLE_CLASS"))

@@ -3,7 +3,10 @@
 // shadow test of the reference reports as occluding must be on the global list
 // or on the list of the cell the device would look up -- half the lights just
 // outside a sphere, where the shadow ray's EPSILON overshoot past the light
-// (scene.h:72-82) reaches into it from any direction.  Prints
+// (scene.h:72-82) reaches into it from any direction; every fifth scene small
+// (diameter 0.2 .. 20) and 1e6 .. 1e10 from the origin, where the rounding
+// of the shadow ray's origin and distance is far above kLgOvershoot's
+// absolute slack and must be covered by the relative margins.  Prints
 // "checked <queries> <occluding pairs> missed <count>".
 #include <cmath>
 #include <cstdio>
@@ -42,12 +45,16 @@ bool hit(V c, double r, V o, V d, double &t) {
 
 int main(int argc, char **argv) {
   const int seeds = argc > 1 ? std::atoi(argv[1]) : 20;
-  long queries = 0, pairs = 0, missed = 0;
+  long queries = 0, pairs = 0, missed = 0, far_q = 0, far_p = 0;
   for (int seed = 0; seed < seeds; seed++) {
     std::mt19937_64 rng(seed);
     std::uniform_real_distribution<double> U(-1.0, 1.0);
-    const double scale = std::pow(10.0, (int)(rng() % 5) - 1);   // 0.1 .. 1000
-    const double shift = (rng() % 3 == 0) ? 1e5 * scale : 0.0;  // far from the origin
+    double scale = std::pow(10.0, (int)(rng() % 5) - 1);   // 0.1 .. 1000
+    double shift = (rng() % 3 == 0) ? 1e5 * scale : 0.0;  // far from the origin
+    if (seed % 5 == 4) {  // small scenes very far from the origin: |coords| / diameter up to 1e10
+      scale = std::pow(10.0, -(double)(rng() % 3));             // 1 .. 0.01
+      shift = std::pow(10.0, 6.0 + 2.0 * (double)(rng() % 3));  // 1e6 .. 1e10
+    }
     const int n = 20 + (int)(rng() % 200), nl = 1 + (int)(rng() % 4);
     const int N = (int[]){1, 2, 7, 32, 64}[rng() % 5];
     std::vector<double> cx(n), cy(n), cz(n), r(n), lx(nl), ly(nl), lz(nl);
@@ -116,10 +123,12 @@ int main(int argc, char **argv) {
       for (int i = 0; i < n; i++) listed[i] = in_c[i] && in_m[i] && in_p[i];
       for (int k = st[cells]; k < st[cells + 1]; k++) listed[ids[k]] = 1;
       queries++;
+      far_q += seed % 5 == 4;
       for (int i = 0; i < n; i++) {
         double t;
         if (hit({cx[i], cy[i], cz[i]}, r[i], so, sd, t) && t < 1e20 && t < dist) {
           pairs++;
+          far_p += seed % 5 == 4;
           if (!listed[i]) {
             missed++;
             if (missed < 10)
@@ -129,6 +138,7 @@ int main(int argc, char **argv) {
       }
     }
   }
+  std::printf("far %ld %ld\n", far_q, far_p);  // the 1e6 .. 1e10 scenes' queries and occluding pairs
   std::printf("checked %ld %ld missed %ld\n", queries, pairs, missed);
   return missed != 0;
 }

@@ -190,28 +190,6 @@ int main(int argc, char **argv) {
             std::printf("WRONG scene %d line %d grid (%d, %.17g) reference (%d, %.17g)\n", seed, li, bi, bt, ri, rt);
         }
         hits += ri >= 0;
-        // the resumable walk (gw_begin / gw_step, render_deferred_grid): the
-        // same tests in the same order, so the same (t, index) and cell count
-        double gt = 1e20;
-        int gi = -1;
-        auto gfold = [&](int i) {
-          double t;
-          if (ref_test(C[i], R[i], o, d, t) && (t < gt || (t == gt && i < gi))) {
-            gt = t;
-            gi = i;
-          }
-        };
-        rtk::Work w3;
-        rtk::GridWalk gw;
-        if (rtk::gw_begin(bv, D3{o.x, o.y, o.z}, D3{d.x, d.y, d.z}, w3, gfold, gw))
-          for (const rtk::GridLine gl = rtk::gw_line(bv, D3{o.x, o.y, o.z}, D3{d.x, d.y, d.z});
-               rtk::gw_step(bv, gl, gw, w3, gfold, [&] { return gt; });) {
-          }
-        if (gi != bi || gt != bt || w3.cull != w2.cull || w3.exact != w2.exact) {
-          if (++wrong <= 10)
-            std::printf("WALK scene %d line %d resumable (%d, %.17g, %lld cells) whole line (%d, %.17g, %lld)\n", seed,
-                        li, gi, gt, (long long)w3.cull, bi, bt, (long long)w2.cull);
-        }
       }
       for (int i = 0; i < N; i++) {
         // long double geometry: distance of the line to the centre, the foot point's t

@@ -31,10 +31,7 @@ CSRC = os.path.join(REPO, "cs420-ray-tracer_amd", "csrc")
 
 
 def test_behind_grid_covers_tangent_lines(tmp_path):
-    """behind_cells and grid_closest_line, on the CPU (tests/native/ug_check.cpp);
-    the resumable walk (gw_begin / gw_step, render_deferred_grid) gives the
-    same (t, index), cells and tests as grid_closest_line on every line (a
-    difference counts as wrong)."""
+    """behind_cells and grid_closest_line, on the CPU (tests/native/ug_check.cpp)."""
     exe = tmp_path / "ug_check"
     subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-I",
                     CSRC, "-I", os.path.join(REPO, "include"), "-o", str(exe),
@@ -106,7 +103,7 @@ def test_tangent_scenes_need_the_negative_root():
 _FORCED = {"RT_HIP_BEHIND_GRID": "1", "RT_HIP_BVH_ALWAYS": "1", "RT_HIP_SPHERE_GRID": "0", "RT_HIP_CAM_GRID": "0"}
 
 
-@pytest.fixture(params=["on", "off", "on-defer1", "closest", "closest-defer-grid"])  # on*: BVH walk ahead + behind_cells
+@pytest.fixture(params=["on", "off", "on-defer1", "closest"])  # on*: BVH walk ahead + behind_cells
 def behind_renderer(request, monkeypatch):
     import rt_hip
 
@@ -119,8 +116,6 @@ def behind_renderer(request, monkeypatch):
     if request.param.startswith("closest"):
         env["RT_HIP_GRID_CLOSEST"] = "1"  # closest hits along the whole line through the grid, no BVH walk
         env["RT_HIP_DEFER_LEVEL"] = "1"
-    if request.param == "closest-defer-grid":
-        env["RT_HIP_DEFER_GRID"] = "1"  # the deferred rays' walks decoupled (render_deferred_grid)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     r = rt_hip.Renderer(0, variant=knob_variant())

@@ -28,9 +28,12 @@ def test_grid_lists_are_conservative(tmp_path):
                    check=True)
     out = subprocess.run([str(exe), "40"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
-    words = out.stdout.split()
+    far, words = [ln.split() for ln in out.stdout.strip().splitlines()[-2:]]
     assert words[0] == "checked" and int(words[1]) > 100000 and int(words[2]) > 100000
     assert words[-1] == "0"
+    # small scenes 1e6 .. 1e10 from the origin (kLgOvershoot's absolute slack is
+    # below their rounding; the relative margins must cover it)
+    assert far[0] == "far" and int(far[1]) > 10000 and int(far[2]) > 30000, out.stdout
 
 
 GRID_SCENES = {
