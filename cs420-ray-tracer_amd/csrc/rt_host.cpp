@@ -18,9 +18,13 @@
 #include <sstream>
 #include <string>
 #include <vector>
-#include <condition_variable>
-#include <mutex>
+#include <atomic>
+#include <memory>
 #include <thread>
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include "rt_hip.h"
 
@@ -117,6 +121,28 @@ V normalized(V a) {
 }
 void put(double *d, V v) { set3(d, v.x, v.y, v.z); }
 
+// Runs fn(k) for k in [0, nchunk) on up to nthr threads (the caller is one
+// of them).  A thread that cannot be started (resource limits) leaves its
+// share to the others; every started thread is joined on every path, so no
+// exception leaves the C ABI and no joinable thread is destroyed.
+template <typename F>
+void run_chunks(size_t nthr, size_t nchunk, F &&fn) {
+  std::atomic<size_t> next{0};
+  auto worker = [&]() {
+    for (size_t k; (k = next.fetch_add(1)) < nchunk;) fn(k);
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nthr; t++) {
+    try {
+      th.emplace_back(worker);
+    } catch (...) {
+      break;  // the threads already started and this one do the rest
+    }
+  }
+  worker();
+  for (auto &t : th) t.join();
+}
+
 }  // namespace
 
 extern "C" {
@@ -189,82 +215,99 @@ int rt_camera_from_scene(const rt_scene *s, rt_camera *c) {
 }
 
 // P3 text identical to write_ppm (src/main.cpp:69-91) -- "r g b\n" per pixel,
-// top row first -- but formatted from a 256-entry table into one buffer
-// instead of ostream double formatting (1.85 s at 1080p upstream).
+// top row first -- formatted from a 256-entry table, in parallel, straight into
+// the file: a sizing pass gives every pixel range's offset, the file is sized
+// once and mapped, and each range is formatted in place (no intermediate
+// buffers, no copy through stdio; 1.85 s at 1080p upstream).  Where the file
+// cannot be mapped (a pipe, a special file) the ranges are formatted into
+// buffers and written in order.
 int rt_write_ppm(const char *path, const uint8_t *rgb, int width, int height, int binary) {
   if (!path || !rgb || width < 0 || height < 0) return RT_ERR_INVALID_ARG;
-  FILE *f = std::fopen(path, "wb");
-  if (!f) return RT_ERR_IO;
-  size_t n = (size_t)width * (size_t)height;
-  std::fprintf(f, "%s\n%d %d\n255\n", binary ? "P6" : "P3", width, height);
-  int rc = RT_OK;
+  const size_t n = (size_t)width * (size_t)height;
+  char hdr[64];
+  const int hn = std::snprintf(hdr, sizeof hdr, "%s\n%d %d\n255\n", binary ? "P6" : "P3", width, height);
   if (binary) {
-    if (std::fwrite(rgb, 1, n * 3, f) != n * 3) rc = RT_ERR_IO;
-  } else {
-    // "0".."255" and their lengths, built once (a function-local static: safe
-    // when several threads write images at the same time)
-    struct Tab {
-      char s[256][4];
-      unsigned char n[256];
-      Tab() {
-        for (int v = 0; v < 256; v++) n[v] = (unsigned char)std::snprintf(s[v], 4, "%d", v);
-      }
-    };
-    static const Tab T;
-    // pixel ranges formatted in parallel (each into its own buffer, at most
-    // 12 bytes per pixel), then written in order: the bytes are the serial
-    // writer's (main.cpp:69-91: rows as given, "r g b\n" per pixel)
-    auto format = [&](size_t p0, size_t p1, std::vector<char> &out) {
-      out.resize((p1 - p0) * 12);
-      char *o = out.data();
-      for (size_t p = p0; p < p1; p++) {
-        for (int c = 0; c < 3; c++) {
-          const unsigned v = rgb[3 * p + c];
-          std::memcpy(o, T.s[v], 4);
-          o += T.n[v];
-          *o++ = c == 2 ? '\n' : ' ';
-        }
-      }
-      out.resize((size_t)(o - out.data()));
-    };
-    const unsigned hw = std::thread::hardware_concurrency();
-    const size_t nthr = n < ((size_t)1 << 16) ? 1 : std::max<size_t>(1, std::min<size_t>(hw ? hw : 1, 16));
-    const size_t nchunk = nthr * 4;  // a few per thread: the first write starts while the rest are formatted
-    std::vector<std::vector<char>> bufs(nchunk);
-    std::vector<unsigned char> done(nchunk, 0);
-    std::mutex mu;
-    std::condition_variable cv;
-    size_t next = 0;
-    auto worker = [&]() {
-      for (;;) {
-        size_t k;
-        {
-          std::lock_guard<std::mutex> lk(mu);
-          if (next >= nchunk) return;
-          k = next++;
-        }
-        format(n * k / nchunk, n * (k + 1) / nchunk, bufs[k]);
-        {
-          std::lock_guard<std::mutex> lk(mu);
-          done[k] = 1;
-        }
-        cv.notify_all();
-      }
-    };
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < nthr; t++) th.emplace_back(worker);
-    if (nthr == 1) worker();
-    for (size_t k = 0; k < nchunk; k++) {
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return done[k] != 0; });
-      }
-      if (rc == RT_OK && std::fwrite(bufs[k].data(), 1, bufs[k].size(), f) != bufs[k].size()) rc = RT_ERR_IO;
-      std::vector<char>().swap(bufs[k]);
-    }
-    for (auto &t : th) t.join();
+    FILE *f = std::fopen(path, "wb");
+    if (!f) return RT_ERR_IO;
+    int rc = std::fwrite(hdr, 1, (size_t)hn, f) == (size_t)hn ? RT_OK : RT_ERR_IO;
+    if (rc == RT_OK && n && std::fwrite(rgb, 1, n * 3, f) != n * 3) rc = RT_ERR_IO;
+    if (std::fclose(f) != 0) rc = RT_ERR_IO;
+    return rc;
   }
-  if (std::fclose(f) != 0) rc = RT_ERR_IO;
+  // "0".."255" and their lengths, built once (a function-local static: safe
+  // when several threads write images at the same time)
+  struct Tab {
+    char s[256][4];
+    unsigned char n[256];
+    Tab() {
+      for (int v = 0; v < 256; v++) n[v] = (unsigned char)std::snprintf(s[v], 4, "%d", v);
+    }
+  };
+  static const Tab T;
+  const unsigned hw = std::thread::hardware_concurrency();
+  const size_t nthr = n < ((size_t)1 << 16) ? 1 : std::max<size_t>(1, std::min<size_t>(hw ? hw : 1, 16));
+  const size_t nchunk = nthr == 1 ? 1 : nthr * 4;
+  auto lo = [&](size_t k) { return n * k / nchunk; };
+  // bytes of each pixel range: the three numbers' digits + 2 spaces + newline
+  std::vector<size_t> off(nchunk + 1, 0);
+  run_chunks(nthr, nchunk, [&](size_t k) {
+    size_t b = 0;
+    for (size_t i = 3 * lo(k), e = 3 * lo(k + 1); i < e; i++) b += T.n[rgb[i]];
+    off[k + 1] = b + 3 * (lo(k + 1) - lo(k));
+  });
+  off[0] = (size_t)hn;
+  for (size_t k = 0; k < nchunk; k++) off[k + 1] += off[k];
+  const size_t total = off[nchunk];
+  // range k formatted at o (exactly off[k + 1] - off[k] bytes): each number
+  // as its 4-byte table slot (the next write overwrites the slot's tail), the
+  // range's last pixel through a bounce buffer so that nothing lands past the
+  // range (the next range may be another thread's)
+  auto format = [&](size_t k, char *o) {
+    auto pixel = [&](size_t p, char *w) {
+      for (int c = 0; c < 3; c++) {
+        const unsigned v = rgb[3 * p + c];
+        std::memcpy(w, T.s[v], 4);
+        w += T.n[v];
+        *w++ = c == 2 ? '\n' : ' ';
+      }
+      return w;
+    };
+    const size_t p0 = lo(k), p1 = lo(k + 1);
+    if (p1 == p0) return;
+    for (size_t p = p0; p + 1 < p1; p++) o = pixel(p, o);
+    char tail[16];
+    std::memcpy(o, tail, (size_t)(pixel(p1 - 1, tail) - tail));
+  };
+  const int fd = ::open(path, O_RDWR | O_CREAT | O_TRUNC, 0666);
+  if (fd < 0) return RT_ERR_IO;
+  int rc = RT_OK;
+  void *m = MAP_FAILED;
+  if (::ftruncate(fd, (off_t)total) == 0) m = ::mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (m != MAP_FAILED) {
+    char *base = static_cast<char *>(m);
+    std::memcpy(base, hdr, (size_t)hn);
+    run_chunks(nthr, nchunk, [&](size_t k) { format(k, base + off[k]); });
+    if (::munmap(m, total) != 0) rc = RT_ERR_IO;
+  } else {  // not mappable (nothing written yet: the file position is 0): format into buffers, write in order
+    std::vector<std::unique_ptr<char[]>> bufs(nchunk);
+    run_chunks(nthr, nchunk, [&](size_t k) {
+      bufs[k].reset(new (std::nothrow) char[off[k + 1] - off[k]]);
+      if (bufs[k]) format(k, bufs[k].get());
+    });
+    auto put = [&](const char *p, size_t len) {
+      while (rc == RT_OK && len > 0) {
+        const ssize_t w = ::write(fd, p, len);
+        if (w <= 0) rc = RT_ERR_IO;
+        else p += w, len -= (size_t)w;
+      }
+    };
+    put(hdr, (size_t)hn);
+    for (size_t k = 0; k < nchunk; k++) {
+      if (!bufs[k]) rc = RT_ERR_IO;
+      put(bufs[k].get(), off[k + 1] - off[k]);
+    }
+  }
+  if (::close(fd) != 0) rc = RT_ERR_IO;
   return rc;
 }
 

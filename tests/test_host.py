@@ -145,6 +145,37 @@ def test_p3_writer_byte_identical_to_reference(tmp_path, name):
     assert hashlib.sha256(p.read_bytes()).hexdigest() == m["sha256_p3"]
 
 
+@pytest.mark.parametrize("name", ["complex_97x61_d4", "complex_1920x1080_d4"])
+def test_p3_writer_through_a_pipe(tmp_path, name):
+    """A file that cannot be sized and mapped (a FIFO): the writer formats its
+    pixel ranges into buffers and writes them in order -- the same bytes."""
+    import threading
+
+    m = manifest()[name]
+    fifo = tmp_path / "out.fifo"
+    os.mkfifo(fifo)
+    got = []
+    reader = threading.Thread(target=lambda: got.append(open(fifo, "rb").read()))
+    reader.start()
+    assert rt_hip.write_ppm(str(fifo), golden_rgb(name), m["width"], m["height"]) is None
+    reader.join(60)
+    assert hashlib.sha256(got[0]).hexdigest() == m["sha256_p3"]
+
+
+def test_p3_writer_edge_sizes(tmp_path):
+    """Empty and one-pixel images, and ranges whose last pixel is short
+    ("0 0 0\n") at every chunk boundary of the parallel path."""
+    import numpy as np
+
+    for W, H in ((0, 0), (1, 1), (3, 0), (1000, 300)):
+        rgb = (np.arange(W * H * 3) % 7 == 0).astype(np.uint8) * 200 if W * H else np.zeros(0, np.uint8)
+        p = tmp_path / ("e%dx%d.ppm" % (W, H))
+        rt_hip.write_ppm(str(p), rgb.tobytes(), W, H)
+        want = "P3\n%d %d\n255\n" % (W, H) + "".join(
+            "%d %d %d\n" % tuple(rgb[3 * i:3 * i + 3]) for i in range(W * H))
+        assert p.read_bytes() == want.encode(), (W, H)
+
+
 def test_p6_writer(tmp_path):
     m = manifest()["complex_97x61_d4"]
     p = tmp_path / "out.ppm"
