@@ -62,6 +62,7 @@ enum CkSite {
   kCkPixbuf,      // merge_tiles' LDS finished-pixel slot
   kCkOut,         // framebuffer byte offset of a tile row or deferred pixel
   kCkCgBuild,     // camera-grid build: disk, (disk, block) pair, cell count and list slot
+  kCkHome,        // stack-home pool: no free home after kHomeSweeps sweeps of its bitmap
   kCkSites
 };
 #ifdef RT_CHECK

@@ -728,6 +728,9 @@ __device__ __forceinline__ int home_acquire(unsigned long long *bits, int nwords
     // the first try: a bit picked by the workgroup id as well (a half-full word
     // then takes one atomic, not two); it learns the word
     unsigned long long cur = ~(1ull << ((blockIdx.x / (unsigned)nwords) & 63u));
+#ifdef RT_CHECK
+    long long spins = 0;
+#endif
     while (h < 0) {
       while (~cur) {
         const int bit = __builtin_ctzll(~cur);
@@ -741,6 +744,18 @@ __device__ __forceinline__ int home_acquire(unsigned long long *bits, int nwords
       if (h < 0) {
         w = w + 1 == nwords ? 0 : w + 1;
         cur = 0ull;
+#ifdef RT_CHECK
+        // the pool holds twice the resident waves, so a wave finds a home
+        // within a sweep or two; a wave still spinning after kHomeSweeps full
+        // sweeps means a leaked home or an under-sized pool: record it and
+        // share home 0 (wrong pixels, RT_ERR_CHECK) so the launch drains
+        // instead of hanging
+        constexpr long long kHomeSweeps = 4096;
+        if (++spins >= kHomeSweeps * nwords) {
+          ck_fail(kCkHome, spins, kHomeSweeps * nwords);
+          h = 0;
+        }
+#endif
       }
     }
   }
@@ -2946,15 +2961,10 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     const size_t npx = (size_t)rows.count * od.xw * nf;
     const size_t cap = std::max<size_t>(64, ((npx / kShards / (size_t)c->defer_div) + 63) & ~(size_t)63);
     const size_t need = cap * kShards * (sizeof(QRay) + (size_t)(depth - 1) * sizeof(StackEnt));
-    if (c->dq_bytes < need) {
-      RT_TRY(c, hipStreamSynchronize(c->stream));
-      if (c->dq_buf) (void)hipFree(c->dq_buf);
-      c->dq_buf = nullptr;
-      c->dq_bytes = 0;
-      RT_TRY(c, hipMalloc(&c->dq_buf, need));
-      c->dq_bytes = need;
-    }
-    if (cap < (size_t)1 << 30 && (unsigned long long)cap * kShards * (unsigned)(depth - 1) < (1ull << 32)) {
+    // the queue is a speed-up: past the 32-bit slot-stack index, or when the
+    // memory is not there (grow_soft), the launch runs without deferral
+    if (cap < (size_t)1 << 30 && (unsigned long long)cap * kShards * (unsigned)(depth - 1) < (1ull << 32) &&
+        grow_soft(c, c->dq_buf, c->dq_bytes, need)) {
       ra.dq = c->dq_buf;
       ra.dq_cap = (int)cap;
       ra.dstack = reinterpret_cast<StackEnt *>(c->dq_buf + cap * kShards);
@@ -3531,7 +3541,7 @@ int rt_render_stats(rt_ctx *c, rt_stats *st) {
         "camera/sphere-grid list slot", "sphere-grid start", "sphere-grid key", "uniform-grid cell",
         "uniform-grid overflow slot", "BVH node reference", "BVH leaf slot", "tile order slot / tile id",
         "deferred-queue slot", "reflection-stack slot", "LDS ray-queue slot", "LDS pixel slot",
-        "framebuffer offset", "camera-grid build slot"};
+        "framebuffer offset", "camera-grid build slot", "stack-home pool exhausted"};
     CheckRec rec{};
     RT_TRY(c, hipMemcpyFromSymbol(&rec, HIP_SYMBOL(g_check), sizeof rec));
     if (rec.count) {
