@@ -732,6 +732,15 @@ def main():
                          "valu_busy": pmc_rec.get("valu_busy") if pmc_ok else None,
                          "fp64_share_of_valu_insts": pmc_rec.get("fp64_share_of_valu_insts") if pmc_ok else None,
                          "valu_lane_utilization": pmc_rec.get("valu_lane_utilization") if pmc_ok else None,
+                         # the PMC FLOP count assumes full exec masks (an upper bound): weighted by the
+                         # measured VALU lane utilisation it is the FLOPs on active lanes (an estimate:
+                         # the fp64 instructions' own lane occupancy is not counted separately)
+                         "lane_weighted": ({
+                             "achieved": round(achieved * pmc_rec["valu_lane_utilization"], 3),
+                             "frac": round(achieved * pmc_rec["valu_lane_utilization"] / FP64_VALU_PEAK_TFLOPS, 4),
+                             "what": "achieved x valu_lane_utilization (SQ_THREAD_CYCLES_VALU / 64 "
+                                     "SQ_ACTIVE_INST_VALU): fp64 FLOPs on active lanes"}
+                             if pmc_ok and achieved is not None and pmc_rec.get("valu_lane_utilization") else None),
                          "kernel_src_sha": src_sha,
                          "pmc_matches_kernel_src": pmc_ok,
                          # PMC counters per FRAME (scripts/make_pmc_json.py); bytes: fetch (raw) / write per frame
