@@ -19,11 +19,13 @@
 #include <string>
 #include <vector>
 #include <atomic>
+#include <cerrno>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
 #include <thread>
 
 #include <fcntl.h>
-#include <sys/mman.h>
 #include <unistd.h>
 
 #include "rt_hip.h"
@@ -121,28 +123,6 @@ V normalized(V a) {
 }
 void put(double *d, V v) { set3(d, v.x, v.y, v.z); }
 
-// Runs fn(k) for k in [0, nchunk) on up to nthr threads (the caller is one
-// of them).  A thread that cannot be started (resource limits) leaves its
-// share to the others; every started thread is joined on every path, so no
-// exception leaves the C ABI and no joinable thread is destroyed.
-template <typename F>
-void run_chunks(size_t nthr, size_t nchunk, F &&fn) {
-  std::atomic<size_t> next{0};
-  auto worker = [&]() {
-    for (size_t k; (k = next.fetch_add(1)) < nchunk;) fn(k);
-  };
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < nthr; t++) {
-    try {
-      th.emplace_back(worker);
-    } catch (...) {
-      break;  // the threads already started and this one do the rest
-    }
-  }
-  worker();
-  for (auto &t : th) t.join();
-}
-
 }  // namespace
 
 extern "C" {
@@ -215,97 +195,111 @@ int rt_camera_from_scene(const rt_scene *s, rt_camera *c) {
 }
 
 // P3 text identical to write_ppm (src/main.cpp:69-91) -- "r g b\n" per pixel,
-// top row first -- formatted from a 256-entry table, in parallel, straight into
-// the file: a sizing pass gives every pixel range's offset, the file is sized
-// once and mapped, and each range is formatted in place (no intermediate
-// buffers, no copy through stdio; 1.85 s at 1080p upstream).  Where the file
-// cannot be mapped (a pipe, a special file) the ranges are formatted into
-// buffers and written in order.
+// top row first -- formatted from a 256-entry table (1.85 s at 1080p upstream
+// with ostream double formatting): pixel ranges are formatted on up to 16
+// threads into their own buffers and written with write(2) in order as they
+// complete, so the formatting hides under the writes.  On the GPU box's
+// overlay file system the writes are the floor (~0.22 ms per MB into the page
+// cache: 5.3-6 ms for 1080p); ordered write(2) beat fwrite (6.7-7.2 ms),
+// pwrite from every thread (5.8-7.0) and a mapped file (13-14 ms)
+// (scripts/p3_write_bench.cpp, profiles/r7b/).  The calling thread formats
+// too, and takes any range no helper has claimed, so the file is complete
+// even when no thread can be started; every started thread is joined.
 int rt_write_ppm(const char *path, const uint8_t *rgb, int width, int height, int binary) {
   if (!path || !rgb || width < 0 || height < 0) return RT_ERR_INVALID_ARG;
   const size_t n = (size_t)width * (size_t)height;
   char hdr[64];
   const int hn = std::snprintf(hdr, sizeof hdr, "%s\n%d %d\n255\n", binary ? "P6" : "P3", width, height);
-  if (binary) {
-    FILE *f = std::fopen(path, "wb");
-    if (!f) return RT_ERR_IO;
-    int rc = std::fwrite(hdr, 1, (size_t)hn, f) == (size_t)hn ? RT_OK : RT_ERR_IO;
-    if (rc == RT_OK && n && std::fwrite(rgb, 1, n * 3, f) != n * 3) rc = RT_ERR_IO;
-    if (std::fclose(f) != 0) rc = RT_ERR_IO;
-    return rc;
-  }
-  // "0".."255" and their lengths, built once (a function-local static: safe
-  // when several threads write images at the same time)
-  struct Tab {
-    char s[256][4];
-    unsigned char n[256];
-    Tab() {
-      for (int v = 0; v < 256; v++) n[v] = (unsigned char)std::snprintf(s[v], 4, "%d", v);
-    }
-  };
-  static const Tab T;
-  const unsigned hw = std::thread::hardware_concurrency();
-  const size_t nthr = n < ((size_t)1 << 16) ? 1 : std::max<size_t>(1, std::min<size_t>(hw ? hw : 1, 16));
-  const size_t nchunk = nthr == 1 ? 1 : nthr * 4;
-  auto lo = [&](size_t k) { return n * k / nchunk; };
-  // bytes of each pixel range: the three numbers' digits + 2 spaces + newline
-  std::vector<size_t> off(nchunk + 1, 0);
-  run_chunks(nthr, nchunk, [&](size_t k) {
-    size_t b = 0;
-    for (size_t i = 3 * lo(k), e = 3 * lo(k + 1); i < e; i++) b += T.n[rgb[i]];
-    off[k + 1] = b + 3 * (lo(k + 1) - lo(k));
-  });
-  off[0] = (size_t)hn;
-  for (size_t k = 0; k < nchunk; k++) off[k + 1] += off[k];
-  const size_t total = off[nchunk];
-  // range k formatted at o (exactly off[k + 1] - off[k] bytes): each number
-  // as its 4-byte table slot (the next write overwrites the slot's tail), the
-  // range's last pixel through a bounce buffer so that nothing lands past the
-  // range (the next range may be another thread's)
-  auto format = [&](size_t k, char *o) {
-    auto pixel = [&](size_t p, char *w) {
-      for (int c = 0; c < 3; c++) {
-        const unsigned v = rgb[3 * p + c];
-        std::memcpy(w, T.s[v], 4);
-        w += T.n[v];
-        *w++ = c == 2 ? '\n' : ' ';
-      }
-      return w;
-    };
-    const size_t p0 = lo(k), p1 = lo(k + 1);
-    if (p1 == p0) return;
-    for (size_t p = p0; p + 1 < p1; p++) o = pixel(p, o);
-    char tail[16];
-    std::memcpy(o, tail, (size_t)(pixel(p1 - 1, tail) - tail));
-  };
-  const int fd = ::open(path, O_RDWR | O_CREAT | O_TRUNC, 0666);
+  const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
   if (fd < 0) return RT_ERR_IO;
   int rc = RT_OK;
-  void *m = MAP_FAILED;
-  if (::ftruncate(fd, (off_t)total) == 0) m = ::mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-  if (m != MAP_FAILED) {
-    char *base = static_cast<char *>(m);
-    std::memcpy(base, hdr, (size_t)hn);
-    run_chunks(nthr, nchunk, [&](size_t k) { format(k, base + off[k]); });
-    if (::munmap(m, total) != 0) rc = RT_ERR_IO;
-  } else {  // not mappable (nothing written yet: the file position is 0): format into buffers, write in order
-    std::vector<std::unique_ptr<char[]>> bufs(nchunk);
-    run_chunks(nthr, nchunk, [&](size_t k) {
-      bufs[k].reset(new (std::nothrow) char[off[k + 1] - off[k]]);
-      if (bufs[k]) format(k, bufs[k].get());
-    });
-    auto put = [&](const char *p, size_t len) {
-      while (rc == RT_OK && len > 0) {
-        const ssize_t w = ::write(fd, p, len);
-        if (w <= 0) rc = RT_ERR_IO;
-        else p += w, len -= (size_t)w;
+  auto put = [&](const char *p, size_t len) {
+    while (rc == RT_OK && len > 0) {
+      const ssize_t w = ::write(fd, p, len);
+      if (w < 0 && errno == EINTR) continue;
+      if (w <= 0) rc = RT_ERR_IO;
+      else p += w, len -= (size_t)w;
+    }
+  };
+  put(hdr, (size_t)hn);
+  if (binary) {
+    put(reinterpret_cast<const char *>(rgb), n * 3);
+  } else {
+    // "0".."255" and their lengths, built once (a function-local static: safe
+    // when several threads write images at the same time)
+    struct Tab {
+      char s[256][4];
+      unsigned char n[256];
+      Tab() {
+        for (int v = 0; v < 256; v++) n[v] = (unsigned char)std::snprintf(s[v], 4, "%d", v);
       }
     };
-    put(hdr, (size_t)hn);
-    for (size_t k = 0; k < nchunk; k++) {
-      if (!bufs[k]) rc = RT_ERR_IO;
-      put(bufs[k].get(), off[k + 1] - off[k]);
+    static const Tab T;
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t nthr = n < ((size_t)1 << 16) ? 1 : std::max<size_t>(1, std::min<size_t>(hw ? hw : 1, 16));
+    const size_t nchunk = nthr == 1 ? 1 : nthr * 4;
+    std::vector<std::unique_ptr<char[]>> bufs(nchunk);
+    std::vector<size_t> len(nchunk, 0);
+    std::vector<unsigned char> done(nchunk, 0);  // under mu
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<size_t> next{0};
+    // claims and formats the next unclaimed range (false: none left); at most
+    // 12 bytes per pixel, each number as its 4-byte table slot (the next
+    // write overwrites the slot's tail; the buffer has 4 bytes of room)
+    auto format_next = [&]() {
+      const size_t k = next.fetch_add(1);
+      if (k >= nchunk) return false;
+      const size_t p0 = n * k / nchunk, p1 = n * (k + 1) / nchunk;
+      char *o = new (std::nothrow) char[(p1 - p0) * 12 + 4];
+      if (o) {
+        char *const b = o;
+        for (size_t p = p0; p < p1; p++) {
+          for (int c = 0; c < 3; c++) {
+            const unsigned v = rgb[3 * p + c];
+            std::memcpy(o, T.s[v], 4);
+            o += T.n[v];
+            *o++ = c == 2 ? '\n' : ' ';
+          }
+        }
+        bufs[k].reset(b);
+        len[k] = (size_t)(o - b);
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        done[k] = 1;
+      }
+      cv.notify_all();
+      return true;
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nthr; t++) {
+      try {
+        th.emplace_back([&] {
+          while (format_next()) {
+          }
+        });
+      } catch (...) {
+        break;  // the started threads and this one format the rest
+      }
     }
+    for (size_t k = 0; k < nchunk; k++) {
+      for (;;) {
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          if (done[k]) break;
+          if (next.load() >= nchunk) {  // claimed by a helper: wait for it
+            cv.wait(lk, [&] { return done[k] != 0; });
+            break;
+          }
+        }
+        format_next();  // nothing finished yet: format an unclaimed range here
+      }
+      if (!bufs[k]) rc = RT_ERR_IO;  // (allocation failed)
+      else put(bufs[k].get(), len[k]);
+      bufs[k].reset();
+    }
+    for (auto &t : th) t.join();
   }
   if (::close(fd) != 0) rc = RT_ERR_IO;
   return rc;

@@ -46,5 +46,70 @@ def main():
                       os.path.getsize(out)), flush=True)
 
 
+def split():
+    """The render split: enqueue into device memory, completion, and the
+    device-to-host copy into pageable vs pinned memory, in a fresh context."""
+    import torch
+
+    scene = sys.argv[1] if len(sys.argv) > 1 else "complex"
+    W, H, D = 1920, 1080, 4
+    path = os.path.join(REPO, "cs420-ray-tracer_amd", "scenes", scene + ".txt")
+    pinned = torch.empty(W * H * 3, dtype=torch.uint8, pin_memory=True)
+    page = bytearray(W * H * 3)
+    for k in range(3):
+        sc = rt_hip.Scene.load(path)
+        r = rt_hip.Renderer(0)
+        r.upload(sc)
+        dev = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r.render_async(sc.camera(), W, H, D, None, dev.data_ptr())
+        t1 = time.perf_counter()
+        st = r.stats()
+        t2 = time.perf_counter()
+        pinned.copy_(dev)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        host = dev.cpu()
+        t4 = time.perf_counter()
+        import ctypes
+        ctypes.memmove((ctypes.c_char * len(page)).from_buffer(page), host.data_ptr(), len(page))
+        t5 = time.perf_counter()
+        r.close()
+        print("split %d: enqueue %.3f, to completion %.3f (kernel %.3f), D2H pinned %.3f, D2H pageable %.3f, "
+              "memcpy %.3f ms" % (k, (t1 - t0) * 1e3, (t2 - t1) * 1e3, st.kernel_ms, (t3 - t2) * 1e3,
+                                  (t4 - t3) * 1e3, (t5 - t4) * 1e3), flush=True)
+
+
+def pin_costs():
+    """What pinning the output costs in a process: hipHostMalloc / hipHostFree
+    of a 1080p RGB8 buffer, hipHostRegister / Unregister of a pageable one."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    nbytes = 1920 * 1080 * 3
+    for k in range(3):
+        p = ctypes.c_void_p()
+        t0 = time.perf_counter()
+        assert hip.hipHostMalloc(ctypes.byref(p), ctypes.c_size_t(nbytes), 0) == 0
+        t1 = time.perf_counter()
+        ctypes.memset(p, 0, nbytes)
+        t2 = time.perf_counter()
+        hip.hipHostFree(p)
+        t3 = time.perf_counter()
+        buf = (ctypes.c_char * nbytes)()
+        t4 = time.perf_counter()
+        assert hip.hipHostRegister(buf, ctypes.c_size_t(nbytes), 0) == 0
+        t5 = time.perf_counter()
+        hip.hipHostUnregister(buf)
+        t6 = time.perf_counter()
+        print("pin %d: hipHostMalloc %.3f, first touch %.3f, hipHostFree %.3f, hipHostRegister %.3f, "
+              "Unregister %.3f ms" % (k, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, (t5 - t4) * 1e3,
+                                      (t6 - t5) * 1e3), flush=True)
+
+
 if __name__ == "__main__":
     main()
+    if os.environ.get("E2E_SPLIT", "1") == "1":
+        split()
+        pin_costs()

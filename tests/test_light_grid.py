@@ -392,3 +392,39 @@ def test_sphere_grid_goldens(monkeypatch):
                 assert bytes(rgb) == want, (name, n, diff_summary(bytes(rgb), want))
         finally:
             r.close()
+
+
+@pytest.mark.gpu
+def test_sphere_grids_built_lazily(monkeypatch):
+    """Default policy: rt_upload_scene builds no sphere grids; a scene's first
+    one-frame launch sweeps, its second launch (or a first multi-frame launch)
+    builds them -- every render equal to the golden either way."""
+    import rt_hip
+    import torch
+    from conftest import golden_rgb, manifest, scene_path
+
+    monkeypatch.delenv("RT_HIP_SPHERE_GRID", raising=False)
+    name = "complex_97x61_d4"
+    m = manifest()[name]
+    want = golden_rgb(name)
+    sc = rt_hip.Scene.load(scene_path(m["scene"]))
+    r = rt_hip.Renderer(0)
+    try:
+        W, H, D = m["width"], m["height"], m["depth"]
+        r.upload(sc)
+        assert r.info().sphere_grids == 0
+        rgb, _ = r.render(sc.camera(), W, H, D)
+        assert bytes(rgb) == want and r.info().sphere_grids == 0
+        rgb, _ = r.render(sc.camera(), W, H, D)
+        assert bytes(rgb) == want and r.info().sphere_grids > 0
+        r.upload(sc)  # a new upload: pending again; a 3-frame launch builds them at once
+        assert r.info().sphere_grids == 0
+        buf = torch.zeros((3, H, W, 3), dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
+        r.render_frames_async([sc.camera()] * 3, W, H, D, None, buf.data_ptr(), H * W * 3)
+        r.stats()
+        assert r.info().sphere_grids > 0
+        for f in range(3):
+            assert buf[f].cpu().numpy().tobytes() == want, f
+    finally:
+        r.close()
