@@ -282,12 +282,14 @@ def moving_camera(rt_hip, torch, r, cam, W, H, D, rows, shard, F, launches=2):
                     "frame): a camera grid per frame built on the device in each launch" % (launches, F)}
 
 
-def end_to_end(rt_hip, scene_file, W, H, D, device, runs=3):
+def end_to_end(rt_hip, scene_file, W, H, D, device, runs=5):
     """The drop-in path end to end in a fresh context (what ray_hip does):
     parse, rt_create, rt_upload_scene, one synchronous render to host memory,
     rt_write_ppm P3.  Median over `runs` of each part and of the total."""
     import tempfile
     import time as _t
+
+    import numpy as np
 
     parts = {k: [] for k in ("parse_ms", "create_ms", "upload_ms", "render_ms", "write_p3_ms", "total_ms")}
     up_parts = {k: [] for k in ("bvh_ms", "light_grids_ms", "sphere_grids_ms", "behind_grid_ms")}
@@ -307,7 +309,8 @@ def end_to_end(rt_hip, scene_file, W, H, D, device, runs=3):
                 for k, v in zip(up_parts, (info.bvh_build_ms, info.light_grid_build_ms, info.sphere_grid_build_ms,
                                            info.behind_grid_build_ms)):
                     up_parts[k].append(v)
-            rgb, st = r.render(cam, W, H, D)
+            # the image buffer as ray_hip allocates it (uninitialised: the render writes every byte)
+            rgb, st = r.render(cam, W, H, D, out=np.empty(W * H * 3, np.uint8))
             t.append(_t.perf_counter())
             rt_hip.write_ppm(out, rgb, W, H)
             t.append(_t.perf_counter())

@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -83,7 +84,7 @@ struct Result {
 };
 
 // Single device: render the full frame.
-int render_single(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::vector<uint8_t> &img, Result &res) {
+int render_single(const Opts &o, const rt_scene &sc, const rt_camera &cam, uint8_t *img, Result &res) {
   rt_ctx *ctx = nullptr;
   CK(rt_create(o.device, &ctx));
   CK(rt_upload_scene(ctx, &sc));
@@ -91,7 +92,7 @@ int render_single(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::
   rt_stats st{};
   for (int it = 0; it < o.repeat; it++) {
     auto t0 = std::chrono::high_resolution_clock::now();
-    CK(rt_render(ctx, &cam, o.width, o.height, o.depth, nullptr, img.data(), 0, &st));
+    CK(rt_render(ctx, &cam, o.width, o.height, o.depth, nullptr, img, 0, &st));
     auto t1 = std::chrono::high_resolution_clock::now();
     res.wall_s = std::chrono::duration<double>(t1 - t0).count();
   }
@@ -105,7 +106,7 @@ int render_single(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::
 }
 
 // G devices in one process: cyclic 8-row bands, ncclGather to device 0, unpermute.
-int render_multi(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::vector<uint8_t> &img, Result &res) {
+int render_multi(const Opts &o, const rt_scene &sc, const rt_camera &cam, uint8_t *img, Result &res) {
   const int G = o.gpus, W = o.width, H = o.height, band = 8;
   rt_rows layout;
   CK(rt_rows_for_shard(H, band, 0, G, &layout));  // the layout bench.py's ranks use
@@ -155,7 +156,7 @@ int render_multi(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::v
     res.wall_s = std::chrono::duration<double>(t1 - t0).count();
   }
   HK(hipSetDevice(0));
-  HK(hipMemcpy(img.data(), image, (size_t)H * W * 3, hipMemcpyDeviceToHost));
+  HK(hipMemcpy(img, image, (size_t)H * W * 3, hipMemcpyDeviceToHost));
   res.kernel_ms = 0;
   for (int g = 0; g < G; g++) {
     rt_stats st{};
@@ -180,9 +181,11 @@ int render_multi(const Opts &o, const rt_scene &sc, const rt_camera &cam, std::v
 }
 
 int render_pass(const Opts &o, const rt_scene &sc, const rt_camera &cam, const char *label, const char *file) {
-  std::vector<uint8_t> img((size_t)o.width * o.height * 3);
+  // the image (every byte written by the render; not zero-filled first: the
+  // reference's framebuffer is value-initialised, this one need not be)
+  std::unique_ptr<uint8_t[]> img(new uint8_t[(size_t)o.width * o.height * 3 + 1]);
   Result res;
-  int rc = (o.gpus > 1 || o.force_gather) ? render_multi(o, sc, cam, img, res) : render_single(o, sc, cam, img, res);
+  int rc = (o.gpus > 1 || o.force_gather) ? render_multi(o, sc, cam, img.get(), res) : render_single(o, sc, cam, img.get(), res);
   if (rc) return rc;
   if (o.mode == "hip")
     std::printf("GPU rendering time: %g seconds\n", res.wall_s);  // main_gpu.cu:519
@@ -202,7 +205,7 @@ int render_pass(const Opts &o, const rt_scene &sc, const rt_camera &cam, const c
         res.kernel_ms, res.wall_s * 1e3, rays / (res.kernel_ms * 1e-3) / 1e6);
   }
   std::fflush(stdout);
-  int wrc = rt_write_ppm(file, img.data(), o.width, o.height, o.p6 ? 1 : 0);
+  int wrc = rt_write_ppm(file, img.get(), o.width, o.height, o.p6 ? 1 : 0);
   if (wrc != RT_OK) {
     std::fprintf(stderr, "could not write %s: %s\n", file, rt_error_string(wrc));
     return 1;
