@@ -726,7 +726,9 @@ __device__ __forceinline__ int home_acquire(unsigned long long *bits, int nwords
   if ((threadIdx.x & 63) == 0) {
     int w = (int)(blockIdx.x % (unsigned)nwords);
     // the first try: a bit picked by the workgroup id as well (a half-full word
-    // then takes one atomic, not two); it learns the word
+    // then takes one atomic, not two); it learns the word.  (Lowest-free-bit
+    // first, to keep the homes in use few and L2-resident, measured the same
+    // HBM writes and frame time: profiles/r7f/.)
     unsigned long long cur = ~(1ull << ((blockIdx.x / (unsigned)nwords) & 63u));
 #ifdef RT_CHECK
     long long spins = 0;
