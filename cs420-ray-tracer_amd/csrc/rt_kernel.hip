@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <mutex>
 #include <string>
 
 #include "rt_hip.h"
@@ -3249,13 +3250,32 @@ int rt_create(int device, rt_ctx **out) {
   std::memset(c->h_counters, 0, kShards * kShardStride * sizeof(unsigned long long));
   for (int i = 0; i < rt_ctx::kRing; i++)
     if (hipEventCreate(&c->ev0[i]) != hipSuccess || hipEventCreate(&c->ev1[i]) != hipSuccess) return bail(RT_ERR_HIP);
-  // load the kernels' code object on this device now (HIP loads it lazily at
-  // a process's first launch, ~8 ms): a drop-in's first render -- the time
-  // ray_serial prints, main.cpp:139-163 -- is then the render alone
+  // The HIP runtime's one-time work in a process, done here rather than
+  // inside the first render: the kernels' code object loads at the first
+  // launch, and the first blocking host-to-device copy, the first large
+  // asynchronous copy (the staging path) each cost ~8 ms on the box
+  // (scripts/copy_warm_probe.cpp).  So a drop-in's first render -- the time
+  // ray_serial prints, main.cpp:139-163 -- is the render alone.  Once per
+  // process and device.
   {
-    hipFuncAttributes fa;
-    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&render_kernel<false, true, 1, kStackMerge, true, true>));
-    (void)hipGetLastError();
+    static std::mutex warm_mu;
+    static std::vector<int> warmed;
+    std::lock_guard<std::mutex> lk(warm_mu);
+    if (std::find(warmed.begin(), warmed.end(), device) == warmed.end()) {
+      hipFuncAttributes fa;
+      (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&render_kernel<false, true, 1, kStackMerge, true, true>));
+      std::vector<unsigned char> h((size_t)1 << 20);
+      void *d = nullptr;
+      if (hipMalloc(&d, h.size()) == hipSuccess) {
+        (void)hipMemcpy(d, h.data(), 8, hipMemcpyHostToDevice);
+        (void)hipMemcpyAsync(d, h.data(), h.size(), hipMemcpyHostToDevice, c->stream);
+        (void)hipMemcpyAsync(h.data(), d, h.size(), hipMemcpyDeviceToHost, c->stream);
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(d);
+      }
+      (void)hipGetLastError();
+      warmed.push_back(device);
+    }
   }
   *out = c;
   return RT_OK;
