@@ -275,7 +275,7 @@ typedef struct rt_info {
     int32_t sphere_grids;        /* spheres with a sphere grid (reflection rays' closest hit; 0: none) */
     int32_t sphere_grid_n;       /* their cells per cube-map face edge */
     uint64_t sphere_grid_entries;  /* list entries of all sphere grids (8 bytes each) */
-    double sphere_grid_build_ms; /* host wall time of their build, part of upload_ms */
+    double sphere_grid_build_ms; /* host wall time of their build (by the scene's first multi-frame or second launch) */
     int32_t behind_grid;         /* 1: the scene has a behind grid (closest-hit lines' part behind their origin) */
     int32_t behind_grid_last;    /* 1: the most recent launch's BVH walks used it */
     uint64_t behind_grid_cells;  /* its cells */
