@@ -3027,9 +3027,13 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     }
     // the sphere grids, lazily (sg_pending): the scene's first multi-frame
     // launch or its second launch builds them, before the launch's timing
+    // (a speed-up: if its build fails the launch runs without the grids)
     if (fast && kCull && c->sg_pending && (nf > 1 || c->scene_launches > 0)) {
-      const int rc = sphere_grids(c);
-      if (rc != RT_OK) return rc;
+      if (sphere_grids(c) != RT_OK) {
+        (void)hipGetLastError();
+        c->err.clear();
+        c->sg_ok = false;
+      }
     }
     // the camera grids' host part (policy, tables, buffers) first; the
     // launch's timing starts after it: the grids' device passes ahead of the
