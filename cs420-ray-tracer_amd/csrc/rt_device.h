@@ -571,17 +571,6 @@ struct BvhArgs {
 };
 constexpr int kOrderedStack = 24;  // pending far children; the host requires depth <= this
 
-// Bytes per wave of the LDS region at ostk_off: the ordered walk's stacks, or
-// (closest hits along the grid, behind_coop) the wave's staged rays.
-__host__ __device__ __forceinline__ size_t walk_lds_bytes(const BvhArgs &bv);
-
-// The default-path kernels (kFast template argument): 0 = every path compiled
-// in; kFastBvh = only the ordered 4-wide BVH walk and the light-grid shadow
-// queries; kFastGrid = the same for scenes whose closest hits walk the
-// uniform grid, with the wave-cooperative walk behind the origins and no BVH
-// closest-hit walk.
-constexpr int kFastBvh = 1, kFastGrid = 2;
-
 // Dynamic LDS (every extern __shared__ array starts at its base).
 extern __shared__ __attribute__((aligned(32))) unsigned char rt_dyn_lds[];
 
@@ -1003,63 +992,42 @@ __device__ __forceinline__ void closest_test(const SphGeo &s, int i, D3 o, D3 d,
 // rounded up; w = -1: no more entries; w = -2 in slot 3: entries x..y of the
 // overflow list continue the cell), so a cell is one 64-B load, issued one
 // cell ahead; sphere ids are read only for the spheres that pass.
-// The fp32 form of a grid walk's line: the origin in grid coordinates (p),
-// the walk direction v (+d for the whole line, -d behind the origin; s is then
-// the line parameter t or -t), its reciprocals, and the part [s0, s1] of the
-// line inside the grid box [0, n cs]^3 (s0 > s1: it misses the grid, or NaN).
-struct GridRay {
-  float ox, oy, oz, dx, dy, dz, dd_hi, dd_lo, p0, p1, p2, v0, v1, v2, i0, i1, i2, s0, s1;
-};
-template <bool kWhole>
-__host__ __device__ __forceinline__ GridRay grid_ray(const BvhArgs &bv, D3 o, D3 d) {
+template <bool kWhole, typename F, typename B>
+__host__ __device__ __forceinline__ void grid_line(const BvhArgs &bv, D3 o, D3 d, Work &work, F &&test_fn,
+                                                   B &&best_fn) {
   const UgArgs &ug = bv.ug;
-  GridRay r;
-  r.ox = (float)(o.x - bv.c0x), r.oy = (float)(o.y - bv.c0y), r.oz = (float)(o.z - bv.c0z);
-  r.dx = (float)d.x, r.dy = (float)d.y, r.dz = (float)d.z;
-  const float d2 = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-  r.dd_hi = d2 * (1.0f + 1e-5f), r.dd_lo = d2 * (1.0f - 1e-5f);
+  for (int k = 0; k < ug.nglob; ++k) {
+    work.exact += 1;
+    test_fn((int)ug.glob[k]);
+  }
+  const float ox = (float)(o.x - bv.c0x), oy = (float)(o.y - bv.c0y), oz = (float)(o.z - bv.c0z);
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float d2 = dx * dx + dy * dy + dz * dz;
+  const float dd_hi = d2 * (1.0f + 1e-5f), dd_lo = d2 * (1.0f - 1e-5f);
+  const float pm = bv.pmargin;
   const float cs = ug.cs;
-  r.p0 = r.ox - ug.gx, r.p1 = r.oy - ug.gy, r.p2 = r.oz - ug.gz;  // the origin in grid coordinates
+  const float p0 = ox - ug.gx, p1 = oy - ug.gy, p2 = oz - ug.gz;  // the origin in grid coordinates
   // walk direction: +d for the whole line, -d behind the origin (then s = -t)
-  r.v0 = kWhole ? r.dx : -r.dx, r.v1 = kWhole ? r.dy : -r.dy, r.v2 = kWhole ? r.dz : -r.dz;
-  r.i0 = 1.0f / r.v0, r.i1 = 1.0f / r.v1, r.i2 = 1.0f / r.v2;  // +-inf for a zero component
+  const float v0 = kWhole ? dx : -dx, v1 = kWhole ? dy : -dy, v2 = kWhole ? dz : -dz;
+  const float i0 = 1.0f / v0, i1 = 1.0f / v1, i2 = 1.0f / v2;  // +-inf for a zero component
   // the walked part inside the grid box [0, n cs]^3: s in [s0, s1]
-  r.s0 = kWhole ? -__builtin_inff() : 0.0f, r.s1 = __builtin_inff();
+  float s0 = kWhole ? -__builtin_inff() : 0.0f, s1 = __builtin_inff();
   auto clip = [&](float p, float iv, int n) {
     const float ta = (0.0f - p) * iv, tb = ((float)n * cs - p) * iv;  // a zero component: +-inf or NaN
     if (iv == __builtin_inff() || iv == -__builtin_inff()) {
-      if (!(p >= 0.0f && p <= (float)n * cs)) r.s1 = -__builtin_inff();  // parallel to the slab and outside it
+      if (!(p >= 0.0f && p <= (float)n * cs)) s1 = -__builtin_inff();  // parallel to the slab and outside it
     } else {
-      r.s0 = fmaxf(r.s0, fminf(ta, tb));
-      r.s1 = fminf(r.s1, fmaxf(ta, tb));
+      s0 = fmaxf(s0, fminf(ta, tb));
+      s1 = fminf(s1, fmaxf(ta, tb));
     }
   };
-  clip(r.p0, r.i0, ug.nx);
-  clip(r.p1, r.i1, ug.ny);
-  clip(r.p2, r.i2, ug.nz);
-  return r;
-}
-
-// Walks the cells the line passes for s in [sa, sb] (within [s0, s1]), in
-// order, from the cell holding s = sa to the one holding sb, handing the
-// listed spheres that pass the prefilter to test_fn.  kStop: stop after the
-// first cell whose exit lies beyond best_fn() + tol (closest hits along +d).
-// kWhole walks along +d, where cells with exit s < 0 lie wholly behind the
-// origin; along -d every cell does.
-// kPrefetch: the next cell's record is loaded while this one's are tested
-// (16 more VGPRs; behind_coop's walks do without).
-template <bool kWhole, bool kStop, bool kPrefetch = true, typename F, typename B>
-__host__ __device__ __forceinline__ void grid_walk(const BvhArgs &bv, const GridRay &r, float sa, float sb,
-                                                   Work &work, F &&test_fn, B &&best_fn) {
-  const UgArgs &ug = bv.ug;
-  const float pm = bv.pmargin;
-  const float cs = ug.cs;
-  const float ox = r.ox, oy = r.oy, oz = r.oz, dx = r.dx, dy = r.dy, dz = r.dz;
-  const float p0 = r.p0, p1 = r.p1, p2 = r.p2, v0 = r.v0, v1 = r.v1, v2 = r.v2, i0 = r.i0, i1 = r.i1, i2 = r.i2;
-  const float s1 = sb;
+  clip(p0, i0, ug.nx);
+  clip(p1, i1, ug.ny);
+  clip(p2, i2, ug.nz);
+  if (!(s0 <= s1)) return;  // misses the grid (or NaN)
   const float ics = 1.0f / cs;
   auto cell_of = [&](float p, float v, int n) {
-    const int c = (int)floorf((p + v * sa) * ics);
+    const int c = (int)floorf((p + v * s0) * ics);
     return c < 0 ? 0 : (c >= n ? n - 1 : c);
   };
   int c0 = cell_of(p0, v0, ug.nx), c1 = cell_of(p1, v1, ug.ny), c2 = cell_of(p2, v2, ug.nz);
@@ -1096,8 +1064,8 @@ __host__ __device__ __forceinline__ void grid_walk(const BvhArgs &bv, const Grid
     }
     const int cur = ci;
     float4 n0 = r0, n1 = r1, n2 = r2, n3 = r3;
-    if (more) ci = RT_CK(kCkUgCell, (c2 * ug.ny + c1) * ug.nx + c0, ug.nx * ug.ny * ug.nz);
-    if (kPrefetch && more) {
+    if (more) {
+      ci = RT_CK(kCkUgCell, (c2 * ug.ny + c1) * ug.nx + c0, ug.nx * ug.ny * ug.nz);
       n0 = ug.rec[4 * ci];
       n1 = ug.rec[4 * ci + 1];
       n2 = ug.rec[4 * ci + 2];
@@ -1111,8 +1079,8 @@ __host__ __device__ __forceinline__ void grid_walk(const BvhArgs &bv, const Grid
       const float cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
       const float x2 = cx * cx + cy * cy + cz * cz;  // (distance to the line)^2 |d|^2
       const float ro = q.w + pm, ri = q.w * (1.0f - 0x1p-22f) - pm;
-      if (x2 > ro * ro * r.dd_hi) return;                          // misses the grown sphere
-      if (behind && ri > 0.0f && x2 < ri * ri * r.dd_lo) return;  // runs deep inside it
+      if (x2 > ro * ro * dd_hi) return;                          // misses the grown sphere
+      if (behind && ri > 0.0f && x2 < ri * ri * dd_lo) return;  // runs deep inside it
       const int id = (int)ids[id_at];
       if (id == last) return;
       last = id;
@@ -1132,203 +1100,12 @@ __host__ __device__ __forceinline__ void grid_walk(const BvhArgs &bv, const Grid
     };
     if (slot(r0, 0) && slot(r1, 1) && slot(r2, 2)) slot(r3, 3);
     if (!more) break;
-    if (kStop && (double)ex > best_fn() + (double)ug.tol) break;
-    if (kPrefetch) {
-      r0 = n0;
-      r1 = n1;
-      r2 = n2;
-      r3 = n3;
-    } else {
-      r0 = ug.rec[4 * ci];
-      r1 = ug.rec[4 * ci + 1];
-      r2 = ug.rec[4 * ci + 2];
-      r3 = ug.rec[4 * ci + 3];
-    }
+    if (kWhole && (double)ex > best_fn() + (double)ug.tol) break;
+    r0 = n0;
+    r1 = n1;
+    r2 = n2;
+    r3 = n3;
   }
-}
-
-// The part of a closest-hit line AHEAD of the origin's cell (whole-line walks
-// of the merged kernels, behind_coop below walks the rest): the global
-// spheres, then the cells from the one holding s = max(s0, 0), stopping as
-// grid_line<true> does.
-template <typename F, typename B>
-__host__ __device__ __forceinline__ void grid_ahead_line(const BvhArgs &bv, D3 o, D3 d, Work &work, F &&test_fn,
-                                                         B &&best_fn) {
-  const UgArgs &ug = bv.ug;
-  for (int k = 0; k < ug.nglob; ++k) {
-    work.exact += 1;
-    test_fn((int)ug.glob[k]);
-  }
-  const GridRay r = grid_ray<true>(bv, o, d);
-  const float sa = fmaxf(r.s0, 0.0f);
-  if (!(sa <= r.s1)) return;  // nothing of the grid ahead (or NaN)
-  grid_walk<true, true>(bv, r, sa, r.s1, work, test_fn, best_fn);
-}
-
-// Piece k of mo of a line's segment behind its origin, [s0, min(s1, 0)]:
-// cut at k / mo (the same expression on both sides of a cut), the segment's
-// ends exact, each piece but the last running on by the grid's tol so that
-// neighbouring pieces overlap (tests/native/ug_check.cpp walks lines in
-// pieces like this on the CPU).
-__host__ __device__ __forceinline__ void behind_piece(const BvhArgs &bv, const GridRay &r, int k, int mo, float &sa,
-                                                      float &sb) {
-  const float se = fminf(r.s1, 0.0f);
-  sa = k == 0 ? r.s0 : r.s0 + (se - r.s0) * ((float)k / (float)mo);
-  sb = k + 1 == mo ? se : fminf(se, r.s0 + (se - r.s0) * ((float)(k + 1) / (float)mo) + bv.ug.tol);
-}
-
-// The part of the active lanes' closest-hit lines BEHIND their origins
-// ([s0, min(s1, 0)] of grid_ray<true>), walked by the whole wave together
-// (cfg 5: 65 % of a reflection ray's cells lie behind its origin, and one
-// lane per line left half the lanes idle -- SIMD efficiency 0.54 by
-// scripts/ug_sim.cpp; these walks were 0.63 of 2.38 ms per frame,
-// profiles/r7s/).  Each line's segment is cut into pieces of about the same
-// number of cells (P = the wave's cells / 64, at least 4), the pieces are
-// dealt to the lanes (at most two rounds), a lane walks its piece of its
-// owner's line with the owner's ray (grid_walk from the cell holding the
-// piece's start to the one holding its end -- consecutive pieces overlap by
-// the grid's tol, so every point of the segment is walked) and tests the candidates with the owner's fp64
-// arithmetic, and each owner folds its pieces' lexicographic (t, index)
-// minima into its own.  The candidates are a superset of grid_line's over
-// the same cells, each result a root of the reference's test, so the minimum
-// is the same.  Wave-uniform call; fold(t, i) for the owner lanes.
-// The wave's staged rays: [component][lane] doubles (o.x o.y o.z d.x d.y d.z)
-// in the LDS region of the ordered walk's stacks, which closest hits along the
-// grid do not use (the host reserves kCoopBytes per wave there: walk_lds_bytes).
-constexpr int kCoopBytes = 6 * 64 * 8;
-__host__ __device__ __forceinline__ size_t walk_lds_bytes(const BvhArgs &bv) {
-  if (!bv.ordered) return 0;
-  const size_t st = (size_t)bv.odepth * 64 * sizeof(int2);
-  return (bv.ug.on && bv.ug.closest && st < (size_t)kCoopBytes) ? (size_t)kCoopBytes : st;
-}
-typedef __attribute__((address_space(3))) double LdsF64;
-__device__ __forceinline__ LdsF64 *coop_stage(const BvhArgs &bv) {
-  typedef __attribute__((address_space(3))) unsigned char LdsByte;
-  LdsByte *base = (LdsByte *)(rt_dyn_lds) + bv.ostk_off;
-  return reinterpret_cast<LdsF64 *>(base + (size_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCoopBytes);
-}
-template <typename F>
-__device__ __forceinline__ void behind_coop(const SphGeo *__restrict__ g, int n, const BvhArgs &bv, bool act, D3 &o,
-                                            D3 &d, Work &work, F &&fold) {
-  const int lane = (int)(threadIdx.x & 63);
-  const UgArgs &ug = bv.ug;
-  LdsF64 *st = coop_stage(bv);
-  int nc = 0;  // this lane's segment, in cells (an estimate: only the balance depends on it)
-  {
-    const GridRay r = grid_ray<true>(bv, o, d);
-    const float se = fminf(r.s1, 0.0f);
-    if (act && r.s0 < se) {
-      const float ics = 1.0f / ug.cs;
-      auto span = [&](float p, float v, int nn) {
-        const float fa = floorf((p + v * r.s0) * ics), fb = floorf((p + v * se) * ics);
-        const float df = fabsf(fb - fa);
-        return df < (float)nn ? (int)df : nn;
-      };
-      nc = 1 + span(r.p0, r.v0, ug.nx) + span(r.p1, r.v1, ug.ny) + span(r.p2, r.v2, ug.nz);
-    }
-  }
-  int tot = nc;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
-  if (tot == 0) return;
-  // the lanes' rays go to LDS (and come back at the end), so they hold no
-  // registers while the pieces are walked
-  st[0 * 64 + lane] = o.x, st[1 * 64 + lane] = o.y, st[2 * 64 + lane] = o.z;
-  st[3 * 64 + lane] = d.x, st[4 * 64 + lane] = d.y, st[5 * 64 + lane] = d.z;
-  const int P = (tot + 63) / 64 < 4 ? 4 : (tot + 63) / 64;
-  const int m = (nc + P - 1) / P;  // this lane's pieces
-  int incl = m;                    // inclusive prefix sum over the lanes
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int y = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += y;
-  }
-  const int base = incl - m;
-  const int M = __shfl(incl, 63, 64);  // pieces of the wave (<= 128)
-  for (int r0 = 0; r0 < M; r0 += 64) {
-    const int q = r0 + lane;
-    // the piece's owner: the first lane whose inclusive prefix exceeds q
-    int owner = 0;
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1) {
-      const int v = __shfl(incl, owner + step - 1, 64);
-      if (v <= q) owner += step;
-    }
-    owner = owner > 63 ? 63 : owner;
-    const int k = q - __shfl(base, owner, 64), mo = __shfl(m, owner, 64);
-    double pbt = kInf, pbn = __builtin_inf();
-    int pbi = -1;
-    if (q < M && k >= 0 && k < mo) {
-      // (read where used: the empty asm keeps the compiler from holding the
-      // six doubles in registers across the walk)
-      auto ray = [&](D3 &oo, D3 &dd) {
-        asm volatile("" ::: "memory");
-        oo = mk(st[0 * 64 + owner], st[1 * 64 + owner], st[2 * 64 + owner]);
-        dd = mk(st[3 * 64 + owner], st[4 * 64 + owner], st[5 * 64 + owner]);
-      };
-      D3 oo, dd;
-      ray(oo, dd);
-      const GridRay r = grid_ray<true>(bv, oo, dd);  // the owner's, bit for bit
-      float sa, sb;
-      behind_piece(bv, r, k, mo, sa, sb);
-      // sweep_closest's test with the owner's ray (re-read from LDS: rare)
-      grid_walk<true, false, false>(bv, r, sa, sb, work, [&](int i) {
-        D3 to, td;
-        ray(to, td);
-        const double a = dot(td, td), a4 = 4.0 * a, a2 = 2.0 * a;
-        double num;
-        const int rr = a2_ok(a2) ? intersect_num(g[RT_CK(kCkSphere, i, n)], to, td, a4, num) : 2;
-        if (rr == 1) {
-          if (num < pbn || i < pbi) {
-            const double t = num / a2;
-            if (t < pbt || (t == pbt && i < pbi)) {
-              pbt = t;
-              pbn = num;
-              pbi = i;
-            }
-          }
-        } else if (rr == 2) {
-          double t;
-          if (intersect(g[i], to, td, a4, a2, t) && (t < pbt || (t == pbt && i < pbi))) {
-            pbt = t;
-            pbn = __builtin_inf();
-            pbi = i;
-          }
-        }
-      }, [] { return 0.0; });
-    }
-    // each owner folds its pieces of this round (lanes first .. first + cnt - 1)
-    const int lo = base > r0 ? base : r0, hi = incl < r0 + 64 ? incl : r0 + 64;
-    const int cnt = hi > lo ? hi - lo : 0, first = lo - r0;
-    int cmax = cnt;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const int y = __shfl_xor(cmax, off, 64);
-      cmax = y > cmax ? y : cmax;
-    }
-    for (int j = 0; j < cmax; ++j) {
-      const int src = (first + j) & 63;
-      const double t = __shfl(pbt, src, 64);
-      const int i = __shfl(pbi, src, 64);
-      if (j < cnt && i >= 0) fold(t, i);
-    }
-  }
-  asm volatile("" ::: "memory");  // the lane's own ray comes back from LDS (not held across the walks)
-  o = mk(st[0 * 64 + lane], st[1 * 64 + lane], st[2 * 64 + lane]);
-  d = mk(st[3 * 64 + lane], st[4 * 64 + lane], st[5 * 64 + lane]);
-}
-
-template <bool kWhole, typename F, typename B>
-__host__ __device__ __forceinline__ void grid_line(const BvhArgs &bv, D3 o, D3 d, Work &work, F &&test_fn,
-                                                   B &&best_fn) {
-  const UgArgs &ug = bv.ug;
-  for (int k = 0; k < ug.nglob; ++k) {
-    work.exact += 1;
-    test_fn((int)ug.glob[k]);
-  }
-  const GridRay r = grid_ray<kWhole>(bv, o, d);
-  if (!(r.s0 <= r.s1)) return;  // misses the grid (or NaN)
-  grid_walk<kWhole, kWhole>(bv, r, r.s0, r.s1, work, test_fn, best_fn);
 }
 
 // Host-callable too (tests/native/ug_check.cpp runs this same code on the CPU).
@@ -1435,7 +1212,7 @@ __device__ __forceinline__ unsigned long long next_group(unsigned long long todo
 // kFast: the default configuration only (ordered 4-wide BVH walk); the other
 // walks are not compiled in, which keeps the default kernel's register
 // allocation free of their cold paths (render_kernel's kFast).
-template <bool kCull, int kFast = 0>
+template <bool kCull, bool kFast = false>
 __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
                                              bool act, D3 o, D3 d, int key, const BvhArgs &bv, double &best_t,
                                              Work &work) {
@@ -1536,17 +1313,6 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
   const bool any_need = have_bvh && __ballot(need) != 0;
   RT_T0(tv);
 #endif
-  if constexpr (kFast == kFastGrid) {
-    if (have_bvh && bv.ug.on && bv.ug.closest && __ballot(need)) {
-      behind_coop(g, n, bv, need, o, d, work, [&](double t, int i) {
-        if (t < bt || (t == bt && i < bi)) {
-          bt = t;
-          bn = __builtin_inf();  // no numerator for this best: every later candidate divides
-          bi = i;
-        }
-      });
-    }
-  }
   if (have_bvh && need) {
     // a box whose entry is beyond the best t (by the margin) holds no closer root;
     // spheres a group pass already tested are harmless to test again
@@ -1556,10 +1322,7 @@ __device__ __forceinline__ int sweep_closest(const SphGeo *__restrict__ g, const
       test(i);
       return true;
     };
-    if constexpr (kFast == kFastGrid) {
-      // the part behind the origin was walked by the whole wave (above)
-      grid_ahead_line(bv, o, d, work, test, [&] { return bt; });
-    } else if constexpr (kFast == kFastBvh) {
+    if constexpr (kFast) {
       if (bv.ug.on && bv.ug.closest) {
         grid_closest_line(bv, o, d, work, test, [&] { return bt; });
       } else {

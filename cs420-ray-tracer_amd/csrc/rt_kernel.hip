@@ -181,7 +181,7 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, int k) {
 // loop below (the hit lane's normal and view direction passed over) -- and each
 // hit lane then adds its lights' terms in file order (scene.h:117): the same
 // bits, in ceil(lights / lpp) passes instead of one per light.
-template <bool kCull, bool kArgMem = false, int kFast = 0, bool kWide = false>
+template <bool kCull, bool kArgMem = false, bool kFast = false, bool kWide = false>
 __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                           const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                           int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o,
@@ -350,7 +350,7 @@ __device__ __forceinline__ void shade_hit(const SphGeo *__restrict__ g, const do
 
 // The closest hit of bounce() (scene.h:41-61) for the `alive` lanes: sphere
 // index (-1: none) and t.  Wave-uniform control flow.
-template <bool kCull, bool kArgMem = false, int kFast = 0>
+template <bool kCull, bool kArgMem = false, bool kFast = false>
 __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const double *__restrict__ rad, int n,
                                            const BvhArgs &bv, bool alive, D3 o, D3 d, int key, Work &work,
                                            double &bt_out, bool cam_pass = false, int frame = 0) {
@@ -395,7 +395,7 @@ __device__ __forceinline__ int closest_hit(const SphGeo *__restrict__ g, const d
   return bi;
 }
 
-template <bool kCull, bool kArgMem = false, int kFast = 0, bool kWide = false>
+template <bool kCull, bool kArgMem = false, bool kFast = false, bool kWide = false>
 __device__ __forceinline__ void bounce(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                        const SphMat *__restrict__ mat, const LightD *__restrict__ slight, int n,
                                        int nl, D3 amb, const BvhArgs &bv, const LgArgs &lg_arg, bool alive, D3 o, D3 d,
@@ -768,7 +768,7 @@ __device__ __forceinline__ void home_release(unsigned long long *bits, int h) {
   if ((threadIdx.x & 63) == 0) atomicAnd(bits + (h >> 6), ~(1ull << (h & 63)));
 }
 
-template <bool kCull, int kFast, bool kWide = false>
+template <bool kCull, bool kFast, bool kWide = false>
 __device__ __forceinline__ void merge_tiles(const SphGeo *__restrict__ g, const double *__restrict__ rad,
                                             const SphMat *__restrict__ mat, const LightD *__restrict__ slight,
                                             const RenderArgs &a, int group, int frame, const CompactArgs &ca,
@@ -1066,7 +1066,7 @@ constexpr int wg_waves() {
   return kLdsGeo ? 4 : 1;
 }
 
-template <bool kLdsGeo, bool kCull, int kSamples, int kStack, int kFast = 0, bool kWide = false>
+template <bool kLdsGeo, bool kCull, int kSamples, int kStack, bool kFast = false, bool kWide = false>
 __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) void render_kernel(
     const RenderArgs a) {
   // Workgroups are dealt to the 8 XCDs round robin (b % 8), so every image
@@ -1126,7 +1126,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
   CompactArgs ca;
   ca.park = nullptr;
   if (!kLdsGeo)  // after the ordered walk's stacks (launch_tiles sizes both)
-    ca.park = reinterpret_cast<D3 *>(smem + stack_off + (size_t)kWg * walk_lds_bytes(a.bv)) +
+    ca.park = reinterpret_cast<D3 *>(smem + stack_off + (a.bv.ordered ? (size_t)kWg * a.bv.odepth * 64 * sizeof(int2) : 0)) +
               (size_t)wave * 64;
   ca.gstack = a.gstack;
   ca.npx = (size_t)a.rows.count * a.od.xw * nf;
@@ -1165,7 +1165,7 @@ __global__ __launch_bounds__((64 * wg_waves<kLdsGeo>()), RT_MIN_WAVES_PER_EU) vo
 // queue slot's [level][slot] entries of dstack), unwinds the chain's whole
 // stack -- the levels merge_tiles copied there at the deferral first -- and
 // stores the pixel.
-template <bool kCull, int kFast = 0, bool kWide = false>
+template <bool kCull, bool kFast = false, bool kWide = false>
 __global__ __launch_bounds__(64, RT_MIN_WAVES_PER_EU) void render_deferred(const RenderArgs a) {
   const unsigned shard = blockIdx.x % kShards, first = blockIdx.x / kShards;
   const int cap = a.dq_cap;
@@ -2876,7 +2876,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   lds = (lds + 31) & ~(size_t)31;
   // the kernel places the ordered walk's stacks from these same arguments
   if (bv.ordered)
-    lds += (size_t)kWg * walk_lds_bytes(bv);
+    lds += (size_t)kWg * bv.odepth * 64 * sizeof(int2);
   if (!kLds && kStack == kStackGlobal) lds += (size_t)kWg * 64 * sizeof(D3);  // parked colours (trace_wave)
   if (kStack == kStackMerge)  // the wave's ray queue and finished pixels (merge_tiles)
     lds += (size_t)c->merge_q * sizeof(QRay) + kPixbufBytes;
@@ -2963,7 +2963,7 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
   ra.merge_end = (int)(ntiles - tail);
   // merge_tiles' pixel bytes: after the scene and the walk stacks, where render_kernel's park/queue region starts
   ra.pix_off = (int)(((lds_layout(kLds, c->nsph, c->nlight, bv.nnodes).end + 31) & ~(size_t)31) +
-                     (size_t)kWg * walk_lds_bytes(bv));
+                     (bv.ordered ? (size_t)kWg * bv.odepth * 64 * sizeof(int2) : 0));
   // row k of frame f starts at ptr + f fstride + 3 (k W + x): dword aligned for every k, f and x = 8i
   ra.rows_dword = ((reinterpret_cast<uintptr_t>(od.ptr) | (uintptr_t)(3 * (size_t)W) | (uintptr_t)od.fstride) & 3) == 0;
   ra.defer_level = c->defer_level;
@@ -2988,18 +2988,11 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
     // the default configuration (ordered 4-wide BVH walk, light grids) has kernels
     // compiled with only those paths (kFast): no registers held for the others
     const bool fast = bv.ordered && bv.wide && lg.on;
-    // kFastGrid: the scene's closest hits walk the uniform grid (scenes above
-    // 1,024 spheres): kernels with the wave-cooperative walk of the lines'
-    // parts behind their origins (behind_coop) and no BVH walk
-    const bool fgrid = fast && kCull && bv.nnodes > 0 && bv.ug.on && bv.ug.closest && bv.ostk_off >= 0 &&
-                       walk_lds_bytes(bv) >= (size_t)kCoopBytes;
     // the light loop of sparse waves spread over the lanes (shade_hit kWide, the default)
     const bool wide = fast && (c->wide_mode >= 2 || (nf == 1 && c->wide_mode == 1));
     if (depth > 1) {  // the stack homes: 2 x the render kernel's resident waves
-      const void *kf = (fgrid && wide) ? reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack, kFastGrid, true>)
-                       : fgrid ? reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack, kFastGrid>)
-                       : wide   ? reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack, kFastBvh, true>)
-                       : fast ? reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack, kFastBvh>)
+      const void *kf = wide   ? reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack, true, true>)
+                       : fast ? reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack, true>)
                               : reinterpret_cast<const void *>(&render_kernel<kLds, kCull, kSamples, kStack>);
       if (kf != c->occ_kernel || lds != c->occ_lds) {
         int nb = 0;
@@ -3059,18 +3052,11 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       ra.sg = SgArgs{c->d_sg_start, c->d_sg_ent, c->d_sg_rho2, c->sg_n, 1, c->sg_nstart, c->sg_nent, c->nsph};
     c->cg_last = ra.cg.on != 0;
     c->cg_last_n = ra.cg.on ? ra.cg.N : 0;
-    if (fgrid && wide)
-      hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, kFastGrid, true>), grid, dim3(64 * kWg), lds,
-                         c->stream, ra);
-    else if (fgrid)
-      hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, kFastGrid>), grid, dim3(64 * kWg), lds, c->stream,
+    if (wide)
+      hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, true, true>), grid, dim3(64 * kWg), lds, c->stream,
                          ra);
-    else if (wide)
-      hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, kFastBvh, true>), grid, dim3(64 * kWg), lds,
-                         c->stream, ra);
     else if (fast)
-      hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, kFastBvh>), grid, dim3(64 * kWg), lds, c->stream,
-                         ra);
+      hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack, true>), grid, dim3(64 * kWg), lds, c->stream, ra);
     else
       hipLaunchKernelGGL((render_kernel<kLds, kCull, kSamples, kStack>), grid, dim3(64 * kWg), lds, c->stream, ra);
     if (ra.dq_cap > 0) {  // 48 one-wave workgroups per shard segment
@@ -3079,18 +3065,11 @@ int launch_tiles(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int depth,
       // the cull sweeps (synth200 1 % slower on the walk kernel)
       if (kCull && fast && c->defer_walk && bv.nnodes > 0 && bv.always && !(bv.ug.on && bv.ug.closest))
         hipLaunchKernelGGL(render_deferred_walk, dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
-      else if (fgrid && c->wide_mode == 3)
-        hipLaunchKernelGGL((render_deferred<kCull, kFastGrid, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds,
-                           c->stream, ra);
-      else if (fgrid)
-        hipLaunchKernelGGL((render_deferred<kCull, kFastGrid>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream,
-                           ra);
       else if (fast && c->wide_mode == 3)  // the deferred waves' tails spread their light loops too
-        hipLaunchKernelGGL((render_deferred<kCull, kFastBvh, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds,
-                           c->stream, ra);
-      else if (fast)
-        hipLaunchKernelGGL((render_deferred<kCull, kFastBvh>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream,
+        hipLaunchKernelGGL((render_deferred<kCull, true, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream,
                            ra);
+      else if (fast)
+        hipLaunchKernelGGL((render_deferred<kCull, true>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
       else
         hipLaunchKernelGGL((render_deferred<kCull>), dim3(RT_DEFER_WGS * kShards), dim3(64), lds, c->stream, ra);
     }
@@ -3115,7 +3094,7 @@ int launch_render4(rt_ctx *c, size_t lds, const Cam &cam, int W, int H, int dept
     // 10 waves, 12 % slower); otherwise the per-pixel global stack
     if constexpr (!kLds && kSamples == 1) {
       const BvhArgs bv = bvh_args(c, cam);
-      const size_t stacks = walk_lds_bytes(bv);
+      const size_t stacks = bv.ordered ? (size_t)bv.odepth * 64 * sizeof(int2) : 0;
       if (od.fmt == RT_FB_RGB8 && !od.full && od.x0 == 0 && od.xw == W)
         for (int q = c->merge_q_max; q >= 8; q /= 2)  // the longest queue that keeps 12 waves per CU
           if (12 * (stacks + (size_t)q * sizeof(QRay) + kPixbufBytes + ((lds + 31) & ~(size_t)31)) <= 160 * 1024) {

@@ -411,7 +411,7 @@ void ugrid(int seeds, Stat &S) {
     const double g0[3] = {(double)ug.gx + c0[0], (double)ug.gy + c0[1], (double)ug.gz + c0[2]};
     const int ncell[3] = {ug.nx, ug.ny, ug.nz};
     const double cs = (double)ug.cs, tol = 1e-7 * diam;
-    std::vector<char> seen(N), seen2(N);
+    std::vector<char> seen(N);
     for (int li = 0; li < 3000; li++) {
       const int si = (int)(rng() % (N - 1));
       const V C = s.C[si];
@@ -468,32 +468,6 @@ void ugrid(int seeds, Stat &S) {
             std::printf("WRONG ugrid seed %d line %d grid (%d, %.17g) reference (%d, %.17g)\n", seed, li, bi, bt, ri,
                         rt);
         }
-        // the cooperative form: behind_coop's pieces (1-8), then grid_ahead_line
-        const int mo = 1 + li % 8;
-        double ct = 1e20;
-        int ci = -1;
-        auto cfold = [&](int i) {
-          double t;
-          seen2[i] = 1;
-          if (ref_test(s.C[i], s.R[i], o, d, t) && (t < ct || (t == ct && i < ci))) ct = t, ci = i;
-        };
-        std::fill(seen2.begin(), seen2.end(), 0);
-        const D3 O{o.x, o.y, o.z}, Dd{d.x, d.y, d.z};
-        const rtk::GridRay gr = rtk::grid_ray<true>(bv, O, Dd);
-        if (gr.s0 < std::fmin(gr.s1, 0.0f))
-          for (int k = 0; k < mo; k++) {
-            float sa, sb;
-            rtk::behind_piece(bv, gr, k, mo, sa, sb);
-            rtk::Work w3;
-            rtk::grid_walk<true, false, false>(bv, gr, sa, sb, w3, cfold, [] { return 0.0; });
-          }
-        rtk::Work w4;
-        rtk::grid_ahead_line(bv, O, Dd, w4, cfold, [&] { return ct; });
-        if (ci != ri || (ri >= 0 && ct != rt)) {
-          if (++S.wrong <= 10)
-            std::printf("WRONG ugrid pieces seed %d line %d grid (%d, %.17g) reference (%d, %.17g)\n", seed, li, ci,
-                        ct, ri, rt);
-        }
       }
       for (int i = 0; i < N; i++) {
         const long double ox = (long double)o.x - s.C[i].x, oy = (long double)o.y - s.C[i].y,
@@ -510,10 +484,6 @@ void ugrid(int seeds, Stat &S) {
         if (!seen[i]) {
           if (++S.missed <= 10)
             std::printf("MISS ugrid seed %d line %d sphere %d disc0 %d\n", seed, li, i, (int)disc0);
-        }
-        if (!seen2[i]) {
-          if (++S.missed <= 10)
-            std::printf("MISS ugrid pieces seed %d line %d sphere %d disc0 %d\n", seed, li, i, (int)disc0);
         }
       }
     }

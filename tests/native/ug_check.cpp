@@ -11,12 +11,9 @@
 // by behind_cells.  Scenes whose listing margin does not cover the prefilter
 // margin are counted (the device does not use the grid for them).
 // grid_closest_line (the grid walk of the whole line, early exit) must give
-// find_intersection's (t, index) exactly, for the same lines, and so must its
-// cooperative form (behind_coop's pieces of the segment behind the origin,
-// behind_piece, 1-8 per line, then grid_ahead_line), whose pieces must also
-// hand every such backward sphere to the test.
+// find_intersection's (t, index) exactly, for the same lines.
 // argv: seeds, cells per listed sphere.  Prints "overflow cells <count>",
-// "closest <lines> hits <count> pieces <count> wrong <count>" and "checked <lines>
+// "closest <lines> hits <count> wrong <count>" and "checked <lines>
 // <near-tangent pairs> <exact disc0 pairs> scenes <used>/<built> cells/line
 // <mean> missed <count>".
 //   hipcc -O2 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I csrc -I include ug_check.cpp csrc/rt_bvh.cpp
@@ -66,7 +63,7 @@ int main(int argc, char **argv) {
   const int seeds = argc > 1 ? std::atoi(argv[1]) : 24;
   const double cps = argc > 2 ? std::atof(argv[2]) : 2.0;  // cells per listed sphere (build_ugrid)
   long overflow = 0;  // cells with more than four entries (their lists continue in the overflow list)
-  long lines = 0, near = 0, exact0 = 0, missed = 0, built = 0, used = 0, wrong = 0, hits = 0, pieces = 0;
+  long lines = 0, near = 0, exact0 = 0, missed = 0, built = 0, used = 0, wrong = 0, hits = 0;
   double cells = 0.0;
   for (int seed = 0; seed < seeds; seed++) {
     std::mt19937_64 rng(9100 + seed);
@@ -146,7 +143,7 @@ int main(int argc, char **argv) {
                         (float)(1e-4 * (double)ug.extent)};
     for (size_t c = 0; c + 1 < ug.start.size(); c++) overflow += ug.start[c + 1] - ug.start[c] > 4;
     bv.tf_min = 0.0f;
-    std::vector<char> seen(N), seen2(N);
+    std::vector<char> seen(N);
     const double tol = 1e-7 * diam;
     for (int li = 0; li < 4000; li++) {
       V o, d;
@@ -193,38 +190,6 @@ int main(int argc, char **argv) {
             std::printf("WRONG scene %d line %d grid (%d, %.17g) reference (%d, %.17g)\n", seed, li, bi, bt, ri, rt);
         }
         hits += ri >= 0;
-        // the cooperative form (behind_coop + grid_ahead_line): the segment
-        // behind the origin in mo pieces, each walked alone, then the rest
-        const int mo = 1 + li % 8;
-        double ct = 1e20;
-        int ci = -1;
-        auto cfold = [&](int i) {
-          double t;
-          seen2[i] = 1;
-          if (ref_test(C[i], R[i], o, d, t) && (t < ct || (t == ct && i < ci))) {
-            ct = t;
-            ci = i;
-          }
-        };
-        std::fill(seen2.begin(), seen2.end(), 0);
-        const D3 O{o.x, o.y, o.z}, Dd{d.x, d.y, d.z};
-        const rtk::GridRay gr = rtk::grid_ray<true>(bv, O, Dd);
-        if (gr.s0 < std::fmin(gr.s1, 0.0f)) {
-          for (int k = 0; k < mo; k++) {
-            float sa, sb;
-            rtk::behind_piece(bv, gr, k, mo, sa, sb);
-            rtk::Work w3;
-            rtk::grid_walk<true, false, false>(bv, gr, sa, sb, w3, cfold, [] { return 0.0; });
-          }
-          pieces += mo;
-        }
-        rtk::Work w4;
-        rtk::grid_ahead_line(bv, O, Dd, w4, cfold, [&] { return ct; });
-        if (ci != ri || (ri >= 0 && ct != rt)) {
-          if (++wrong <= 10)
-            std::printf("WRONG pieces scene %d line %d grid (%d, %.17g) reference (%d, %.17g)\n", seed, li, ci, ct,
-                        ri, rt);
-        }
       }
       for (int i = 0; i < N; i++) {
         // long double geometry: distance of the line to the centre, the foot point's t
@@ -245,14 +210,11 @@ int main(int argc, char **argv) {
             std::printf("MISS scene %d line %d sphere %d r %.17g dist-r %.3Lg t %.6Lg disc0 %d\n", seed, li, i, R[i],
                         dist - std::fabs((long double)R[i]), tf, (int)disc0);
         }
-        if (!seen2[i]) {
-          if (++missed <= 10) std::printf("MISS pieces scene %d line %d sphere %d disc0 %d\n", seed, li, i, (int)disc0);
-        }
       }
     }
   }
   std::printf("overflow cells %ld\n", overflow);
-  std::printf("closest %ld hits %ld pieces %ld wrong %ld\n", lines, hits, pieces, wrong);
+  std::printf("closest %ld hits %ld wrong %ld\n", lines, hits, wrong);
   std::printf("checked %ld %ld %ld scenes %ld/%ld cells/line %.1f missed %ld\n", lines, near, exact0, used, built,
               cells / (double)(lines ? lines : 1), missed);
   return (missed || wrong) ? 2 : 0;
