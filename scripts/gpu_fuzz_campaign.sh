@@ -1,11 +1,19 @@
 # A long randomised parity campaign on the final tree (new seeds, every
-# generator): scripts/gpu_fuzz.py phases of $SECS seconds each; stops at the
+# generator; SET=2: large images and the bounds-checked build): scripts/gpu_fuzz.py
+# phases of $SECS seconds each; stops at the
 # first mismatch (the scene goes to gpurun_out/fuzz_mismatch.txt).
 set -o pipefail
 OUT=gpurun_out/fuzz_campaign; mkdir -p $OUT; export TMPDIR=/tmp
 SECS=${SECS:-240}; B=${SEED_BASE:-5100}
 run() { name=$1; shift; timeout -k 10 $((SECS + 60)) env "$@" python -u scripts/gpu_fuzz.py $SECS $((B + ${#name})) > $OUT/$name.log 2>&1 || { tail -5 $OUT/$name.log; exit 1; }; echo "$name: $(tail -1 $OUT/$name.log)"; }
-run general FUZZ_X=0
-run near_lights FUZZ_NEAR_LIGHTS=1
-run margin FUZZ_MARGIN=1
-run margin_camgrid FUZZ_MARGIN=1 RT_HIP_CAM_GRID=2
+if [ "${SET:-1}" = 1 ]; then
+  run general FUZZ_X=0
+  run near_lights FUZZ_NEAR_LIGHTS=1
+  run margin FUZZ_MARGIN=1
+  run margin_camgrid FUZZ_MARGIN=1 RT_HIP_CAM_GRID=2
+else  # images of 1,024+ tiles (tile order, launch tails, deferral shards) and the bounds-checked build
+  run large_general FUZZ_LARGE=1
+  run large_near_lights FUZZ_LARGE=1 FUZZ_NEAR_LIGHTS=1
+  run checked_margin FUZZ_MARGIN=1 FUZZ_VARIANT=check
+  run checked_general FUZZ_VARIANT=check
+fi
