@@ -185,14 +185,16 @@ int rt_upload_scene(rt_ctx *ctx, const rt_scene *scene);
 int rt_render(rt_ctx *ctx, const rt_camera *cam, int width, int height, int depth, const rt_rows *rows,
               uint8_t *rgb_out, int out_on_device, rt_stats *stats);
 /* Asynchronous render into DEVICE memory on the context's stream.  The kernels
- * are only enqueued, but two host-side builds can happen inside the call and
- * then wait for the context's stream first (work in flight may still read the
+ * are only enqueued, but host-side work can happen inside the call and then
+ * wait for the context's stream first (work in flight may still read the
  * buffer being replaced):
  *   - the tile launch order (rt_sched), rebuilt when the view, the image or
- *     shard geometry or the scene changed since the previous launch (~1 ms);
- *   - the camera grid (closest hits of camera rays), built per camera position
- *     for a launch of >= 8 frames sharing one position or a position repeated
- *     from the previous launch (50-180 ms; a moving camera never builds one).
+ *     shard geometry or the scene changed since the previous launch (~0.1 ms);
+ *   - the camera grid's cube-map tables and buffers, the first time a grid
+ *     size is used.  The camera grids themselves (closest hits of camera rays)
+ *     are built on the device ahead of the render kernel, per camera position,
+ *     for a multi-frame launch (one grid per distinct position) or a one-frame
+ *     launch at the previous launch's position (~0.05 ms, cached).
  * rt_get_info() reports both.  rt_render_stats() waits for the stream and
  * returns the stats of the most recent rt_render_async. */
 int rt_render_async(rt_ctx *ctx, const rt_camera *cam, int width, int height, int depth, const rt_rows *rows,
