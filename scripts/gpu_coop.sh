@@ -1,3 +1,5 @@
+# Historical record (profiles/r7t): the A/B of the cooperative backward walk,
+# commit d3980a4, reverted after it; variants/exp/ held the previous library.
 # The wave-cooperative backward walk (kFastGrid kernels): parity on the scenes
 # above 1,024 spheres (goldens, tangent scenes, fuzz), then cfg 5 and synth200
 # against the previous library, alternating.
