@@ -1,5 +1,6 @@
 # A long randomised parity campaign on the final tree (new seeds, every
-# generator; SET=2: large images and the bounds-checked build): scripts/gpu_fuzz.py
+# generator; SET=2: large images and the bounds-checked build; SET=3: the
+# product's environment knobs): scripts/gpu_fuzz.py
 # phases of $SECS seconds each; stops at the
 # first mismatch (the scene goes to gpurun_out/fuzz_mismatch.txt).
 set -o pipefail
@@ -11,9 +12,14 @@ if [ "${SET:-1}" = 1 ]; then
   run near_lights FUZZ_NEAR_LIGHTS=1
   run margin FUZZ_MARGIN=1
   run margin_camgrid FUZZ_MARGIN=1 RT_HIP_CAM_GRID=2
-else  # images of 1,024+ tiles (tile order, launch tails, deferral shards) and the bounds-checked build
+elif [ "$SET" = 2 ]; then  # images of 1,024+ tiles (tile order, launch tails, deferral shards) and the bounds-checked build
   run large_general FUZZ_LARGE=1
   run large_near_lights FUZZ_LARGE=1 FUZZ_NEAR_LIGHTS=1
   run checked_margin FUZZ_MARGIN=1 FUZZ_VARIANT=check
   run checked_general FUZZ_VARIANT=check
+else  # the product library's two environment knobs: the LDS-staged scene, the camera grid off / every launch
+  run lds_general RT_HIP_LDS_SCENE=1
+  run lds_margin FUZZ_MARGIN=1 RT_HIP_LDS_SCENE=1
+  run camgrid0_near FUZZ_NEAR_LIGHTS=1 RT_HIP_CAM_GRID=0
+  run camgrid2_general RT_HIP_CAM_GRID=2
 fi
